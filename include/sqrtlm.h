@@ -1,0 +1,155 @@
+/*
+ * sqrtlm.h — C ABI of the MI355X square-root Levenberg–Marquardt
+ * bundle-adjustment backend (libsqrtlm.so).
+ *
+ * Drop-in seam: the reference dispatches every BA call through the static
+ * façade `Optimizer` (include/backend/Optimizer.h:42-71, solver switch
+ * src/backend/Optimizer.cc:26-28) into `g2oOptimizer`, which assembles a g2o
+ * graph and calls `SparseOptimizer::optimize`. A host adapter (see
+ * INTEGRATION.md) replaces that g2o graph with the plain arrays below and
+ * calls this library instead; the Tracking / LocalMapping / LoopClosing
+ * threads are untouched.
+ *
+ * Conventions (all mirror the g2o path):
+ *   - poses are T_cw as SE3Quat: q = (qx,qy,qz,qw) unit, qw >= 0, t (3);
+ *     tangent order [omega; upsilon], left update T <- exp(d) T
+ *     (Thirdparty/g2o/g2o/types/types_six_dof_expmap.h:73-76);
+ *   - observations are EdgeSE3ProjectXYZ in insertion order (edge id = index);
+ *     error = obs - project(T X) (types_six_dof_expmap.h:90-95);
+ *     information = I * info; Huber delta per edge, 0 = no robust kernel;
+ *   - every call is FP64 end to end.
+ * Error model: every entry point returns an int status (SQLM_OK = 0, < 0 on
+ * error); nothing throws across the ABI. A non-SPD damped system is NOT an
+ * error: the LM step is rejected, as g2o does (levenberg.cpp:126-127).
+ * Threading: one context per calling thread (LBA, loop-closing and GBA threads
+ * may each own one); a context owns its HIP stream and device memory.
+ */
+#ifndef SQRTLM_H
+#define SQRTLM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SQLM_OK 0
+#define SQLM_ERR_INVALID_ARG (-1)
+#define SQLM_ERR_HIP (-2)
+#define SQLM_ERR_NOT_SPD (-3)
+#define SQLM_ERR_OOM (-4)
+#define SQLM_ERR_ABORTED (-5)
+#define SQLM_ERR_NO_DEVICE (-6)
+#define SQLM_ERR_STATE (-7)
+#define SQLM_ERR_UNSUPPORTED (-8)
+#define SQLM_ERR_COMM (-9)
+
+#define SQLM_TRACE_MAX 256
+
+typedef struct sqlm_ctx sqlm_ctx;
+
+/* Per optimize() statistics; field meaning follows g2o's loop
+ * (sparse_optimizer.cpp:354-419, optimization_algorithm_levenberg.cpp:61-164). */
+typedef struct sqlm_stats {
+  int iterations;     /* value SparseOptimizer::optimize returns               */
+  int trials;         /* inner LM trials, all iterations                         */
+  int result;         /* last SolverResult: 0 OK, 1 Terminate, 2 Fail          */
+  int n_active_edges;
+  double chi2_begin;  /* robust chi2 at the start of iteration 0               */
+  double chi2_end;    /* currentChi after the last iteration                   */
+  double lambda_end;
+  int trace_len;
+  double trace_chi2[SQLM_TRACE_MAX];
+  double trace_lambda[SQLM_TRACE_MAX];
+  int trace_trials[SQLM_TRACE_MAX];
+  /* wall time split (ms, host clock around stream syncs) */
+  double ms_total, ms_setup, ms_linearize, ms_trials;
+} sqlm_stats;
+
+const char *sqlm_version(void);
+const char *sqlm_status_string(int status);
+
+/* Context / device. Replaces `new g2o::SparseOptimizer` + solver setup
+ * (g2oOptimizer.cc:784-798). device_id < 0 picks the current HIP device. */
+int sqlm_ctx_create(int device_id, sqlm_ctx **out);
+int sqlm_ctx_destroy(sqlm_ctx *ctx);
+
+/* Graph assembly: replaces the addVertex/addEdge loops of
+ * g2oOptimizer::LocalBundleAdjustment (g2oOptimizer.cc:805-912) and
+ * ::BundleAdjustment (:142-296). Arrays are copied (caller keeps ownership).
+ *   pose_q [n_pose][4], pose_t [n_pose][3], pose_fixed [n_pose], intr [n_pose][4]
+ *   pt [n_pt][3]
+ *   obs_pose/obs_pt [n_obs], obs_uv [n_obs][2], obs_info [n_obs] (invSigma2),
+ *   obs_delta [n_obs] Huber delta (0 = none; NULL = none), obs_level [n_obs] (NULL = 0). */
+int sqlm_set_problem(sqlm_ctx *ctx, int n_pose, const double *pose_q, const double *pose_t,
+                     const uint8_t *pose_fixed, const double *intr, int n_pt, const double *pt,
+                     int64_t n_obs, const int32_t *obs_pose, const int32_t *obs_pt, const double *obs_uv,
+                     const double *obs_info, const double *obs_delta, const uint8_t *obs_level);
+
+/* EdgeLidarFlatPoint unary pose edges (types_six_dof_expmap.h:206-234), added
+ * after the mono edges (g2oOptimizer.cc:1062-1070). Level 0, no kernel. */
+int sqlm_set_lidar(sqlm_ctx *ctx, int64_t n, const int32_t *pose, const double *p_cam,
+                   const double *p_world, const double *normal, const double *info);
+
+/* e->setLevel / e->setRobustKernel for every mono edge (NULL delta = none). */
+int sqlm_set_edge_level(sqlm_ctx *ctx, const uint8_t *level);
+int sqlm_set_robust(sqlm_ctx *ctx, const double *delta);
+int sqlm_set_lidar_level(sqlm_ctx *ctx, const uint8_t *level);
+
+/* optimizer.initializeOptimization(level); optimizer.optimize(iterations).
+ * user_lambda > 0 mirrors setUserLambdaInit. stop mirrors setForceStopFlag
+ * (polled before each iteration and each trial; may be NULL).
+ * *n_iter receives optimize()'s return value. */
+int sqlm_optimize(sqlm_ctx *ctx, int level, int iterations, double user_lambda,
+                  const volatile uint8_t *stop, sqlm_stats *stats, int *n_iter);
+
+/* The whole g2oOptimizer::LocalBundleAdjustment schedule on the set problem
+ * (g2oOptimizer.cc:923-1136): pass 1 optimize(5) with the set Huber kernels;
+ * unless stopped, tag chi2 > 5.991 || depth <= 0 edges to level 1, drop the
+ * kernels, pass 2 optimize(10); pass 3 optimize(20) with the LiDAR edges;
+ * outlier[n_obs] receives the final erase tags. *ran = 0 when the stop flag
+ * was already set (the reference returns before pass 1). */
+int sqlm_local_ba(sqlm_ctx *ctx, const volatile uint8_t *stop, uint8_t *outlier,
+                  sqlm_stats stats[3], int *ran);
+
+/* g2oOptimizer::BundleAdjustment core (g2oOptimizer.cc:299-301): optimize
+ * level 0 for `iterations`, kernels as set. */
+int sqlm_global_ba(sqlm_ctx *ctx, int iterations, const volatile uint8_t *stop, sqlm_stats *stats,
+                   int *n_iter);
+
+/* Results (write-back inputs, g2oOptimizer.cc:1167-1189, :306-360). */
+int sqlm_get_poses(sqlm_ctx *ctx, double *pose_q, double *pose_t);
+int sqlm_get_points(sqlm_ctx *ctx, double *pt);
+/* e->chi2() from the last computed error (g2o semantics: may belong to a
+ * rejected trial, and level-1 edges keep their pass-1 value). */
+int sqlm_get_edge_chi2(sqlm_ctx *ctx, double *chi2);
+/* e->isDepthPositive() evaluated at the current estimate. */
+int sqlm_get_edge_depth_positive(sqlm_ctx *ctx, uint8_t *positive);
+int sqlm_get_edge_level(sqlm_ctx *ctx, uint8_t *level);
+
+/* Converter::toSE3Quat / toCvMat(SE3Quat) (src/utils/Converter.cc:55-79,98-109):
+ * float32 row-major 4x4 T_cw <-> (q, t). */
+void sqlm_pose_from_Tcw_f32(const float T[16], double q[4], double t[3]);
+void sqlm_pose_to_Tcw_f32(const double q[4], const double t[3], float T[16]);
+
+/* Multi-GPU: landmark-sharded global BA, one context per rank. Each rank
+ * calls sqlm_set_problem with ALL poses and ITS landmarks/observations; the
+ * reduced camera system, gradient and scalars are summed over RCCL (xGMI).
+ * Rank 0 creates the id; the caller broadcasts it (e.g. torch.distributed). */
+int sqlm_comm_id_size(void);
+int sqlm_comm_get_unique_id(char *id_out);
+int sqlm_ctx_set_comm(sqlm_ctx *ctx, const char *unique_id, int rank, int nranks);
+
+/* Device-resident benchmarking hooks: time `n` LM iterations on the set
+ * problem with data already in HBM (bench.py). Per-kernel averaged durations
+ * (HIP events on the context stream) are returned through kernel_ms
+ * [SQLM_NKERNEL_TIMERS] when non-NULL. */
+#define SQLM_NKERNEL_TIMERS 8
+int sqlm_bench_iterations(sqlm_ctx *ctx, int warmup, int n, double *ms_per_iter, double *kernel_ms,
+                          sqlm_stats *stats);
+const char *sqlm_kernel_timer_name(int i);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

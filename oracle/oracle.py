@@ -1,0 +1,177 @@
+"""TEST INFRASTRUCTURE — ctypes binding of the CPU oracle (oracle/g2o_ref.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module, and only as the checker / CPU baseline. PARITY UNPINNED: see
+oracle/oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+TRACE_MAX = 256
+
+
+class OrcGraph(C.Structure):
+    _fields_ = [
+        ("n_pose", C.c_int), ("pose_q", C.c_void_p), ("pose_t", C.c_void_p), ("pose_fixed", C.c_void_p),
+        ("intr", C.c_void_p), ("n_pt", C.c_int), ("pt", C.c_void_p), ("n_obs", C.c_int64),
+        ("obs_pose", C.c_void_p), ("obs_pt", C.c_void_p), ("obs_uv", C.c_void_p), ("obs_info", C.c_void_p),
+        ("obs_delta", C.c_void_p), ("obs_level", C.c_void_p), ("obs_err", C.c_void_p), ("n_lid", C.c_int64),
+        ("lid_pose", C.c_void_p), ("lid_pc", C.c_void_p), ("lid_pw", C.c_void_p), ("lid_n", C.c_void_p),
+        ("lid_info", C.c_void_p), ("lid_level", C.c_void_p), ("lid_err", C.c_void_p),
+    ]
+
+
+class OrcStats(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_int), ("trials", C.c_int), ("result", C.c_int), ("n_active_edges", C.c_int),
+        ("chi2_begin", C.c_double), ("chi2_end", C.c_double), ("lambda_end", C.c_double),
+        ("trace_len", C.c_int), ("trace_chi2", C.c_double * TRACE_MAX),
+        ("trace_lambda", C.c_double * TRACE_MAX), ("trace_trials", C.c_int * TRACE_MAX),
+    ]
+
+    def as_dict(self) -> dict:
+        n = self.trace_len
+        return dict(iterations=self.iterations, trials=self.trials, result=self.result,
+                    n_active_edges=self.n_active_edges, chi2_begin=self.chi2_begin,
+                    chi2_end=self.chi2_end, lambda_end=self.lambda_end,
+                    trace_chi2=list(self.trace_chi2[:n]), trace_lambda=list(self.trace_lambda[:n]),
+                    trace_trials=list(self.trace_trials[:n]))
+
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = C.CDLL(_LIB_PATH)
+        _lib.orc_optimize.restype = C.c_int
+        _lib.orc_local_ba.restype = C.c_int
+        _lib.orc_global_ba.restype = C.c_int
+        _lib.orc_lidar_error.restype = C.c_double
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class OracleGraph:
+    """Owns numpy copies of a BAProblem and the orc_graph view over them."""
+
+    def __init__(self, prob):
+        self.pose_q = prob.pose_q.copy()
+        self.pose_t = prob.pose_t.copy()
+        self.pose_fixed = prob.pose_fixed.copy()
+        self.intr = prob.intr.copy()
+        self.pt = prob.pt.copy()
+        self.obs_pose = prob.obs_pose.copy()
+        self.obs_pt = prob.obs_pt.copy()
+        self.obs_uv = prob.obs_uv.copy()
+        self.obs_info = prob.obs_info.copy()
+        self.obs_delta = prob.obs_delta.copy()
+        self.obs_level = prob.obs_level.copy()
+        self.obs_err = np.zeros((prob.n_obs, 2))
+        self.lid_pose = prob.lid_pose.copy()
+        self.lid_pc = prob.lid_pc.copy()
+        self.lid_pw = prob.lid_pw.copy()
+        self.lid_n = prob.lid_n.copy()
+        self.lid_info = prob.lid_info.copy()
+        self.lid_level = np.zeros(prob.n_lid, np.uint8)
+        self.lid_err = np.zeros(prob.n_lid)
+        g = OrcGraph()
+        g.n_pose, g.n_pt, g.n_obs, g.n_lid = prob.n_pose, prob.n_pt, prob.n_obs, prob.n_lid
+        for name in ("pose_q", "pose_t", "pose_fixed", "intr", "pt", "obs_pose", "obs_pt", "obs_uv",
+                     "obs_info", "obs_delta", "obs_level", "obs_err", "lid_pose", "lid_pc", "lid_pw",
+                     "lid_n", "lid_info", "lid_level", "lid_err"):
+            setattr(g, name, _p(getattr(self, name)))
+        self.g = g
+
+    def optimize(self, level=0, iterations=10, user_lambda=0.0, stop=None):
+        st = OrcStats()
+        n = lib().orc_optimize(C.byref(self.g), level, iterations, C.c_double(user_lambda),
+                               _p(stop), C.byref(st))
+        return n, st.as_dict()
+
+    def local_ba(self, stop=None):
+        st = (OrcStats * 3)()
+        outl = np.zeros(self.obs_pose.shape[0], np.uint8)
+        ran = lib().orc_local_ba(C.byref(self.g), _p(stop), _p(outl), st)
+        return ran, outl, [s.as_dict() for s in st]
+
+    def global_ba(self, iterations=10, stop=None):
+        st = OrcStats()
+        n = lib().orc_global_ba(C.byref(self.g), iterations, _p(stop), C.byref(st))
+        return n, st.as_dict()
+
+    def edge_chi2(self):
+        out = np.zeros(self.obs_pose.shape[0])
+        lib().orc_edge_chi2(C.byref(self.g), _p(out))
+        return out
+
+    def depth_positive(self):
+        out = np.zeros(self.obs_pose.shape[0], np.uint8)
+        lib().orc_depth_positive(C.byref(self.g), _p(out))
+        return out
+
+    def compute_errors(self):
+        lib().orc_compute_mono_errors(C.byref(self.g))
+        return self.obs_err
+
+
+def se3_exp(upd):
+    q, t = np.zeros(4), np.zeros(3)
+    lib().orc_se3_exp(_p(np.ascontiguousarray(upd, np.float64)), _p(q), _p(t))
+    return q, t
+
+
+def se3_oplus(q, t, d):
+    q = np.array(q, np.float64); t = np.array(t, np.float64)
+    lib().orc_se3_oplus(_p(q), _p(t), _p(np.ascontiguousarray(d, np.float64)))
+    return q, t
+
+
+def mono_jacobians(q, t, intr, X):
+    Jl, Jp = np.zeros(6), np.zeros(12)
+    f = lambda a: _p(np.ascontiguousarray(a, np.float64))
+    lib().orc_mono_jacobians(f(q), f(t), f(intr), f(X), _p(Jl), _p(Jp))
+    return Jl.reshape(2, 3), Jp.reshape(2, 6)
+
+
+def lidar_error(q, t, pc, pw, n):
+    f = lambda a: _p(np.ascontiguousarray(a, np.float64))
+    return lib().orc_lidar_error(f(q), f(t), f(pc), f(pw), f(n))
+
+
+def lidar_jacobian(q, t, pc, pw, n):
+    J = np.zeros(6)
+    f = lambda a: _p(np.ascontiguousarray(a, np.float64))
+    lib().orc_lidar_jacobian(f(q), f(t), f(pc), f(pw), f(n), _p(J))
+    return J
+
+
+def se3_from_Tcw_f32(T):
+    q, t = np.zeros(4), np.zeros(3)
+    lib().orc_se3_from_Tcw_f32(_p(np.ascontiguousarray(T, np.float32)), _p(q), _p(t))
+    return q, t
+
+
+def se3_to_Tcw_f32(q, t):
+    T = np.zeros(16, np.float32)
+    f = lambda a: _p(np.ascontiguousarray(a, np.float64))
+    lib().orc_se3_to_Tcw_f32(f(q), f(t), _p(T))
+    return T.reshape(4, 4)

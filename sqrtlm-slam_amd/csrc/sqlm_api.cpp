@@ -1,0 +1,834 @@
+// sqlm_api.cpp — C ABI (include/sqrtlm.h) and host LM driver.
+//
+// The host side owns only control: it mirrors g2o's Levenberg–Marquardt loop
+// decision for decision (optimization_algorithm_levenberg.cpp:61-164,
+// sparse_optimizer.cpp:354-419) and keeps every array in HBM; one small
+// device->host copy of the reduced scalars per LM trial is the only sync.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <new>
+#include <vector>
+
+#include "../../include/sqrtlm.h"
+#include "se3_dev.h"
+#include "sqlm_comm.h"
+#include "sqlm_internal.h"
+
+using namespace sqlm;
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+struct Timer {
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  double ms() const {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+};
+
+const char *kTimerNames[SQLM_NKERNEL_TIMERS] = {"k_linearize", "k_camera_pass", "k_damp", "k_rcs",
+                                                "k_solve", "k_pose_update", "k_landmark_update", "reduce+sync"};
+
+}  // namespace
+
+struct sqlm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // ---- host copy of the graph (caller order) ----
+  bool has_problem = false;
+  int n_pose = 0, n_pt = 0;
+  int64_t n_obs = 0, n_lid = 0;
+  std::vector<double> pose_q, pose_t, intr, pt;
+  std::vector<uint8_t> pose_fixed;
+  std::vector<int32_t> obs_pose, obs_pt;
+  std::vector<double> obs_uv, obs_info, obs_delta, obs_err;
+  std::vector<uint8_t> obs_level;
+  std::vector<int32_t> lid_pose;
+  std::vector<double> lid_pc, lid_pw, lid_n, lid_info, lid_err;
+  std::vector<uint8_t> lid_level;
+  // ---- structure of the current optimize() call ----
+  DevProblem d;
+  std::vector<Bucket> buckets;
+  std::vector<int> bucket_part_off;
+  int n_lm_parts = 0;
+  std::vector<int> slot_pt;          // device slot -> point id
+  std::vector<int64_t> dev_edge;     // device obs -> edge id
+  std::vector<int64_t> dev_lid_edge; // device lidar -> lidar edge id
+  int max_row_blocks = 0;
+  int n_active_edges = 0;
+  // ---- device memory ----
+  std::vector<DevBuf> bufs;
+  double *h_scalars = nullptr;  // pinned
+  // ---- comm ----
+  Comm comm;
+  // ---- timing ----
+  hipEvent_t ev[2 * SQLM_NKERNEL_TIMERS] = {};
+  bool timing = false;
+  double kernel_ms_acc[SQLM_NKERNEL_TIMERS] = {};
+  int kernel_ms_n = 0;
+};
+
+#define HIP_OK(x)                          \
+  do {                                     \
+    if ((x) != hipSuccess) return SQLM_ERR_HIP; \
+  } while (0)
+
+namespace {
+
+template <class T>
+int ensure(sqlm_ctx *c, int idx, size_t n, T **out) {
+  if ((int)c->bufs.size() <= idx) c->bufs.resize(idx + 1);
+  DevBuf &b = c->bufs[idx];
+  size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  bytes = (bytes + 255) & ~size_t(255);
+  if (b.cap < bytes) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) return SQLM_ERR_OOM;
+    b.cap = bytes;
+  }
+  *out = static_cast<T *>(b.p);
+  return SQLM_OK;
+}
+
+template <class T>
+int upload(sqlm_ctx *c, int idx, const std::vector<T> &v, T **out) {
+  int s = ensure(c, idx, v.size(), out);
+  if (s) return s;
+  if (!v.empty()) HIP_OK(hipMemcpyAsync(*out, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return SQLM_OK;
+}
+
+enum BufId {
+  B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
+  B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS,
+  B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
+  B_SCAL, B_MAXD, B_FLAGS
+};
+
+inline int seg_width(int k) {
+  int w = 2;
+  while (w < k && w < 64) w <<= 1;
+  return w;
+}
+
+inline bool stopped(const volatile uint8_t *s) { return s && *s; }
+
+// initializeOptimization(level) + BlockSolver::buildStructure: active set,
+// index mapping (free poses by id, then points), landmark-sorted buckets,
+// camera CSR and the upper block pattern of the reduced camera system.
+int prepare(sqlm_ctx *c, int level) {
+  DevProblem &d = c->d;
+  std::vector<uint8_t> pose_act(c->n_pose, 0), pt_act(c->n_pt, 0);
+  std::vector<int> kcount(c->n_pt, 0);
+  int64_t n_ae = 0;
+  for (int64_t e = 0; e < c->n_obs; ++e) {
+    if (c->obs_level[e] != level) continue;
+    pose_act[c->obs_pose[e]] = 1;
+    pt_act[c->obs_pt[e]] = 1;
+    kcount[c->obs_pt[e]]++;
+    ++n_ae;
+  }
+  std::vector<int64_t> lid_act;
+  for (int64_t e = 0; e < c->n_lid; ++e) {
+    if (c->lid_level[e] != level || c->pose_fixed[c->lid_pose[e]]) continue;
+    lid_act.push_back(e);
+    pose_act[c->lid_pose[e]] = 1;
+  }
+  c->n_active_edges = (int)(n_ae + (int64_t)lid_act.size());
+  std::vector<int> phidx(c->n_pose, -1), hidxp;
+  for (int p = 0; p < c->n_pose; ++p)
+    if (pose_act[p] && !c->pose_fixed[p]) { phidx[p] = (int)hidxp.size(); hidxp.push_back(p); }
+  const int nP = (int)hidxp.size();
+  if (nP > kMaxFreePoses) return SQLM_ERR_UNSUPPORTED;
+  // landmark slots: bucket by segment width, point-id order inside a bucket
+  std::vector<int> pts;
+  for (int l = 0; l < c->n_pt; ++l)
+    if (pt_act[l]) pts.push_back(l);
+  std::stable_sort(pts.begin(), pts.end(),
+                   [&](int a, int b) { return seg_width(kcount[a]) < seg_width(kcount[b]); });
+  const int nL = (int)pts.size();
+  if (nP + nL == 0) return SQLM_ERR_STATE;  // "0 vertices to optimize"
+  std::vector<int> pt_slot(c->n_pt, -1);
+  for (int s = 0; s < nL; ++s) pt_slot[pts[s]] = s;
+  c->slot_pt = pts;
+  c->buckets.clear();
+  c->bucket_part_off.clear();
+  c->n_lm_parts = 0;
+  for (int s = 0; s < nL;) {
+    const int W = seg_width(kcount[pts[s]]);
+    int e = s;
+    while (e < nL && seg_width(kcount[pts[e]]) == W) ++e;
+    Bucket b{W, s, e};
+    c->buckets.push_back(b);
+    c->bucket_part_off.push_back(c->n_lm_parts);
+    c->n_lm_parts += linearize_blocks(b);
+    s = e;
+  }
+  if (c->n_lm_parts > 16384) return SQLM_ERR_UNSUPPORTED;
+  // observations in slot order (edge-id order inside a landmark)
+  std::vector<int> lm_begin(nL + 1, 0);
+  for (int s = 0; s < nL; ++s) lm_begin[s + 1] = lm_begin[s] + kcount[pts[s]];
+  const int64_t nE = lm_begin[nL];
+  if (nE > (int64_t)std::numeric_limits<int>::max()) return SQLM_ERR_UNSUPPORTED;
+  std::vector<int> fill(lm_begin.begin(), lm_begin.end() - 1);
+  c->dev_edge.assign(nE, 0);
+  std::vector<int> obs_lm(nE), obs_cam(nE), obs_camh(nE);
+  std::vector<double> obs_uv(2 * nE), obs_info(nE), obs_delta(nE);
+  for (int64_t e = 0; e < c->n_obs; ++e) {
+    if (c->obs_level[e] != level) continue;
+    const int s = pt_slot[c->obs_pt[e]];
+    const int o = fill[s]++;
+    c->dev_edge[o] = e;
+    obs_lm[o] = s;
+    obs_cam[o] = c->obs_pose[e];
+    obs_camh[o] = phidx[c->obs_pose[e]];
+    obs_uv[2 * o] = c->obs_uv[2 * e];
+    obs_uv[2 * o + 1] = c->obs_uv[2 * e + 1];
+    obs_info[o] = c->obs_info[e];
+    obs_delta[o] = c->obs_delta[e];
+  }
+  // camera CSR (device obs in slot order)
+  std::vector<int> cam_ptr(nP + 1, 0), cam_obs;
+  for (int64_t o = 0; o < nE; ++o)
+    if (obs_camh[o] >= 0) cam_ptr[obs_camh[o] + 1]++;
+  for (int i = 0; i < nP; ++i) cam_ptr[i + 1] += cam_ptr[i];
+  cam_obs.resize(cam_ptr[nP]);
+  {
+    std::vector<int> f(cam_ptr.begin(), cam_ptr.end() - 1);
+    for (int64_t o = 0; o < nE; ++o)
+      if (obs_camh[o] >= 0) cam_obs[f[obs_camh[o]]++] = (int)o;
+  }
+  // reduced-camera-system pattern (upper, diagonal first)
+  std::vector<int> s_row(nP + 1, 0), s_col;
+  {
+    std::vector<int> mark(nP, -1), row;
+    std::vector<std::vector<int>> rows(nP);
+    for (int i = 0; i < nP; ++i) {
+      row.clear();
+      row.push_back(i);
+      mark[i] = i;
+      for (int t = cam_ptr[i]; t < cam_ptr[i + 1]; ++t) {
+        const int s = obs_lm[cam_obs[t]];
+        for (int o = lm_begin[s]; o < lm_begin[s + 1]; ++o) {
+          const int j = obs_camh[o];
+          if (j > i && mark[j] != i) { mark[j] = i; row.push_back(j); }
+        }
+      }
+      std::sort(row.begin() + 1, row.end());
+      rows[i] = row;
+    }
+    for (int i = 0; i < nP; ++i) s_row[i + 1] = s_row[i] + (int)rows[i].size();
+    s_col.resize(s_row[nP]);
+    int mx = 0;
+    for (int i = 0; i < nP; ++i) {
+      std::copy(rows[i].begin(), rows[i].end(), s_col.begin() + s_row[i]);
+      mx = std::max(mx, (int)rows[i].size());
+    }
+    c->max_row_blocks = mx;
+  }
+  if (c->max_row_blocks > 128) return SQLM_ERR_UNSUPPORTED;
+  // lidar edges grouped by free camera
+  std::vector<int> lid_ptr(nP + 1, 0), lid_pose;
+  std::vector<double> lid_data;
+  {
+    std::vector<std::vector<int64_t>> per(nP);
+    for (int64_t e : lid_act) per[phidx[c->lid_pose[e]]].push_back(e);
+    c->dev_lid_edge.clear();
+    for (int i = 0; i < nP; ++i) {
+      lid_ptr[i + 1] = lid_ptr[i] + (int)per[i].size();
+      for (int64_t e : per[i]) {
+        c->dev_lid_edge.push_back(e);
+        lid_pose.push_back(c->lid_pose[e]);
+        for (int k = 0; k < 3; ++k) lid_data.push_back(c->lid_pc[3 * e + k]);
+        for (int k = 0; k < 3; ++k) lid_data.push_back(c->lid_pw[3 * e + k]);
+        for (int k = 0; k < 3; ++k) lid_data.push_back(c->lid_n[3 * e + k]);
+        lid_data.push_back(c->lid_info[e]);
+        lid_data.push_back(0.0);
+        lid_data.push_back(0.0);
+      }
+    }
+  }
+  // ---------------- upload ----------------
+  d.n_pose = c->n_pose;
+  d.sharded = c->comm.enabled() ? 1 : 0;
+  d.rank = c->comm.rank;
+  d.nP = nP;
+  d.nL = nL;
+  d.nE = nE;
+  d.nLid = (int64_t)lid_act.size();
+  d.nnzb = s_row[nP];
+  std::vector<double> qt(8 * (size_t)c->n_pose, 0.0), X(4 * (size_t)nL, 0.0);
+  for (int p = 0; p < c->n_pose; ++p) {
+    for (int k = 0; k < 4; ++k) qt[8 * p + k] = c->pose_q[4 * p + k];
+    for (int k = 0; k < 3; ++k) qt[8 * p + 4 + k] = c->pose_t[3 * p + k];
+  }
+  for (int s = 0; s < nL; ++s)
+    for (int k = 0; k < 3; ++k) X[4 * s + k] = c->pt[3 * pts[s] + k];
+  int st = 0;
+#define UP(id, vec, ptr) \
+  if ((st = upload(c, id, vec, &ptr))) return st;
+#define AL(id, n, ptr) \
+  if ((st = ensure(c, id, n, &ptr))) return st;
+  UP(B_QT0, qt, d.pose_qt[0]);
+  UP(B_QT1, qt, d.pose_qt[1]);
+  AL(B_RT0, 16 * (size_t)c->n_pose, d.pose_rt[0]);
+  AL(B_RT1, 16 * (size_t)c->n_pose, d.pose_rt[1]);
+  UP(B_INTR, c->intr, d.intr);
+  UP(B_PHIDX, phidx, d.pose_hidx);
+  UP(B_HIDXP, hidxp, d.hidx_pose);
+  UP(B_X0, X, d.X[0]);
+  UP(B_X1, X, d.X[1]);
+  UP(B_LMBEG, lm_begin, d.lm_begin);
+  AL(B_LMR, 8 * (size_t)nL, d.lm_R);
+  AL(B_LMB, 4 * (size_t)nL, d.lm_b);
+  AL(B_LMM, 8 * (size_t)nL, d.lm_M);
+  AL(B_LMV, 4 * (size_t)nL, d.lm_v);
+  UP(B_OBSLM, obs_lm, d.obs_lm);
+  UP(B_OBSCAM, obs_cam, d.obs_cam);
+  UP(B_OBSCAMH, obs_camh, d.obs_camh);
+  UP(B_OBSUV, obs_uv, d.obs_uv);
+  UP(B_OBSINFO, obs_info, d.obs_info);
+  UP(B_OBSDELTA, obs_delta, d.obs_delta);
+  AL(B_OBSP, 18 * (size_t)nE, d.obs_P);
+  AL(B_OBSJP, 16 * (size_t)nE, d.obs_jp);
+  AL(B_OBSERR, 2 * (size_t)nE, d.obs_err);
+  UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
+  UP(B_CAMOBS, cam_obs, d.cam_obs);
+  AL(B_HPP, 36 * (size_t)nP, d.Hpp);
+  AL(B_BP, 8 * (size_t)nP, d.bp);
+  UP(B_LIDPTR, lid_ptr, d.lid_cam_ptr);
+  UP(B_LIDDATA, lid_data, d.lid_data);
+  UP(B_LIDPOSE, lid_pose, d.lid_pose);
+  AL(B_LIDERR, (size_t)d.nLid, d.lid_err);
+  UP(B_SROW, s_row, d.s_row_ptr);
+  UP(B_SCOL, s_col, d.s_col);
+  AL(B_S, 36 * (size_t)d.nnzb, d.S);
+  AL(B_G, 6 * (size_t)nP, d.g);
+  AL(B_DX, 6 * (size_t)nP, d.dx);
+  AL(B_DENSE, (size_t)6 * nP * 6 * nP, d.dense);
+  AL(B_PART, (size_t)kMaxPartials, d.partials);
+  AL(B_SCAL, (size_t)kNScalars, d.scalars);
+  AL(B_MAXD, 1, d.maxdiag);
+  AL(B_FLAGS, 4, d.flags);
+#undef UP
+#undef AL
+  HIP_OK(hipMemsetAsync(d.partials, 0, sizeof(double) * kMaxPartials, c->stream));
+  HIP_OK(hipMemsetAsync(d.obs_err, 0, sizeof(double) * 2 * std::max<int64_t>(nE, 1), c->stream));
+  launch_pose_prep(d, 0, c->stream);
+  return SQLM_OK;
+}
+
+void finish(sqlm_ctx *c) {
+  DevProblem &d = c->d;
+  std::vector<double> qt(8 * (size_t)c->n_pose), X(4 * (size_t)d.nL), err(2 * (size_t)d.nE), lerr(d.nLid);
+  (void)hipMemcpyAsync(qt.data(), d.pose_qt[0], qt.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  if (d.nL) (void)hipMemcpyAsync(X.data(), d.X[0], X.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  if (d.nE) (void)hipMemcpyAsync(err.data(), d.obs_err, err.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  if (d.nLid) (void)hipMemcpyAsync(lerr.data(), d.lid_err, lerr.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+  (void)hipStreamSynchronize(c->stream);
+  for (int p = 0; p < c->n_pose; ++p) {
+    for (int k = 0; k < 4; ++k) c->pose_q[4 * p + k] = qt[8 * p + k];
+    for (int k = 0; k < 3; ++k) c->pose_t[3 * p + k] = qt[8 * p + 4 + k];
+  }
+  for (int s = 0; s < d.nL; ++s)
+    for (int k = 0; k < 3; ++k) c->pt[3 * c->slot_pt[s] + k] = X[4 * s + k];
+  for (int64_t o = 0; o < d.nE; ++o) {
+    c->obs_err[2 * c->dev_edge[o]] = err[2 * o];
+    c->obs_err[2 * c->dev_edge[o] + 1] = err[2 * o + 1];
+  }
+  for (int64_t t = 0; t < d.nLid; ++t) c->lid_err[c->dev_lid_edge[t]] = lerr[t];
+}
+
+inline void tmark(sqlm_ctx *c, int i, bool end) {
+  if (c->timing) (void)hipEventRecord(c->ev[2 * i + (end ? 1 : 0)], c->stream);
+}
+
+// Add the elapsed times of timer pairs [i0, i1) (events already complete).
+void acc_events(sqlm_ctx *c, int i0, int i1) {
+  if (!c->timing) return;
+  for (int i = i0; i < i1; ++i) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev[2 * i], c->ev[2 * i + 1]) == hipSuccess) c->kernel_ms_acc[i] += ms;
+  }
+}
+
+// computeActiveErrors + buildSystem for the current state.
+int linearize(sqlm_ctx *c) {
+  DevProblem &d = c->d;
+  HIP_OK(hipMemsetAsync(d.maxdiag, 0, sizeof(unsigned long long), c->stream));
+  tmark(c, 0, false);
+  for (size_t b = 0; b < c->buckets.size(); ++b) launch_linearize(d, c->buckets[b], c->bucket_part_off[b], c->stream);
+  tmark(c, 0, true);
+  tmark(c, 1, false);
+  launch_camera_pass(d, c->stream);
+  if (c->comm.enabled()) {
+    if (comm_allreduce_hpp(c->comm, d, c->stream)) return SQLM_ERR_COMM;
+    launch_pose_maxdiag(d, c->stream);
+  }
+  tmark(c, 1, true);
+  return SQLM_OK;
+}
+
+struct TrialOut {
+  double chi_cur, chi_new, scale, maxdiag;
+  bool ok;
+};
+
+int reduce_and_fetch(sqlm_ctx *c, TrialOut &o) {
+  DevProblem &d = c->d;
+  launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream);
+  int s = comm_allreduce_scalars(c->comm, d.scalars, c->stream);
+  if (s) return s;
+  HIP_OK(hipMemcpyAsync(c->h_scalars, d.scalars, sizeof(double) * kNScalars, hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  o.chi_cur = c->h_scalars[kChiCur];
+  o.chi_new = c->h_scalars[kChiNew];
+  o.scale = c->h_scalars[kScale];
+  o.maxdiag = c->h_scalars[kMaxDiag];
+  o.ok = c->h_scalars[kSolveOk] > 0.5;
+  return SQLM_OK;
+}
+
+// setLambda + BlockSolver::solve + update + restoreDiagonal + computeActiveErrors.
+int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
+  DevProblem &d = c->d;
+  tmark(c, 2, false);
+  launch_damp(d, lambda, c->stream);
+  tmark(c, 2, true);
+  tmark(c, 3, false);
+  launch_rcs(d, lambda, c->max_row_blocks, c->stream);
+  tmark(c, 3, true);
+  int s = comm_allreduce_rcs(c->comm, d, lambda, c->stream);
+  if (s) return s;
+  tmark(c, 4, false);
+  s = launch_dense_solve(d, c->stream);
+  if (s) return s;
+  tmark(c, 4, true);
+  tmark(c, 5, false);
+  launch_pose_update(d, lambda, c->stream);
+  tmark(c, 5, true);
+  tmark(c, 6, false);
+  for (size_t b = 0; b < c->buckets.size(); ++b)
+    launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream);
+  launch_lidar_chi2(d, c->stream);
+  tmark(c, 6, true);
+  tmark(c, 7, false);
+  s = reduce_and_fetch(c, o);
+  tmark(c, 7, true);
+  acc_events(c, 2, SQLM_NKERNEL_TIMERS);
+  return s;
+}
+
+void swap_state(sqlm_ctx *c) {
+  std::swap(c->d.pose_qt[0], c->d.pose_qt[1]);
+  std::swap(c->d.pose_rt[0], c->d.pose_rt[1]);
+  std::swap(c->d.X[0], c->d.X[1]);
+}
+
+// The Levenberg–Marquardt loop of g2o (levenberg.cpp:61-164 inside
+// sparse_optimizer.cpp:376-414). `bench` keeps iterating after Terminate so a
+// fixed number of iterations can be timed.
+int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8_t *stop, sqlm_stats *st,
+           int *n_iter, bool bench) {
+  sqlm_stats local;
+  if (!st) st = &local;
+  std::memset(st, 0, sizeof(*st));
+  st->n_active_edges = c->n_active_edges;
+  double lambda = -1., ni = 2.;
+  int nbad = 0, its = 0, result = 0;
+  Timer tt;
+  for (int it = 0; it < iterations && !stopped(stop) && (result == 0 || bench); ++it) {
+    Timer tl;
+    int s = linearize(c);
+    if (s) return s;
+    double currentChi = 0.0;
+    if (it == 0) {
+      TrialOut o0{};
+      s = reduce_and_fetch(c, o0);
+      if (s) return s;
+      currentChi = o0.chi_cur;
+      st->chi2_begin = currentChi;
+      lambda = user_lambda > 0 ? user_lambda : 1e-5 * o0.maxdiag;
+      ni = 2;
+      nbad = 0;
+    }
+    st->ms_linearize += tl.ms();
+    Timer tr;
+    double iniChi = currentChi, tempChi = currentChi, rho = 0;
+    int qmax = 0;
+    do {
+      TrialOut o{};
+      s = trial(c, lambda, o);
+      if (s) return s;
+      if (qmax == 0 && it > 0) { currentChi = o.chi_cur; iniChi = currentChi; }
+      if (qmax == 0) acc_events(c, 0, 2);
+      tempChi = o.chi_new;
+      if (!o.ok) tempChi = std::numeric_limits<double>::max();
+      rho = (currentChi - tempChi);
+      double scale = o.ok ? o.scale : 0.0;
+      scale += 1e-3;
+      rho /= scale;
+      if (rho > 0 && std::isfinite(tempChi)) {
+        double alpha = 1. - std::pow((2 * rho - 1), 3);
+        alpha = std::min(alpha, 2. / 3.);
+        const double scaleFactor = std::max(1. / 3., alpha);
+        lambda *= scaleFactor;
+        ni = 2;
+        currentChi = tempChi;
+        swap_state(c);
+      } else {
+        lambda *= ni;
+        ni *= 2;
+      }
+      qmax++;
+      st->trials++;
+    } while (rho < 0 && qmax < 10 && !stopped(stop));
+    st->ms_trials += tr.ms();
+    c->kernel_ms_n++;
+    if (qmax == 10 || rho == 0) result = 1;
+    else {
+      if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
+      else nbad = 0;
+      if (nbad >= 3) result = 1;
+    }
+    if (its < SQLM_TRACE_MAX) {
+      st->trace_chi2[its] = currentChi;
+      st->trace_lambda[its] = lambda;
+      st->trace_trials[its] = qmax;
+      st->trace_len = its + 1;
+    }
+    st->chi2_end = currentChi;
+    st->lambda_end = lambda;
+    ++its;
+  }
+  st->iterations = its;
+  st->result = result;
+  st->ms_total = tt.ms();
+  if (n_iter) *n_iter = its;
+  return SQLM_OK;
+}
+
+int optimize_impl(sqlm_ctx *c, int level, int iterations, double user_lambda, const volatile uint8_t *stop,
+                  sqlm_stats *st, int *n_iter) {
+  if (!c->has_problem) return SQLM_ERR_STATE;
+  Timer ts;
+  int s = prepare(c, level);
+  if (s == SQLM_ERR_STATE) {  // nothing to optimize: optimize() returns -1
+    if (st) std::memset(st, 0, sizeof(*st));
+    if (n_iter) *n_iter = -1;
+    return SQLM_OK;
+  }
+  if (s) return s;
+  const double setup = ts.ms();
+  s = run_lm(c, iterations, user_lambda, stop, st, n_iter, false);
+  if (s) return s;
+  finish(c);
+  if (st) st->ms_setup = setup;
+  return SQLM_OK;
+}
+
+void depth_positive_host(const sqlm_ctx *c, std::vector<uint8_t> &out) {
+  out.resize(c->n_obs);
+  for (int64_t e = 0; e < c->n_obs; ++e) {
+    const int p = c->obs_pose[e];
+    double o[3];
+    q_rotate(&c->pose_q[4 * p], &c->pt[3 * c->obs_pt[e]], o);
+    out[e] = (o[2] + c->pose_t[3 * p + 2]) > 0.0;
+  }
+}
+
+inline double edge_chi2(const sqlm_ctx *c, int64_t e) {
+  const double e0 = c->obs_err[2 * e], e1 = c->obs_err[2 * e + 1], w = c->obs_info[e];
+  return e0 * (w * e0) + e1 * (w * e1);
+}
+
+}  // namespace
+
+// ====================================================================== ABI
+
+extern "C" {
+
+const char *sqlm_version(void) { return "sqrtlm-mi355x 0.1.0 (gfx950)"; }
+
+const char *sqlm_status_string(int s) {
+  switch (s) {
+    case SQLM_OK: return "ok";
+    case SQLM_ERR_INVALID_ARG: return "invalid argument";
+    case SQLM_ERR_HIP: return "HIP runtime error";
+    case SQLM_ERR_NOT_SPD: return "system not positive definite";
+    case SQLM_ERR_OOM: return "out of device memory";
+    case SQLM_ERR_ABORTED: return "aborted by stop flag";
+    case SQLM_ERR_NO_DEVICE: return "no HIP device";
+    case SQLM_ERR_STATE: return "call order / state error";
+    case SQLM_ERR_UNSUPPORTED: return "problem shape not supported by this build";
+    case SQLM_ERR_COMM: return "RCCL communicator error";
+    default: return "unknown";
+  }
+}
+
+int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
+  if (!out) return SQLM_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return SQLM_ERR_NO_DEVICE;
+  int dev = device_id;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return SQLM_ERR_HIP;
+  if (dev >= n) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(dev) != hipSuccess) return SQLM_ERR_HIP;
+  sqlm_ctx *c = new (std::nothrow) sqlm_ctx();
+  if (!c) return SQLM_ERR_OOM;
+  c->device = dev;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return SQLM_ERR_HIP; }
+  if (hipHostMalloc((void **)&c->h_scalars, sizeof(double) * kNScalars) != hipSuccess) {
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SQLM_ERR_HIP;
+  }
+  for (auto &e : c->ev) (void)hipEventCreate(&e);
+  *out = c;
+  return SQLM_OK;
+}
+
+int sqlm_ctx_destroy(sqlm_ctx *c) {
+  if (!c) return SQLM_ERR_INVALID_ARG;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  comm_destroy(c->comm);
+  for (auto &b : c->bufs)
+    if (b.p) (void)hipFree(b.p);
+  for (auto &e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->h_scalars) (void)hipHostFree(c->h_scalars);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+  return SQLM_OK;
+}
+
+int sqlm_set_problem(sqlm_ctx *c, int n_pose, const double *pose_q, const double *pose_t,
+                     const uint8_t *pose_fixed, const double *intr, int n_pt, const double *pt, int64_t n_obs,
+                     const int32_t *obs_pose, const int32_t *obs_pt, const double *obs_uv, const double *obs_info,
+                     const double *obs_delta, const uint8_t *obs_level) {
+  if (!c || n_pose < 0 || n_pt < 0 || n_obs < 0) return SQLM_ERR_INVALID_ARG;
+  if ((n_pose && (!pose_q || !pose_t || !pose_fixed || !intr)) || (n_pt && !pt) ||
+      (n_obs && (!obs_pose || !obs_pt || !obs_uv || !obs_info)))
+    return SQLM_ERR_INVALID_ARG;
+  for (int64_t e = 0; e < n_obs; ++e)
+    if (obs_pose[e] < 0 || obs_pose[e] >= n_pose || obs_pt[e] < 0 || obs_pt[e] >= n_pt) return SQLM_ERR_INVALID_ARG;
+  c->n_pose = n_pose;
+  c->n_pt = n_pt;
+  c->n_obs = n_obs;
+  c->pose_q.assign(pose_q, pose_q + 4 * (size_t)n_pose);
+  c->pose_t.assign(pose_t, pose_t + 3 * (size_t)n_pose);
+  c->pose_fixed.assign(pose_fixed, pose_fixed + n_pose);
+  c->intr.assign(intr, intr + 4 * (size_t)n_pose);
+  c->pt.assign(pt, pt + 3 * (size_t)n_pt);
+  c->obs_pose.assign(obs_pose, obs_pose + n_obs);
+  c->obs_pt.assign(obs_pt, obs_pt + n_obs);
+  c->obs_uv.assign(obs_uv, obs_uv + 2 * n_obs);
+  c->obs_info.assign(obs_info, obs_info + n_obs);
+  if (obs_delta) c->obs_delta.assign(obs_delta, obs_delta + n_obs);
+  else c->obs_delta.assign(n_obs, 0.0);
+  if (obs_level) c->obs_level.assign(obs_level, obs_level + n_obs);
+  else c->obs_level.assign(n_obs, 0);
+  c->obs_err.assign(2 * n_obs, 0.0);
+  c->n_lid = 0;
+  c->lid_pose.clear(); c->lid_pc.clear(); c->lid_pw.clear(); c->lid_n.clear(); c->lid_info.clear();
+  c->lid_level.clear(); c->lid_err.clear();
+  c->has_problem = true;
+  return SQLM_OK;
+}
+
+int sqlm_set_lidar(sqlm_ctx *c, int64_t n, const int32_t *pose, const double *p_cam, const double *p_world,
+                   const double *normal, const double *info) {
+  if (!c || !c->has_problem || n < 0) return SQLM_ERR_INVALID_ARG;
+  if (n && (!pose || !p_cam || !p_world || !normal || !info)) return SQLM_ERR_INVALID_ARG;
+  for (int64_t e = 0; e < n; ++e)
+    if (pose[e] < 0 || pose[e] >= c->n_pose) return SQLM_ERR_INVALID_ARG;
+  c->n_lid = n;
+  c->lid_pose.assign(pose, pose + n);
+  c->lid_pc.assign(p_cam, p_cam + 3 * n);
+  c->lid_pw.assign(p_world, p_world + 3 * n);
+  c->lid_n.assign(normal, normal + 3 * n);
+  c->lid_info.assign(info, info + n);
+  c->lid_level.assign(n, 0);
+  c->lid_err.assign(n, 0.0);
+  return SQLM_OK;
+}
+
+int sqlm_set_edge_level(sqlm_ctx *c, const uint8_t *level) {
+  if (!c || !c->has_problem || (!level && c->n_obs)) return SQLM_ERR_INVALID_ARG;
+  c->obs_level.assign(level, level + c->n_obs);
+  return SQLM_OK;
+}
+
+int sqlm_set_lidar_level(sqlm_ctx *c, const uint8_t *level) {
+  if (!c || !c->has_problem || (!level && c->n_lid)) return SQLM_ERR_INVALID_ARG;
+  c->lid_level.assign(level, level + c->n_lid);
+  return SQLM_OK;
+}
+
+int sqlm_set_robust(sqlm_ctx *c, const double *delta) {
+  if (!c || !c->has_problem) return SQLM_ERR_INVALID_ARG;
+  if (delta) c->obs_delta.assign(delta, delta + c->n_obs);
+  else c->obs_delta.assign(c->n_obs, 0.0);
+  return SQLM_OK;
+}
+
+int sqlm_optimize(sqlm_ctx *c, int level, int iterations, double user_lambda, const volatile uint8_t *stop,
+                  sqlm_stats *st, int *n_iter) {
+  if (!c || iterations < 0) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  return optimize_impl(c, level, iterations, user_lambda, stop, st, n_iter);
+}
+
+int sqlm_local_ba(sqlm_ctx *c, const volatile uint8_t *stop, uint8_t *outlier, sqlm_stats st[3], int *ran) {
+  if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  sqlm_stats tmp[3];
+  if (!st) st = tmp;
+  std::memset(st, 0, 3 * sizeof(sqlm_stats));
+  if (ran) *ran = 0;
+  if (stopped(stop)) return SQLM_OK;  // g2oOptimizer.cc:923-928
+  for (auto &l : c->lid_level) l = 255;  // LiDAR edges only exist in pass 3
+  int n = 0, s = optimize_impl(c, 0, 5, 0.0, stop, &st[0], &n);
+  if (s) return s;
+  if (!stopped(stop)) {  // :952-975
+    std::vector<uint8_t> dp;
+    depth_positive_host(c, dp);
+    for (int64_t e = 0; e < c->n_obs; ++e) {
+      if (edge_chi2(c, e) > 5.991 || !dp[e]) c->obs_level[e] = 1;
+      c->obs_delta[e] = 0.0;
+    }
+    s = optimize_impl(c, 0, 10, 0.0, stop, &st[1], &n);
+    if (s) return s;
+  }
+  for (auto &l : c->lid_level) l = 0;  // :1113-1114
+  s = optimize_impl(c, 0, 20, 0.0, stop, &st[2], &n);
+  if (s) return s;
+  if (outlier) {  // :1119-1136
+    std::vector<uint8_t> dp;
+    depth_positive_host(c, dp);
+    for (int64_t e = 0; e < c->n_obs; ++e) outlier[e] = (edge_chi2(c, e) > 5.991 || !dp[e]);
+  }
+  if (ran) *ran = 1;
+  return SQLM_OK;
+}
+
+int sqlm_global_ba(sqlm_ctx *c, int iterations, const volatile uint8_t *stop, sqlm_stats *st, int *n_iter) {
+  return sqlm_optimize(c, 0, iterations, 0.0, stop, st, n_iter);
+}
+
+int sqlm_get_poses(sqlm_ctx *c, double *q, double *t) {
+  if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  if (q) std::memcpy(q, c->pose_q.data(), sizeof(double) * c->pose_q.size());
+  if (t) std::memcpy(t, c->pose_t.data(), sizeof(double) * c->pose_t.size());
+  return SQLM_OK;
+}
+
+int sqlm_get_points(sqlm_ctx *c, double *pt) {
+  if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  if (pt) std::memcpy(pt, c->pt.data(), sizeof(double) * c->pt.size());
+  return SQLM_OK;
+}
+
+int sqlm_get_edge_chi2(sqlm_ctx *c, double *chi2) {
+  if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  if (!chi2 && c->n_obs) return SQLM_ERR_INVALID_ARG;
+  for (int64_t e = 0; e < c->n_obs; ++e) chi2[e] = edge_chi2(c, e);
+  return SQLM_OK;
+}
+
+int sqlm_get_edge_depth_positive(sqlm_ctx *c, uint8_t *pos) {
+  if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  if (!pos && c->n_obs) return SQLM_ERR_INVALID_ARG;
+  std::vector<uint8_t> dp;
+  depth_positive_host(c, dp);
+  if (c->n_obs) std::memcpy(pos, dp.data(), c->n_obs);
+  return SQLM_OK;
+}
+
+int sqlm_get_edge_level(sqlm_ctx *c, uint8_t *level) {
+  if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  if (!level && c->n_obs) return SQLM_ERR_INVALID_ARG;
+  if (c->n_obs) std::memcpy(level, c->obs_level.data(), c->n_obs);
+  return SQLM_OK;
+}
+
+void sqlm_pose_from_Tcw_f32(const float T[16], double q[4], double t[3]) {
+  double R[9];
+  for (int r = 0; r < 3; ++r)
+    for (int k = 0; k < 3; ++k) R[r * 3 + k] = (double)T[r * 4 + k];
+  q_from_mat(R, q);
+  q_normalize_rot(q);
+  for (int r = 0; r < 3; ++r) t[r] = (double)T[r * 4 + 3];
+}
+
+void sqlm_pose_to_Tcw_f32(const double q[4], const double t[3], float T[16]) {
+  double R[9];
+  q_to_mat(q, R);
+  for (int r = 0; r < 3; ++r) {
+    for (int k = 0; k < 3; ++k) T[r * 4 + k] = (float)R[r * 3 + k];
+    T[r * 4 + 3] = (float)t[r];
+  }
+  T[12] = 0.f; T[13] = 0.f; T[14] = 0.f; T[15] = 1.f;
+}
+
+int sqlm_comm_id_size(void) { return comm_id_size(); }
+int sqlm_comm_get_unique_id(char *id) { return comm_get_unique_id(id); }
+int sqlm_ctx_set_comm(sqlm_ctx *c, const char *id, int rank, int nranks) {
+  if (!c || !id || rank < 0 || nranks < 1 || rank >= nranks) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  return comm_init(c->comm, id, rank, nranks);
+}
+
+int sqlm_bench_iterations(sqlm_ctx *c, int warmup, int n, double *ms_per_iter, double *kernel_ms, sqlm_stats *st) {
+  if (!c || !c->has_problem || n <= 0 || warmup < 0) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  // warmup from the initial state, then reset and time n iterations
+  const auto q0 = c->pose_q, t0 = c->pose_t, p0 = c->pt;
+  int s = prepare(c, 0);
+  if (s) return s;
+  if (warmup > 0) {
+    s = run_lm(c, warmup, 0.0, nullptr, nullptr, nullptr, true);
+    if (s) return s;
+    c->pose_q = q0; c->pose_t = t0; c->pt = p0;
+    s = prepare(c, 0);
+    if (s) return s;
+  }
+  HIP_OK(hipStreamSynchronize(c->stream));
+  s = comm_barrier(c->comm, c->stream);
+  if (s) return s;
+  c->timing = kernel_ms != nullptr;
+  std::fill(c->kernel_ms_acc, c->kernel_ms_acc + SQLM_NKERNEL_TIMERS, 0.0);
+  c->kernel_ms_n = 0;
+  Timer t;
+  s = run_lm(c, n, 0.0, nullptr, st, nullptr, true);
+  HIP_OK(hipStreamSynchronize(c->stream));
+  const double ms = t.ms();
+  c->timing = false;
+  if (s) return s;
+  if (ms_per_iter) *ms_per_iter = ms / n;
+  if (kernel_ms) {
+    for (int i = 0; i < SQLM_NKERNEL_TIMERS; ++i)
+      kernel_ms[i] = c->kernel_ms_n ? c->kernel_ms_acc[i] / c->kernel_ms_n : 0.0;
+  }
+  finish(c);
+  return SQLM_OK;
+}
+
+const char *sqlm_kernel_timer_name(int i) {
+  return (i >= 0 && i < SQLM_NKERNEL_TIMERS) ? kTimerNames[i] : "";
+}
+
+}  // extern "C"

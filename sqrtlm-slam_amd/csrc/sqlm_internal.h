@@ -1,0 +1,109 @@
+// sqlm_internal.h — shared between the host LM driver (sqlm_api.cpp) and the
+// HIP kernels (sqlm_kernels.hip). Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sqlm {
+
+constexpr int kBlock = 256;
+
+// HBM layout of one optimize() call. Everything is FP64 except indices.
+//   poses     : all problem poses, index = pose id (ascending id = g2o order)
+//   landmarks : ACTIVE points only, in "device slot" order: bucketed by track
+//               length into segments of width W in {2,4,8,16,32,64}
+//   obs       : ACTIVE mono edges only, contiguous per landmark slot
+//   cameras   : free active poses, hidx = g2o hessianIndex order
+struct DevProblem {
+  int n_pose = 0, nP = 0, nL = 0;
+  int sharded = 0, rank = 0;               // landmark-sharded multi-GPU run
+  int64_t nE = 0;
+  // pose state, double-buffered (cur = 0 / trial = 1 swapped on accept)
+  double *pose_qt[2] = {nullptr, nullptr};  // [n_pose][8]  qx qy qz qw tx ty tz 0
+  double *pose_rt[2] = {nullptr, nullptr};  // [n_pose][16] R(9) t(3) fx fy cx cy
+  double *intr = nullptr;                   // [n_pose][4]
+  int *pose_hidx = nullptr;                 // [n_pose] free hidx or -1
+  int *hidx_pose = nullptr;                 // [nP]
+  // landmarks
+  double *X[2] = {nullptr, nullptr};        // [nL][4]
+  int *lm_begin = nullptr;                  // [nL+1]
+  double *lm_R = nullptr;                   // [nL][8]  R upper (6) of QR(J_l)
+  double *lm_b = nullptr;                   // [nL][4]  b_l = -J_l^T W r
+  double *lm_M = nullptr;                   // [nL][8]  (H_ll + lambda I)^-1, sym (6)
+  double *lm_v = nullptr;                   // [nL][4]  M b_l
+  // observations
+  int *obs_lm = nullptr;                    // [nE] landmark slot
+  int *obs_cam = nullptr;                   // [nE] pose id
+  int *obs_camh = nullptr;                  // [nE] free hidx or -1
+  double *obs_uv = nullptr;                 // [nE][2]
+  double *obs_info = nullptr;               // [nE]
+  double *obs_delta = nullptr;              // [nE] Huber delta, 0 = none
+  double *obs_P = nullptr;                  // [nE][18] H_pl^T block J_l^T W J_p (3x6)
+  double *obs_jp = nullptr;                 // [nE][16] sqrt(w) J_p (12), sqrt(w) r (2)
+  double *obs_err = nullptr;                // [nE][2] last computed error (g2o _error)
+  // cameras
+  int *cam_obs_ptr = nullptr;               // [nP+1]
+  int *cam_obs = nullptr;                   // device obs ids per camera, landmark order
+  double *Hpp = nullptr;                    // [nP][36]
+  double *bp = nullptr;                     // [nP][8]
+  // lidar unary edges (grouped by camera)
+  int64_t nLid = 0;
+  int *lid_cam_ptr = nullptr;               // [nP+1]
+  double *lid_data = nullptr;               // [nLid][12] pc(3) pw(3) n(3) info pad pad
+  int *lid_pose = nullptr;                  // [nLid]
+  double *lid_err = nullptr;                // [nLid]
+  // reduced camera system, BSR upper, row i = free camera i
+  int64_t nnzb = 0;
+  int *s_row_ptr = nullptr;                 // [nP+1]
+  int *s_col = nullptr;                     // [nnzb]
+  double *S = nullptr;                      // [nnzb][36]
+  double *g = nullptr;                      // [6 nP]
+  double *dx = nullptr;                     // [6 nP]
+  double *dense = nullptr;                  // [n][n] dense workspace (upper)
+  // reductions
+  double *partials = nullptr;               // [kMaxPartials]
+  double *scalars = nullptr;                // [8] see Scalar
+  unsigned long long *maxdiag = nullptr;    // bit pattern of a non-negative double
+  int *flags = nullptr;                     // [4] solve_ok ...
+};
+
+enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kNScalars = 8 };
+
+// partial-sum slots
+enum PartialRegion {
+  kPartChiCurLm = 0,         // landmark linearize blocks       (<= 16384)
+  kPartChiCurLid = 16384,    // camera pass, one per free camera (<= 131072)
+  kPartChiNewLm = 147456,    // landmark update blocks          (<= 16384)
+  kPartChiNewLid = 163840,   // lidar chi2 at trial state blocks (<= 16384)
+  kPartScaleCam = 180224,    // pose part of computeScale blocks (<= 16384)
+  kPartScaleLm = 196608,     // landmark part                   (<= 16384)
+  kPartEnd = 212992
+};
+constexpr int kMaxPartials = kPartEnd;
+constexpr int kMaxFreePoses = 131072;
+
+struct Bucket {
+  int W;            // segment width
+  int slot_begin;   // first landmark slot
+  int slot_end;
+};
+
+// kernel launchers (sqlm_kernels.hip). All asynchronous on `st`.
+void launch_pose_prep(const DevProblem &d, int buf, hipStream_t st);
+void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStream_t st);
+void launch_camera_pass(const DevProblem &d, hipStream_t st);
+void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
+void launch_damp(const DevProblem &d, double lambda, hipStream_t st);
+void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st);
+int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
+void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
+void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off,
+                            hipStream_t st);
+void launch_lidar_chi2(const DevProblem &d, hipStream_t st);
+void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts,
+                   int n_lid_parts, hipStream_t st);
+void launch_depth_positive(const DevProblem &d, uint8_t *out_dev, hipStream_t st);
+
+int linearize_blocks(const Bucket &b);
+
+}  // namespace sqlm

@@ -1,0 +1,751 @@
+// sqlm_kernels.hip — hand-written CDNA4 (gfx950) kernels of the square-root
+// LM bundle-adjustment step. FP64 throughout. One wavefront = 64 lanes.
+//
+// Pipeline of one LM iteration (reference counterparts in brackets):
+//   k_pose_prep        quaternion -> rotation matrix per pose
+//   k_linearize<W>     per landmark segment of W lanes: residual, robust weight,
+//                      Jacobians, TSQR of the landmark Jacobian, H_pl blocks
+//                      [computeActiveErrors + linearizeOplus + constructQuadraticForm,
+//                       sparse_optimizer.cpp:73-76, block_solver.hpp:502-560]
+//   k_camera_pass      per free camera: H_pp, b_p, LiDAR unary edges
+//   --- per LM trial ---
+//   k_damp             Givens-damp R with sqrt(lambda) I -> M = (H_ll+lambda)^-1
+//                      [setLambda + D->inverse(), block_solver.hpp:564-589, :389]
+//   k_rcs              reduced camera system rows S_i*, g_i
+//                      [Schur loop, block_solver.hpp:381-439]
+//   k_dense_chol_solve S dx = g  [LinearSolverEigen::solve]
+//   k_pose_update      T <- exp(dx) T, pose part of computeScale
+//   k_landmark_update<W> back-substitution, X += dl, new residuals + chi2
+//                      [block_solver.hpp:459-483, sparse_optimizer.cpp:422-435]
+//   k_reduce           deterministic fixed-order sums of the block partials
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "se3_dev.h"
+#include "sqlm_internal.h"
+
+namespace sqlm {
+
+// ---------------------------------------------------------------- helpers
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// Deterministic block sum (blockDim = 256): wave butterflies then waves in order.
+__device__ double block_sum(double v, double *red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0) r = ((red[0] + red[1]) + red[2]) + red[3];
+  return r;
+}
+
+__device__ double block_max(double v, double *red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0) r = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  return r;
+}
+
+// Givens-rotate row a = (a0,a1,a2) into upper-triangular R (r00 r01 r02 r11 r12 r22).
+// Diagonal of R stays >= 0, so the factor is canonical.
+__device__ __forceinline__ void givens_add_row(double R[6], double a0, double a1, double a2) {
+  if (a0 != 0.0) {
+    const double r = sqrt(R[0] * R[0] + a0 * a0);
+    const double c = R[0] / r, s = a0 / r;
+    R[0] = r;
+    const double t1 = c * R[1] + s * a1; a1 = c * a1 - s * R[1]; R[1] = t1;
+    const double t2 = c * R[2] + s * a2; a2 = c * a2 - s * R[2]; R[2] = t2;
+  }
+  if (a1 != 0.0) {
+    const double r = sqrt(R[3] * R[3] + a1 * a1);
+    const double c = R[3] / r, s = a1 / r;
+    R[3] = r;
+    const double t2 = c * R[4] + s * a2; a2 = c * a2 - s * R[4]; R[4] = t2;
+  }
+  if (a2 != 0.0) R[5] = sqrt(R[5] * R[5] + a2 * a2);
+}
+
+// EdgeSE3ProjectXYZ at one observation (types_six_dof_expmap.h:90-95, .cpp:103-147),
+// with the Huber weight folded in as sqrt(rho' * info) (robust_kernel_impl.cpp:78-90).
+struct MonoEval {
+  double e0, e1;      // raw error obs - proj
+  double chi_rob;     // rho(chi2) (robust) or chi2
+  double s;           // sqrt(rho' * info)
+  double x, y, z;     // camera-frame point
+};
+
+__device__ __forceinline__ void mono_error(const double *__restrict__ prt, double X0, double X1, double X2,
+                                           double u, double v, double info, double delta, MonoEval &m) {
+  m.x = prt[0] * X0 + prt[1] * X1 + prt[2] * X2 + prt[9];
+  m.y = prt[3] * X0 + prt[4] * X1 + prt[5] * X2 + prt[10];
+  m.z = prt[6] * X0 + prt[7] * X1 + prt[8] * X2 + prt[11];
+  const double pu = (m.x / m.z) * prt[12] + prt[14];
+  const double pv = (m.y / m.z) * prt[13] + prt[15];
+  m.e0 = u - pu;
+  m.e1 = v - pv;
+  const double chi2 = m.e0 * (info * m.e0) + m.e1 * (info * m.e1);
+  double rho1 = 1.0;
+  m.chi_rob = chi2;
+  if (delta > 0.0) {
+    const double dsqr = delta * delta;
+    if (chi2 > dsqr) {
+      const double sq = sqrt(chi2);
+      m.chi_rob = 2 * sq * delta - dsqr;
+      rho1 = delta / sq;
+    }
+  }
+  m.s = sqrt(rho1 * info);
+}
+
+// Weighted Jacobians: jl (2x3, row-major) d e / d X, jp (2x6) d e / d [omega; upsilon].
+__device__ __forceinline__ void mono_jac(const double *__restrict__ prt, const MonoEval &m, double jl[6],
+                                         double jp[12]) {
+  const double x = m.x, y = m.y, z = m.z, z_2 = z * z;
+  const double fx = prt[12], fy = prt[13];
+  const double iz = -1. / z;
+  const double t00 = iz * fx, t02 = iz * (-x / z * fx);
+  const double t11 = iz * fy, t12 = iz * (-y / z * fy);
+  const double s = m.s;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    jl[c] = s * (t00 * prt[c] + t02 * prt[6 + c]);
+    jl[3 + c] = s * (t11 * prt[3 + c] + t12 * prt[6 + c]);
+  }
+  jp[0] = s * (x * y / z_2 * fx);
+  jp[1] = s * (-(1 + (x * x / z_2)) * fx);
+  jp[2] = s * (y / z * fx);
+  jp[3] = s * (-1. / z * fx);
+  jp[4] = 0.0;
+  jp[5] = s * (x / z_2 * fx);
+  jp[6] = s * ((1 + y * y / z_2) * fy);
+  jp[7] = s * (-x * y / z_2 * fy);
+  jp[8] = s * (-x / z * fy);
+  jp[9] = 0.0;
+  jp[10] = s * (-1. / z * fy);
+  jp[11] = s * (y / z_2 * fy);
+}
+
+__device__ __forceinline__ void store2(double *p, double a, double b) {
+  *reinterpret_cast<double2 *>(p) = make_double2(a, b);
+}
+
+// ---------------------------------------------------------------- pose prep
+
+__global__ void k_pose_prep(const double *__restrict__ qt, const double *__restrict__ intr,
+                            double *__restrict__ rt, int n) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  double q[4] = {qt[8 * p], qt[8 * p + 1], qt[8 * p + 2], qt[8 * p + 3]};
+  double R[9];
+  q_to_mat(q, R);
+  double *o = rt + 16 * p;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) o[i] = R[i];
+  o[9] = qt[8 * p + 4]; o[10] = qt[8 * p + 5]; o[11] = qt[8 * p + 6];
+  o[12] = intr[4 * p]; o[13] = intr[4 * p + 1]; o[14] = intr[4 * p + 2]; o[15] = intr[4 * p + 3];
+}
+
+void launch_pose_prep(const DevProblem &d, int buf, hipStream_t st) {
+  if (d.n_pose == 0) return;
+  hipLaunchKernelGGL(k_pose_prep, dim3((d.n_pose + 255) / 256), dim3(256), 0, st, d.pose_qt[buf], d.intr,
+                     d.pose_rt[buf], d.n_pose);
+}
+
+// ---------------------------------------------------------------- linearize
+
+constexpr int kMaxGrid = 2048;
+
+int linearize_blocks(const Bucket &b) {
+  const int nseg = b.slot_end - b.slot_begin;
+  const int segs_per_block = kBlock / b.W;
+  int tiles = (nseg + segs_per_block - 1) / segs_per_block;
+  return tiles < kMaxGrid ? tiles : kMaxGrid;
+}
+
+// One landmark per W-lane segment. Each lane folds its observations' two
+// weighted Jacobian rows into a private 3x3 R by Givens rotations; a butterfly
+// over the segment merges the R's (TSQR), so every lane ends with the QR
+// factor of the landmark's stacked 2k x 3 Jacobian without forming J^T J.
+template <int W>
+__global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin, int slot_end, int part_off) {
+  __shared__ double red[4];
+  constexpr int SPB = kBlock / W;
+  const int lane = threadIdx.x & (W - 1);
+  const int nseg = slot_end - slot_begin;
+  const int ntiles = (nseg + SPB - 1) / SPB;
+  const double *__restrict__ prt_all = d.pose_rt[0];
+  double chi_acc = 0.0, dmax = 0.0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int seg = tile * SPB + threadIdx.x / W;
+    const int slot = slot_begin + seg;
+    const bool valid = seg < nseg;
+    double R[6] = {0, 0, 0, 0, 0, 0};
+    double b0 = 0, b1 = 0, b2 = 0, g0 = 0, g1 = 0, g2 = 0, chi = 0;
+    if (valid) {
+      const double X0 = d.X[0][4 * slot], X1 = d.X[0][4 * slot + 1], X2 = d.X[0][4 * slot + 2];
+      const int beg = d.lm_begin[slot], end = d.lm_begin[slot + 1];
+      for (int e = beg + lane; e < end; e += W) {
+        const int cam = d.obs_cam[e];
+        const double *prt = prt_all + 16 * cam;
+        const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
+        MonoEval m;
+        mono_error(prt, X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
+        store2(d.obs_err + 2 * e, m.e0, m.e1);
+        chi += m.chi_rob;
+        double jl[6], jp[12];
+        mono_jac(prt, m, jl, jp);
+        const double r0 = m.s * m.e0, r1 = m.s * m.e1;
+        b0 -= jl[0] * r0 + jl[3] * r1;
+        b1 -= jl[1] * r0 + jl[4] * r1;
+        b2 -= jl[2] * r0 + jl[5] * r1;
+        g0 += jl[0] * jl[0] + jl[3] * jl[3];
+        g1 += jl[1] * jl[1] + jl[4] * jl[4];
+        g2 += jl[2] * jl[2] + jl[5] * jl[5];
+        givens_add_row(R, jl[0], jl[1], jl[2]);
+        givens_add_row(R, jl[3], jl[4], jl[5]);
+        if (d.obs_camh[e] >= 0) {
+          double *P = d.obs_P + 18 * e;  // H_lp block: jl^T jp, 3x6 row-major
+#pragma unroll
+          for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int c = 0; c < 6; c += 2)
+              store2(P + 6 * a + c, jl[a] * jp[c] + jl[3 + a] * jp[6 + c],
+                     jl[a] * jp[c + 1] + jl[3 + a] * jp[6 + c + 1]);
+          double *J = d.obs_jp + 16 * e;
+#pragma unroll
+          for (int c = 0; c < 12; c += 2) store2(J + c, jp[c], jp[c + 1]);
+          store2(J + 12, r0, r1);
+        }
+      }
+    }
+    // TSQR butterfly inside the segment (canonical: lower lane's R absorbs the upper's rows)
+#pragma unroll
+    for (int off = 1; off < W; off <<= 1) {
+      double o[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) o[i] = __shfl_xor(R[i], off, 64);
+      const bool lo = (lane & off) == 0;
+      double A[6], B[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) { A[i] = lo ? R[i] : o[i]; B[i] = lo ? o[i] : R[i]; }
+      givens_add_row(A, B[0], B[1], B[2]);
+      givens_add_row(A, 0.0, B[3], B[4]);
+      givens_add_row(A, 0.0, 0.0, B[5]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) R[i] = A[i];
+      b0 += __shfl_xor(b0, off, 64); b1 += __shfl_xor(b1, off, 64); b2 += __shfl_xor(b2, off, 64);
+      g0 += __shfl_xor(g0, off, 64); g1 += __shfl_xor(g1, off, 64); g2 += __shfl_xor(g2, off, 64);
+      chi += __shfl_xor(chi, off, 64);
+    }
+    if (valid && lane == 0) {
+      double *Ro = d.lm_R + 8 * slot;
+      store2(Ro, R[0], R[1]); store2(Ro + 2, R[2], R[3]); store2(Ro + 4, R[4], R[5]);
+      double *bo = d.lm_b + 4 * slot;
+      store2(bo, b0, b1); store2(bo + 2, b2, 0.0);
+      chi_acc += chi;
+      dmax = fmax(dmax, fmax(g0, fmax(g1, g2)));
+    }
+  }
+  const double s = block_sum(chi_acc, red);
+  const double mx = block_max(dmax, red);
+  if (threadIdx.x == 0) {
+    d.partials[kPartChiCurLm + part_off + blockIdx.x] = s;
+    atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
+  }
+}
+
+void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStream_t st) {
+  const int nb = linearize_blocks(b);
+  if (nb <= 0) return;
+  switch (b.W) {
+#define SQLM_CASE(WW) \
+  case WW: hipLaunchKernelGGL(k_linearize<WW>, dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, part_off); break;
+    SQLM_CASE(2) SQLM_CASE(4) SQLM_CASE(8) SQLM_CASE(16) SQLM_CASE(32) SQLM_CASE(64)
+#undef SQLM_CASE
+    default: break;
+  }
+}
+
+// ---------------------------------------------------------------- camera pass
+
+// One wave per free camera: H_pp = sum jp^T jp, b_p = -sum jp^T r, plus the
+// camera's LiDAR unary edges (numeric Jacobian, base_unary_edge.hpp:82-122).
+__global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + wave;
+  double H[21], b[6], chi = 0.0;
+#pragma unroll
+  for (int k = 0; k < 21; ++k) H[k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) b[k] = 0.0;
+  if (i < d.nP) {
+    for (int t = d.cam_obs_ptr[i] + lane; t < d.cam_obs_ptr[i + 1]; t += 64) {
+      const double *J = d.obs_jp + 16 * d.cam_obs[t];
+      double j[14];
+#pragma unroll
+      for (int k = 0; k < 14; k += 2) {
+        const double2 v = *reinterpret_cast<const double2 *>(J + k);
+        j[k] = v.x; j[k + 1] = v.y;
+      }
+      int k = 0;
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        b[r] -= j[r] * j[12] + j[6 + r] * j[13];
+#pragma unroll
+        for (int c = r; c < 6; ++c) H[k++] += j[r] * j[c] + j[6 + r] * j[6 + c];
+      }
+    }
+    if (d.nLid > 0) {
+      const int p = d.hidx_pose[i];
+      const double *qt = d.pose_qt[0] + 8 * p;
+      const double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t3[3] = {qt[4], qt[5], qt[6]};
+      for (int t = d.lid_cam_ptr[i] + lane; t < d.lid_cam_ptr[i + 1]; t += 64) {
+        const double *L = d.lid_data + 12 * t;
+        const double e = lidar_error(q, t3, L, L + 3, L + 6);
+        d.lid_err[t] = e;
+        const double info = L[9];
+        chi += e * (info * e);
+        double J[6];
+        lidar_jacobian(q, t3, L, L + 3, L + 6, J);
+        int k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          b[r] -= (J[r] * info) * e;
+#pragma unroll
+          for (int c = r; c < 6; ++c) H[k++] += (J[r] * info) * J[c];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 21; ++k) H[k] = wave_sum(H[k]);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) b[k] = wave_sum(b[k]);
+  chi = wave_sum(chi);
+  if (i < d.nP && lane == 0) {
+    double *Ho = d.Hpp + 36 * i;
+    int k = 0;
+    double mx = 0.0;
+    for (int r = 0; r < 6; ++r)
+      for (int c = r; c < 6; ++c) {
+        Ho[r * 6 + c] = H[k];
+        Ho[c * 6 + r] = H[k];
+        if (r == c) mx = fmax(mx, fabs(H[k]));
+        ++k;
+      }
+    for (int r = 0; r < 6; ++r) d.bp[8 * i + r] = b[r];
+    d.partials[kPartChiCurLid + i] = chi;
+    if (!d.sharded) atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
+  }
+}
+
+void launch_camera_pass(const DevProblem &d, hipStream_t st) {
+  if (d.nP == 0) return;
+  hipLaunchKernelGGL(k_camera_pass, dim3((d.nP + 3) / 4), dim3(256), 0, st, d);
+}
+
+// Sharded runs: max |diag(H_pp)| after the cross-rank sum of H_pp.
+__global__ __launch_bounds__(256) void k_pose_maxdiag(DevProblem d) {
+  __shared__ double red[4];
+  double mx = 0.0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.nP; i += gridDim.x * blockDim.x)
+    for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(d.Hpp[36 * i + 7 * k]));
+  mx = block_max(mx, red);
+  if (threadIdx.x == 0) atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
+}
+
+void launch_pose_maxdiag(const DevProblem &d, hipStream_t st) {
+  if (d.nP == 0) return;
+  hipLaunchKernelGGL(k_pose_maxdiag, dim3(std::min(64, (d.nP + 255) / 256)), dim3(256), 0, st, d);
+}
+
+// ---------------------------------------------------------------- damping
+
+// R' = QR([R; sqrt(lambda) I]) by three Givens sweeps; M = R'^-1 R'^-T.
+__global__ void k_damp(DevProblem d, double lambda) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= d.nL) return;
+  const double *Rl = d.lm_R + 8 * l;
+  double R[6] = {Rl[0], Rl[1], Rl[2], Rl[3], Rl[4], Rl[5]};
+  const double sl = sqrt(lambda);
+  givens_add_row(R, sl, 0.0, 0.0);
+  givens_add_row(R, 0.0, sl, 0.0);
+  givens_add_row(R, 0.0, 0.0, sl);
+  const double i00 = 1.0 / R[0], i11 = 1.0 / R[3], i22 = 1.0 / R[5];
+  const double i01 = -(R[1] * i11) * i00;
+  const double i12 = -(R[4] * i22) * i11;
+  const double i02 = -(R[1] * i12 + R[2] * i22) * i00;
+  const double m00 = i00 * i00 + i01 * i01 + i02 * i02;
+  const double m01 = i01 * i11 + i02 * i12;
+  const double m02 = i02 * i22;
+  const double m11 = i11 * i11 + i12 * i12;
+  const double m12 = i12 * i22;
+  const double m22 = i22 * i22;
+  double *M = d.lm_M + 8 * l;
+  store2(M, m00, m01); store2(M + 2, m02, m11); store2(M + 4, m12, m22);
+  const double *bl = d.lm_b + 4 * l;
+  const double v0 = m00 * bl[0] + m01 * bl[1] + m02 * bl[2];
+  const double v1 = m01 * bl[0] + m11 * bl[1] + m12 * bl[2];
+  const double v2 = m02 * bl[0] + m12 * bl[1] + m22 * bl[2];
+  double *v = d.lm_v + 4 * l;
+  store2(v, v0, v1); store2(v + 2, v2, 0.0);
+}
+
+void launch_damp(const DevProblem &d, double lambda, hipStream_t st) {
+  if (d.nL == 0) return;
+  hipLaunchKernelGGL(k_damp, dim3((d.nL + 255) / 256), dim3(256), 0, st, d, lambda);
+}
+
+// ---------------------------------------------------------------- RCS
+
+// Row i of the reduced camera system. Each wave walks a share of camera i's
+// landmarks and accumulates -P_i^T M P_j into a wave-private LDS copy of the
+// row (one observation j at a time, so no two lanes touch one entry); the four
+// copies are summed in wave order at the end => bitwise deterministic.
+__global__ __launch_bounds__(256) void k_rcs(DevProblem d, double lambda, int nslot_max) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int i = blockIdx.x;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int rb = d.s_row_ptr[i], nslot = d.s_row_ptr[i + 1] - rb;
+  double *acc = smem + wave * nslot_max * 36;
+  double *gw = smem + 4 * nslot_max * 36;                 // [4][8]
+  int *cols = reinterpret_cast<int *>(gw + 32);           // [nslot_max]
+  for (int k = lane; k < nslot * 36; k += 64) acc[k] = 0.0;
+  for (int k = threadIdx.x; k < nslot; k += 256) cols[k] = d.s_col[rb + k];
+  __syncthreads();
+  const int r = lane / 6, c = lane % 6;  // entry owned by lanes 0..35
+  double gacc = 0.0;                     // lanes 0..5: g_r partial
+  for (int t = d.cam_obs_ptr[i] + wave; t < d.cam_obs_ptr[i + 1]; t += 4) {
+    const int oi = d.cam_obs[t];
+    const int l = d.obs_lm[oi];
+    const double *Ml = d.lm_M + 8 * l;
+    const double M00 = Ml[0], M01 = Ml[1], M02 = Ml[2], M11 = Ml[3], M12 = Ml[4], M22 = Ml[5];
+    const double *Pi = d.obs_P + 18 * oi;
+    // lanes 0..17 compute Z[zr][zc] = (P_i^T M)[zr][zc], zr in 0..5, zc in 0..2
+    double zval = 0.0;
+    if (lane < 18) {
+      const int zr = lane / 3, zc = lane % 3;
+      const double p0 = Pi[zr], p1 = Pi[6 + zr], p2 = Pi[12 + zr];
+      const double m0 = zc == 0 ? M00 : (zc == 1 ? M01 : M02);
+      const double m1 = zc == 0 ? M01 : (zc == 1 ? M11 : M12);
+      const double m2 = zc == 0 ? M02 : (zc == 1 ? M12 : M22);
+      zval = p0 * m0 + p1 * m1 + p2 * m2;
+    }
+    if (lane < 6) {
+      const double *v = d.lm_v + 4 * l;
+      gacc -= Pi[lane] * v[0] + Pi[6 + lane] * v[1] + Pi[12 + lane] * v[2];
+    }
+    const int rr = lane < 36 ? r : 0;
+    const double z0 = __shfl(zval, 3 * rr, 64);
+    const double z1 = __shfl(zval, 3 * rr + 1, 64);
+    const double z2 = __shfl(zval, 3 * rr + 2, 64);
+    const int beg = d.lm_begin[l], end = d.lm_begin[l + 1];
+    for (int o = beg; o < end; ++o) {
+      const int cj = d.obs_camh[o];
+      if (cj < i) continue;  // fixed (-1) or lower triangle
+      // binary search slot of cj in the sorted row pattern
+      int lo = 0, hi = nslot - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cols[mid] < cj) lo = mid + 1; else hi = mid;
+      }
+      if (lane < 36) {
+        const double *Pj = d.obs_P + 18 * o;
+        const double v = z0 * Pj[c] + z1 * Pj[6 + c] + z2 * Pj[12 + c];
+        acc[lo * 36 + lane] -= v;
+      }
+    }
+  }
+  if (lane < 6) gw[wave * 8 + lane] = gacc;
+  __syncthreads();
+  double *Srow = d.S + (int64_t)rb * 36;
+  for (int k = threadIdx.x; k < nslot * 36; k += 256) {
+    const int nsm = nslot_max * 36;
+    double v = ((smem[k] + smem[nsm + k]) + smem[2 * nsm + k]) + smem[3 * nsm + k];
+    if (k < 36 && (!d.sharded || d.rank == 0)) {  // slot 0 = diagonal block (cols[0] == i)
+      v += d.Hpp[36 * i + k];
+      if (k % 7 == 0) v += lambda;
+    }
+    Srow[k] = v;
+  }
+  if (threadIdx.x < 6) {
+    const int rr = threadIdx.x;
+    const double bpv = (!d.sharded || d.rank == 0) ? d.bp[8 * i + rr] : 0.0;
+    d.g[6 * i + rr] = bpv + (((gw[rr] + gw[8 + rr]) + gw[16 + rr]) + gw[24 + rr]);
+  }
+}
+
+void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st) {
+  if (d.nP == 0) return;
+  const size_t lds = (size_t)4 * max_row_blocks * 36 * sizeof(double) + 32 * sizeof(double) +
+                     (size_t)max_row_blocks * sizeof(int) + 16;
+  hipLaunchKernelGGL(k_rcs, dim3(d.nP), dim3(256), lds, st, d, lambda, max_row_blocks);
+}
+
+// ---------------------------------------------------------------- dense solve
+
+// Single-workgroup Cholesky S = U^T U of the (small) reduced camera system and
+// the two triangular solves. Used for local-BA sized systems.
+__global__ __launch_bounds__(1024) void k_dense_chol_solve(DevProblem d, int n) {
+  extern __shared__ __attribute__((aligned(16))) double vec[];  // [n]
+  __shared__ int fail;
+  double *A = d.dense;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  // scatter BSR upper blocks to dense row-major upper
+  for (int64_t k = tid; k < (int64_t)n * n; k += nt) A[k] = 0.0;
+  __syncthreads();
+  for (int i = 0; i < d.nP; ++i) {
+    for (int s = d.s_row_ptr[i]; s < d.s_row_ptr[i + 1]; ++s) {
+      const int j = d.s_col[s];
+      for (int e = tid; e < 36; e += nt) {
+        const int r = 6 * i + e / 6, c = 6 * j + e % 6;
+        if (r <= c) A[(int64_t)r * n + c] = d.S[(int64_t)s * 36 + e];
+      }
+    }
+  }
+  if (tid == 0) fail = 0;
+  for (int k = tid; k < n; k += nt) vec[k] = d.g[k];
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    if (tid == 0) {
+      const double akk = A[(int64_t)k * n + k];
+      if (!(akk > 0.0)) fail = 1;
+      A[(int64_t)k * n + k] = sqrt(akk);
+    }
+    __syncthreads();
+    if (fail) break;
+    const double ukk = A[(int64_t)k * n + k];
+    for (int j = k + 1 + tid; j < n; j += nt) A[(int64_t)k * n + j] /= ukk;
+    __syncthreads();
+    const int m = n - k - 1;
+    for (int64_t idx = tid; idx < (int64_t)m * m; idx += nt) {
+      const int ii = k + 1 + (int)(idx / m), jj = k + 1 + (int)(idx % m);
+      if (jj >= ii) A[(int64_t)ii * n + jj] -= A[(int64_t)k * n + ii] * A[(int64_t)k * n + jj];
+    }
+    __syncthreads();
+  }
+  if (fail) {
+    if (tid == 0) d.flags[0] = 0;
+    for (int k = tid; k < n; k += nt) d.dx[k] = 0.0;
+    return;
+  }
+  // U^T y = g
+  for (int k = 0; k < n; ++k) {
+    const double yk = vec[k] / A[(int64_t)k * n + k];
+    __syncthreads();
+    if (tid == 0) vec[k] = yk;
+    for (int j = k + 1 + tid; j < n; j += nt) vec[j] -= A[(int64_t)k * n + j] * yk;
+    __syncthreads();
+  }
+  // U x = y
+  for (int k = n - 1; k >= 0; --k) {
+    const double xk = vec[k] / A[(int64_t)k * n + k];
+    __syncthreads();
+    if (tid == 0) vec[k] = xk;
+    for (int j = tid; j < k; j += nt) vec[j] -= A[(int64_t)j * n + k] * xk;
+    __syncthreads();
+  }
+  for (int k = tid; k < n; k += nt) d.dx[k] = vec[k];
+  if (tid == 0) d.flags[0] = 1;
+}
+
+int launch_dense_solve(const DevProblem &d, hipStream_t st) {
+  const int n = 6 * d.nP;
+  if (n == 0) return 0;
+  if ((size_t)n * sizeof(double) > 150 * 1024) return -8;  // SQLM_ERR_UNSUPPORTED
+  hipLaunchKernelGGL(k_dense_chol_solve, dim3(1), dim3(1024), (size_t)n * sizeof(double), st, d, n);
+  return 0;
+}
+
+// ---------------------------------------------------------------- updates
+
+__global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda) {
+  __shared__ double red[4];
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  double sc = 0.0;
+  if (p < d.n_pose) {
+    const double *qt = d.pose_qt[0] + 8 * p;
+    double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t[3] = {qt[4], qt[5], qt[6]};
+    const int h = d.pose_hidx[p];
+    if (h >= 0) {
+      const double *dx = d.dx + 6 * h;
+      const double dd[6] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5]};
+      se3_oplus(q, t, dd);
+      if (!d.sharded || d.rank == 0)
+        for (int k = 0; k < 6; ++k) sc += dd[k] * (lambda * dd[k] + d.bp[8 * h + k]);
+    }
+    double *o = d.pose_qt[1] + 8 * p;
+    store2(o, q[0], q[1]); store2(o + 2, q[2], q[3]); store2(o + 4, t[0], t[1]); store2(o + 6, t[2], 0.0);
+    double R[9];
+    q_to_mat(q, R);
+    double *rt = d.pose_rt[1] + 16 * p;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) rt[k] = R[k];
+    rt[9] = t[0]; rt[10] = t[1]; rt[11] = t[2];
+    rt[12] = d.intr[4 * p]; rt[13] = d.intr[4 * p + 1]; rt[14] = d.intr[4 * p + 2]; rt[15] = d.intr[4 * p + 3];
+  }
+  const double s = block_sum(sc, red);
+  if (threadIdx.x == 0) d.partials[kPartScaleCam + blockIdx.x] = s;
+}
+
+void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st) {
+  if (d.n_pose == 0) return;
+  hipLaunchKernelGGL(k_pose_update, dim3((d.n_pose + 255) / 256), dim3(256), 0, st, d, lambda);
+}
+
+// Back-substitution dl = M (b_l - sum_i H_lp,i dx_i), X' = X + dl, then the
+// residuals of the landmark's edges at the trial state (computeActiveErrors).
+template <int W>
+__global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
+                                                         double lambda, int part_off) {
+  __shared__ double red[4];
+  constexpr int SPB = kBlock / W;
+  const int lane = threadIdx.x & (W - 1);
+  const int nseg = slot_end - slot_begin;
+  const int ntiles = (nseg + SPB - 1) / SPB;
+  double chi_acc = 0.0, sc_acc = 0.0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int seg = tile * SPB + threadIdx.x / W;
+    const int slot = slot_begin + seg;
+    const bool valid = seg < nseg;
+    double a0 = 0, a1 = 0, a2 = 0;
+    int beg = 0, end = 0;
+    if (valid) {
+      beg = d.lm_begin[slot]; end = d.lm_begin[slot + 1];
+      for (int e = beg + lane; e < end; e += W) {
+        const int h = d.obs_camh[e];
+        if (h < 0) continue;
+        const double *P = d.obs_P + 18 * e, *dx = d.dx + 6 * h;
+        double x[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) x[k] = dx[k];
+        a0 += P[0] * x[0] + P[1] * x[1] + P[2] * x[2] + P[3] * x[3] + P[4] * x[4] + P[5] * x[5];
+        a1 += P[6] * x[0] + P[7] * x[1] + P[8] * x[2] + P[9] * x[3] + P[10] * x[4] + P[11] * x[5];
+        a2 += P[12] * x[0] + P[13] * x[1] + P[14] * x[2] + P[15] * x[3] + P[16] * x[4] + P[17] * x[5];
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < W; off <<= 1) {
+      a0 += __shfl_xor(a0, off, 64); a1 += __shfl_xor(a1, off, 64); a2 += __shfl_xor(a2, off, 64);
+    }
+    double chi = 0.0;
+    if (valid) {
+      const double *M = d.lm_M + 8 * slot, *bl = d.lm_b + 4 * slot;
+      const double c0 = bl[0] - a0, c1 = bl[1] - a1, c2 = bl[2] - a2;
+      const double dl0 = M[0] * c0 + M[1] * c1 + M[2] * c2;
+      const double dl1 = M[1] * c0 + M[3] * c1 + M[4] * c2;
+      const double dl2 = M[2] * c0 + M[4] * c1 + M[5] * c2;
+      const double *X = d.X[0] + 4 * slot;
+      const double X0 = X[0] + dl0, X1 = X[1] + dl1, X2 = X[2] + dl2;
+      if (lane == 0) {
+        double *Xo = d.X[1] + 4 * slot;
+        store2(Xo, X0, X1); store2(Xo + 2, X2, 0.0);
+        sc_acc += dl0 * (lambda * dl0 + bl[0]) + dl1 * (lambda * dl1 + bl[1]) + dl2 * (lambda * dl2 + bl[2]);
+      }
+      const double *prt_all = d.pose_rt[1];
+      for (int e = beg + lane; e < end; e += W) {
+        const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
+        MonoEval m;
+        mono_error(prt_all + 16 * d.obs_cam[e], X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
+        store2(d.obs_err + 2 * e, m.e0, m.e1);
+        chi += m.chi_rob;
+      }
+    }
+#pragma unroll
+    for (int off = 1; off < W; off <<= 1) chi += __shfl_xor(chi, off, 64);
+    if (valid && lane == 0) chi_acc += chi;
+  }
+  const double s1 = block_sum(chi_acc, red);
+  const double s2 = block_sum(sc_acc, red);
+  if (threadIdx.x == 0) {
+    d.partials[kPartChiNewLm + part_off + blockIdx.x] = s1;
+    d.partials[kPartScaleLm + part_off + blockIdx.x] = s2;
+  }
+}
+
+void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st) {
+  const int nb = linearize_blocks(b);
+  if (nb <= 0) return;
+  switch (b.W) {
+#define SQLM_CASE(WW)                                                                                      \
+  case WW:                                                                                                 \
+    hipLaunchKernelGGL(k_landmark_update<WW>, dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, \
+                       lambda, part_off);                                                                  \
+    break;
+    SQLM_CASE(2) SQLM_CASE(4) SQLM_CASE(8) SQLM_CASE(16) SQLM_CASE(32) SQLM_CASE(64)
+#undef SQLM_CASE
+    default: break;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_lidar_chi2(DevProblem d) {
+  __shared__ double red[4];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  double chi = 0.0;
+  if (t < d.nLid) {
+    const double *qt = d.pose_qt[1] + 8 * d.lid_pose[t];
+    const double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t3[3] = {qt[4], qt[5], qt[6]};
+    const double *L = d.lid_data + 12 * t;
+    const double e = lidar_error(q, t3, L, L + 3, L + 6);
+    d.lid_err[t] = e;
+    chi = e * (L[9] * e);
+  }
+  const double s = block_sum(chi, red);
+  if (threadIdx.x == 0) d.partials[kPartChiNewLid + blockIdx.x] = s;
+}
+
+void launch_lidar_chi2(const DevProblem &d, hipStream_t st) {
+  if (d.nLid == 0) return;
+  hipLaunchKernelGGL(k_lidar_chi2, dim3((d.nLid + 255) / 256), dim3(256), 0, st, d);
+}
+
+// ---------------------------------------------------------------- reductions
+
+__device__ double region_sum(const double *p, int n, double *red) {
+  double v = 0.0;
+  for (int k = threadIdx.x; k < n; k += 256) v += p[k];
+  return block_sum(v, red);
+}
+
+__global__ __launch_bounds__(256) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam, int n_lid) {
+  __shared__ double red[4];
+  const double c0 = region_sum(d.partials + kPartChiCurLm, n_lm_cur, red);
+  const double c1 = region_sum(d.partials + kPartChiCurLid, d.nP, red);
+  const double n0 = region_sum(d.partials + kPartChiNewLm, n_lm_new, red);
+  const double n1 = region_sum(d.partials + kPartChiNewLid, n_lid, red);
+  const double s0 = region_sum(d.partials + kPartScaleCam, n_cam, red);
+  const double s1 = region_sum(d.partials + kPartScaleLm, n_lm_new, red);
+  if (threadIdx.x == 0) {
+    d.scalars[kChiCur] = c0 + c1;
+    d.scalars[kChiNew] = n0 + n1;
+    d.scalars[kScale] = s0 + s1;
+    d.scalars[kMaxDiag] = __longlong_as_double((long long)*d.maxdiag);
+    d.scalars[kSolveOk] = (double)d.flags[0];
+  }
+}
+
+void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts, int n_lid_parts,
+                   hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, st, d, n_lm_parts_cur, n_lm_parts_new, n_cam_parts,
+                     n_lid_parts);
+}
+
+}  // namespace sqlm

@@ -1,0 +1,83 @@
+"""ctypes binding of libsqrtlm.so (include/sqrtlm.h).
+
+The library is the product: there is no CPU fallback. Importing works without
+a GPU (the CPU test suite checks the exports), but creating a context on a
+machine without a HIP device fails loudly with SQLM_ERR_NO_DEVICE.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsqrtlm.so")
+TRACE_MAX = 256
+NKERNEL_TIMERS = 8
+
+SQLM_OK = 0
+STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "not SPD", -4: "out of device memory",
+          -5: "aborted", -6: "no HIP device", -7: "state error", -8: "unsupported problem shape", -9: "RCCL error"}
+
+# every symbol include/sqrtlm.h declares
+EXPORTS = [
+    "sqlm_version", "sqlm_status_string", "sqlm_ctx_create", "sqlm_ctx_destroy", "sqlm_set_problem",
+    "sqlm_set_lidar", "sqlm_set_edge_level", "sqlm_set_robust", "sqlm_set_lidar_level", "sqlm_optimize",
+    "sqlm_local_ba", "sqlm_global_ba", "sqlm_get_poses", "sqlm_get_points", "sqlm_get_edge_chi2",
+    "sqlm_get_edge_depth_positive", "sqlm_get_edge_level", "sqlm_pose_from_Tcw_f32", "sqlm_pose_to_Tcw_f32",
+    "sqlm_comm_id_size", "sqlm_comm_get_unique_id", "sqlm_ctx_set_comm", "sqlm_bench_iterations",
+    "sqlm_kernel_timer_name",
+]
+
+
+class SqlmError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        super().__init__(f"{what}: {STATUS.get(status, status)} ({status})")
+        self.status = status
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("iterations", C.c_int), ("trials", C.c_int), ("result", C.c_int), ("n_active_edges", C.c_int),
+        ("chi2_begin", C.c_double), ("chi2_end", C.c_double), ("lambda_end", C.c_double),
+        ("trace_len", C.c_int), ("trace_chi2", C.c_double * TRACE_MAX),
+        ("trace_lambda", C.c_double * TRACE_MAX), ("trace_trials", C.c_int * TRACE_MAX),
+        ("ms_total", C.c_double), ("ms_setup", C.c_double), ("ms_linearize", C.c_double),
+        ("ms_trials", C.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        n = self.trace_len
+        return dict(iterations=self.iterations, trials=self.trials, result=self.result,
+                    n_active_edges=self.n_active_edges, chi2_begin=self.chi2_begin, chi2_end=self.chi2_end,
+                    lambda_end=self.lambda_end, trace_chi2=list(self.trace_chi2[:n]),
+                    trace_lambda=list(self.trace_lambda[:n]), trace_trials=list(self.trace_trials[:n]),
+                    ms_total=self.ms_total, ms_setup=self.ms_setup, ms_linearize=self.ms_linearize,
+                    ms_trials=self.ms_trials)
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} missing: build it with __graft_entry__.build() "
+                              "(make -C sqrtlm-slam_amd/csrc); there is no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        L.sqlm_version.restype = C.c_char_p
+        L.sqlm_status_string.restype = C.c_char_p
+        L.sqlm_kernel_timer_name.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != SQLM_OK:
+        raise SqlmError(status, what)
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)

@@ -1,0 +1,216 @@
+"""Host-side mirror of the reference's BA entry points, over the C ABI.
+
+``Optimizer`` reproduces the static façade of include/backend/Optimizer.h:42-71
+for the bundle-adjustment calls; each method takes the graph the reference's
+``g2oOptimizer`` would have assembled (a :class:`BAProblem`) and runs the same
+schedule on the MI355X through libsqrtlm.so:
+
+* ``LocalBundleAdjustment``  -> g2oOptimizer.cc:704-1191 (3 passes, outlier tags)
+* ``GlobalBundleAdjustemnt`` -> g2oOptimizer.cc:80-89 (the reference's spelling)
+* ``BundleAdjustment``       -> g2oOptimizer.cc:110-362
+
+Results are written back into the problem (poses, points) like the
+reference's ``SetPose`` / ``SetWorldPos`` write-back (g2oOptimizer.cc:1167-1189).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+from .problem import HUBER_MONO_GBA, BAProblem
+
+
+class Context:
+    """One ``sqlm_ctx``: a HIP stream + device memory on one GPU. Create one per
+    calling thread (the reference runs LBA, loop closing and GBA concurrently)."""
+
+    def __init__(self, device: int = -1):
+        self._h = C.c_void_p()
+        check(lib().sqlm_ctx_create(int(device), C.byref(self._h)), "sqlm_ctx_create")
+        self.problem: BAProblem | None = None
+
+    def close(self) -> None:
+        if self._h:
+            lib().sqlm_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------- graph
+    def set_problem(self, p: BAProblem) -> None:
+        check(lib().sqlm_set_problem(
+            self._h, p.n_pose, ptr(p.pose_q), ptr(p.pose_t), ptr(p.pose_fixed), ptr(p.intr), p.n_pt, ptr(p.pt),
+            C.c_int64(p.n_obs), ptr(p.obs_pose), ptr(p.obs_pt), ptr(p.obs_uv), ptr(p.obs_info), ptr(p.obs_delta),
+            ptr(p.obs_level)), "sqlm_set_problem")
+        if p.n_lid:
+            check(lib().sqlm_set_lidar(self._h, C.c_int64(p.n_lid), ptr(p.lid_pose), ptr(p.lid_pc), ptr(p.lid_pw),
+                                       ptr(p.lid_n), ptr(p.lid_info)), "sqlm_set_lidar")
+        self.problem = p
+
+    def set_edge_level(self, level: np.ndarray) -> None:
+        level = np.ascontiguousarray(level, np.uint8)
+        check(lib().sqlm_set_edge_level(self._h, ptr(level)), "sqlm_set_edge_level")
+
+    def set_robust(self, delta: np.ndarray | None) -> None:
+        d = None if delta is None else np.ascontiguousarray(delta, np.float64)
+        check(lib().sqlm_set_robust(self._h, ptr(d)), "sqlm_set_robust")
+
+    def set_lidar_level(self, level: np.ndarray) -> None:
+        level = np.ascontiguousarray(level, np.uint8)
+        check(lib().sqlm_set_lidar_level(self._h, ptr(level)), "sqlm_set_lidar_level")
+
+    # ------------------------------------------------------------- solve
+    def optimize(self, level: int = 0, iterations: int = 10, user_lambda: float = 0.0, stop=None):
+        st = _lib.Stats()
+        n = C.c_int(0)
+        check(lib().sqlm_optimize(self._h, int(level), int(iterations), C.c_double(user_lambda), ptr(stop),
+                                  C.byref(st), C.byref(n)), "sqlm_optimize")
+        return n.value, st.as_dict()
+
+    def local_ba(self, stop=None):
+        st = (_lib.Stats * 3)()
+        ran = C.c_int(0)
+        outl = np.zeros(self.problem.n_obs if self.problem else 0, np.uint8)
+        check(lib().sqlm_local_ba(self._h, ptr(stop), ptr(outl), st, C.byref(ran)), "sqlm_local_ba")
+        return ran.value, outl, [s.as_dict() for s in st]
+
+    def global_ba(self, iterations: int, stop=None):
+        st = _lib.Stats()
+        n = C.c_int(0)
+        check(lib().sqlm_global_ba(self._h, int(iterations), ptr(stop), C.byref(st), C.byref(n)), "sqlm_global_ba")
+        return n.value, st.as_dict()
+
+    def bench(self, warmup: int, n: int):
+        ms = C.c_double(0)
+        kms = np.zeros(_lib.NKERNEL_TIMERS)
+        st = _lib.Stats()
+        check(lib().sqlm_bench_iterations(self._h, int(warmup), int(n), C.byref(ms), ptr(kms), C.byref(st)),
+              "sqlm_bench_iterations")
+        names = [lib().sqlm_kernel_timer_name(i).decode() for i in range(_lib.NKERNEL_TIMERS)]
+        return ms.value, dict(zip(names, kms.tolist())), st.as_dict()
+
+    def set_comm(self, unique_id: bytes, rank: int, nranks: int) -> None:
+        buf = C.create_string_buffer(unique_id, len(unique_id))
+        check(lib().sqlm_ctx_set_comm(self._h, buf, int(rank), int(nranks)), "sqlm_ctx_set_comm")
+
+    # ------------------------------------------------------------- results
+    def poses(self):
+        n = self.problem.n_pose
+        q, t = np.zeros((n, 4)), np.zeros((n, 3))
+        check(lib().sqlm_get_poses(self._h, ptr(q), ptr(t)), "sqlm_get_poses")
+        return q, t
+
+    def points(self):
+        X = np.zeros((self.problem.n_pt, 3))
+        check(lib().sqlm_get_points(self._h, ptr(X)), "sqlm_get_points")
+        return X
+
+    def edge_chi2(self):
+        out = np.zeros(self.problem.n_obs)
+        check(lib().sqlm_get_edge_chi2(self._h, ptr(out)), "sqlm_get_edge_chi2")
+        return out
+
+    def depth_positive(self):
+        out = np.zeros(self.problem.n_obs, np.uint8)
+        check(lib().sqlm_get_edge_depth_positive(self._h, ptr(out)), "sqlm_get_edge_depth_positive")
+        return out
+
+    def edge_level(self):
+        out = np.zeros(self.problem.n_obs, np.uint8)
+        check(lib().sqlm_get_edge_level(self._h, ptr(out)), "sqlm_get_edge_level")
+        return out
+
+
+def comm_unique_id() -> bytes:
+    n = lib().sqlm_comm_id_size()
+    buf = C.create_string_buffer(n)
+    check(lib().sqlm_comm_get_unique_id(buf), "sqlm_comm_get_unique_id")
+    return buf.raw
+
+
+def pose_from_Tcw_f32(T):
+    """Converter::toSE3Quat (src/utils/Converter.cc:55-68)."""
+    q, t = np.zeros(4), np.zeros(3)
+    lib().sqlm_pose_from_Tcw_f32(ptr(np.ascontiguousarray(T, np.float32).reshape(16)), ptr(q), ptr(t))
+    return q, t
+
+
+def pose_to_Tcw_f32(q, t):
+    """Converter::toCvMat(SE3Quat) (src/utils/Converter.cc:73-79,98-109)."""
+    T = np.zeros(16, np.float32)
+    lib().sqlm_pose_to_Tcw_f32(ptr(np.ascontiguousarray(q, np.float64)), ptr(np.ascontiguousarray(t, np.float64)),
+                               ptr(T))
+    return T.reshape(4, 4)
+
+
+@dataclass
+class LBAResult:
+    ran: bool
+    outlier: np.ndarray
+    stats: list
+
+
+class Optimizer:
+    """Static façade mirroring include/backend/Optimizer.h:42-71 (BA calls)."""
+
+    _ctx: Context | None = None
+
+    @classmethod
+    def _context(cls, ctx):
+        if ctx is not None:
+            return ctx
+        if cls._ctx is None:
+            cls._ctx = Context()
+        return cls._ctx
+
+    @staticmethod
+    def _write_back(ctx: Context, prob: BAProblem) -> None:
+        q, t = ctx.poses()
+        prob.pose_q[:] = q
+        prob.pose_t[:] = t
+        prob.pt[:] = ctx.points()
+
+    @classmethod
+    def LocalBundleAdjustment(cls, prob: BAProblem, stop_flag=None, ctx: Context | None = None) -> LBAResult:
+        """Local BA on an assembled local window (g2oOptimizer.cc:704-1191).
+        ``prob.obs_delta`` carries the pass-1 Huber deltas ((float)sqrt(5.991));
+        LiDAR flat edges in ``prob`` join in pass 3. Outlier tags returned are
+        the edges the reference erases (chi2 > 5.991 or depth <= 0)."""
+        c = cls._context(ctx)
+        c.set_problem(prob)
+        ran, outl, st = c.local_ba(stop_flag)
+        if ran:
+            cls._write_back(c, prob)
+        return LBAResult(bool(ran), outl, st)
+
+    @classmethod
+    def BundleAdjustment(cls, prob: BAProblem, nIterations: int = 5, stop_flag=None, nLoopKF: int = 0,
+                         bRobust: bool = True, ctx: Context | None = None):
+        """g2oOptimizer::BundleAdjustment (g2oOptimizer.cc:110-362): KF 0 fixed
+        (caller sets pose_fixed), Huber (float)sqrt(5.99) if bRobust."""
+        c = cls._context(ctx)
+        prob.obs_delta[:] = HUBER_MONO_GBA if bRobust else 0.0
+        c.set_problem(prob)
+        n, st = c.global_ba(nIterations, stop_flag)
+        cls._write_back(c, prob)
+        return n, st
+
+    @classmethod
+    def GlobalBundleAdjustemnt(cls, prob: BAProblem, nIterations: int = 5, stop_flag=None, nLoopKF: int = 0,
+                               bRobust: bool = True, ctx: Context | None = None):
+        """g2oOptimizer::GlobalBundleAdjustemnt (g2oOptimizer.cc:80-89)."""
+        return cls.BundleAdjustment(prob, nIterations, stop_flag, nLoopKF, bRobust, ctx)

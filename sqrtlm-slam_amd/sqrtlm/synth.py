@@ -1,0 +1,278 @@
+"""Synthetic KITTI-like bundle-adjustment problems.
+
+Portable and seeded: a counter-based SplitMix64 stream with Box–Muller normals,
+so the same seed gives the same problem on any host. Inputs are rounded to
+float32 exactly where the reference's are (keypoints ``cv::KeyPoint.pt``,
+``cv::Mat CV_32F`` poses and points, ``mvInvLevelSigma2``), then widened to
+double as ``Converter::toSE3Quat`` / ``toVector3d`` do (src/utils/Converter.cc:55-68,166-174).
+
+* intrinsics: KITTI-00 ``cfg/KITTI00-02.yaml:8-19`` (fx=fy=718.856, 1241x376);
+* trajectory: forward along camera +z at 1 m per keyframe, yaw 0.02 sin(i/10);
+* landmarks: back-projected from a pixel of the first observing keyframe at
+  depth U[5,40] m, observed by the following keyframes where they project;
+* octave ~ Geometric(0.5) clipped to [0,7], information ``invSigma2`` built in
+  float like ``ORBextractor`` (src/frontend/ORBextractor.cc:485-505), pixel
+  noise N(0, sigma2[octave]); a fraction of observations displaced 10-50 px;
+* initial guess: free poses perturbed N(0,(0.3 deg)^2) in rotation and
+  N(0,(0.05 m)^2) in translation, points N(0,(0.1 m)^2).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .problem import HUBER_MONO_GBA, HUBER_MONO_LBA, BAProblem
+
+KITTI_INTR = (718.856, 718.856, 607.1928, 185.2157)
+KITTI_WH = (1241, 376)
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+class SplitMix64:
+    """Counter-based SplitMix64: draw i = mix(seed + (i+1)*golden)."""
+
+    def __init__(self, seed: int):
+        self.seed = np.uint64(seed & 0xFFFFFFFFFFFFFFFF)
+        self.ctr = 0
+
+    def u64(self, n: int) -> np.ndarray:
+        with np.errstate(over="ignore"):
+            i = np.arange(self.ctr + 1, self.ctr + n + 1, dtype=np.uint64)
+            self.ctr += n
+            z = self.seed + i * _GOLDEN
+            z = (z ^ (z >> np.uint64(30))) * _M1
+            z = (z ^ (z >> np.uint64(27))) * _M2
+            return z ^ (z >> np.uint64(31))
+
+    def uniform(self, n: int) -> np.ndarray:
+        return (self.u64(n) >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+
+    def normal(self, n: int) -> np.ndarray:
+        u1 = 1.0 - self.uniform(n)  # (0,1]
+        u2 = self.uniform(n)
+        return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+    def integers(self, lo: int, hi: int, n: int) -> np.ndarray:
+        """Uniform integers in [lo, hi]."""
+        return lo + np.minimum((self.uniform(n) * (hi - lo + 1)).astype(np.int64), hi - lo)
+
+
+def orb_inv_level_sigma2(n_levels: int = 8, scale: float = 1.2) -> np.ndarray:
+    """mvInvLevelSigma2 computed in float as ORBextractor.cc:485-505."""
+    s = [np.float32(1.0)]
+    for _ in range(1, n_levels):
+        s.append(np.float32(s[-1] * np.float32(scale)))
+    sig2 = [np.float32(v * v) for v in s]
+    return np.array([np.float32(1.0) / v for v in sig2], np.float32)
+
+
+def _rot_y(a: np.ndarray) -> np.ndarray:
+    c, s = np.cos(a), np.sin(a)
+    R = np.zeros(a.shape + (3, 3))
+    R[..., 0, 0] = c; R[..., 0, 2] = s; R[..., 1, 1] = 1.0; R[..., 2, 0] = -s; R[..., 2, 2] = c
+    return R
+
+
+def _so3_exp(w: np.ndarray) -> np.ndarray:
+    th = np.linalg.norm(w, axis=-1)[..., None, None]
+    K = np.zeros(w.shape[:-1] + (3, 3))
+    K[..., 0, 1] = -w[..., 2]; K[..., 0, 2] = w[..., 1]
+    K[..., 1, 0] = w[..., 2]; K[..., 1, 2] = -w[..., 0]
+    K[..., 2, 0] = -w[..., 1]; K[..., 2, 1] = w[..., 0]
+    th_safe = np.where(th < 1e-12, 1.0, th)
+    a = np.where(th < 1e-12, 1.0, np.sin(th_safe) / th_safe)
+    b = np.where(th < 1e-12, 0.5, (1 - np.cos(th_safe)) / th_safe ** 2)
+    return np.eye(3) + a * K + b * (K @ K)
+
+
+def quat_from_mat(R: np.ndarray) -> np.ndarray:
+    """Eigen Quaterniond(Matrix3d) + SE3Quat::normalizeRotation, vectorised.
+    Returns (N,4) x,y,z,w."""
+    R = np.asarray(R, np.float64).reshape(-1, 3, 3)
+    q = np.zeros((R.shape[0], 4))
+    tr = (R[:, 0, 0] + R[:, 1, 1]) + R[:, 2, 2]
+    pos = tr > 0
+    if pos.any():
+        Rp = R[pos]
+        t = np.sqrt(tr[pos] + 1.0)
+        w = 0.5 * t
+        t = 0.5 / t
+        q[pos, 3] = w
+        q[pos, 0] = (Rp[:, 2, 1] - Rp[:, 1, 2]) * t
+        q[pos, 1] = (Rp[:, 0, 2] - Rp[:, 2, 0]) * t
+        q[pos, 2] = (Rp[:, 1, 0] - Rp[:, 0, 1]) * t
+    for n in np.nonzero(~pos)[0]:
+        m = R[n]
+        i = 0
+        if m[1, 1] > m[0, 0]:
+            i = 1
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+        q[n, i] = 0.5 * t
+        t = 0.5 / t
+        q[n, 3] = (m[k, j] - m[j, k]) * t
+        q[n, j] = (m[j, i] + m[i, j]) * t
+        q[n, k] = (m[k, i] + m[i, k]) * t
+    q[q[:, 3] < 0] *= -1.0
+    nrm = np.sqrt((q[:, 0] ** 2 + q[:, 2] ** 2) + (q[:, 1] ** 2 + q[:, 3] ** 2))
+    return q / nrm[:, None]
+
+
+def quat_to_mat(q: np.ndarray) -> np.ndarray:
+    q = np.asarray(q, np.float64).reshape(-1, 4)
+    x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    tx, ty, tz = 2 * x, 2 * y, 2 * z
+    R = np.empty((q.shape[0], 3, 3))
+    R[:, 0, 0] = 1 - (ty * y + tz * z); R[:, 0, 1] = ty * x - tz * w; R[:, 0, 2] = tz * x + ty * w
+    R[:, 1, 0] = ty * x + tz * w; R[:, 1, 1] = 1 - (tx * x + tz * z); R[:, 1, 2] = tz * y - tx * w
+    R[:, 2, 0] = tz * x - ty * w; R[:, 2, 1] = tz * y + tx * w; R[:, 2, 2] = 1 - (tx * x + ty * y)
+    return R
+
+
+def pose_through_f32(R: np.ndarray, t: np.ndarray):
+    """Round a pose through a CV_32F Tcw and back (Converter::toSE3Quat)."""
+    Rf = np.asarray(R, np.float32).astype(np.float64)
+    tf = np.asarray(t, np.float32).astype(np.float64)
+    return quat_from_mat(Rf), tf.reshape(-1, 3)
+
+
+def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_window: int = 0,
+                 n_fixed: int = 1, seed: int = 0, outlier_frac: float = 0.02, robust: bool = True,
+                 huber_delta: float | None = None, noise: bool = True, perturb: bool = True) -> BAProblem:
+    """Generate a synthetic BA problem.
+
+    pair_window > 0 selects the local-BA layout of config 2: every landmark has
+    exactly two observers, the second within ``pair_window`` keyframes of the
+    first. Otherwise k ~ U{k_min..k_max} consecutive keyframes (config 4)."""
+    rng = SplitMix64(seed)
+    fx, fy, cx, cy = KITTI_INTR
+    W, H = KITTI_WH
+    idx = np.arange(n_kf)
+    yaw = 0.02 * np.sin(idx / 10.0)
+    R_wc = _rot_y(yaw)
+    c = np.stack([np.zeros(n_kf), np.zeros(n_kf), idx * 1.0], axis=1)
+    R_cw = np.transpose(R_wc, (0, 2, 1))
+    t_cw = -np.einsum("nij,nj->ni", R_cw, c)
+
+    # landmark spans
+    if pair_window > 0:
+        k = np.full(n_lm, 2, np.int64)
+        a = rng.integers(0, n_kf - 1 - 1, n_lm)
+        off = rng.integers(1, pair_window, n_lm)
+        b = np.minimum(a + off, n_kf - 1)
+        span = b - a + 1
+    else:
+        k = rng.integers(k_min, k_max, n_lm)
+        k = np.minimum(k, n_kf)
+        a = (rng.uniform(n_lm) * (n_kf - k + 1)).astype(np.int64)
+        a = np.minimum(a, n_kf - k)
+        span = k
+    dmin = np.maximum(5.0, span + 3.0)
+    d = dmin + rng.uniform(n_lm) * (40.0 - dmin)
+    s = (d - (span - 1)) / d
+    xb = np.array([(0 - cx) / fx, (W - cx) / fx]) * 0.9
+    yb = np.array([(0 - cy) / fy, (H - cy) / fy]) * 0.9
+    xi = (xb[0] + rng.uniform(n_lm) * (xb[1] - xb[0])) * s
+    yi = (yb[0] + rng.uniform(n_lm) * (yb[1] - yb[0])) * s
+    pc = np.stack([xi * d, yi * d, d], axis=1)
+    X = np.einsum("nij,nj->ni", R_wc[a], pc) + c[a]
+
+    # observations
+    if pair_window > 0:
+        lm = np.repeat(np.arange(n_lm), 2)
+        kf = np.stack([a, b], axis=1).reshape(-1)
+    else:
+        lm = np.repeat(np.arange(n_lm), k)
+        starts = np.repeat(a, k)
+        first = np.repeat(np.cumsum(k) - k, k)
+        kf = starts + (np.arange(lm.size) - first)
+    Xc = np.einsum("nij,nj->ni", R_cw[kf], X[lm]) + t_cw[kf]
+    u = fx * Xc[:, 0] / Xc[:, 2] + cx
+    v = fy * Xc[:, 1] / Xc[:, 2] + cy
+    vis = (Xc[:, 2] > 0.5) & (u >= 0) & (u < W) & (v >= 0) & (v < H)
+    # keep landmarks with >= 2 visible observations
+    cnt = np.bincount(lm[vis], minlength=n_lm)
+    keep_lm = cnt >= 2
+    keep = vis & keep_lm[lm]
+    lm, kf, u, v = lm[keep], kf[keep], u[keep], v[keep]
+    remap = -np.ones(n_lm, np.int64)
+    remap[keep_lm] = np.arange(int(keep_lm.sum()))
+    lm = remap[lm]
+    X = X[keep_lm]
+    # sort landmarks by first observing keyframe (stable)
+    first_kf = np.full(X.shape[0], n_kf, np.int64)
+    np.minimum.at(first_kf, lm, kf)
+    order = np.argsort(first_kf, kind="stable")
+    inv = np.empty_like(order)
+    inv[order] = np.arange(order.size)
+    X = X[order]
+    lm = inv[lm]
+    o2 = np.lexsort((kf, lm))
+    lm, kf, u, v = lm[o2], kf[o2], u[o2], v[o2]
+    E = lm.size
+
+    # octaves, information, noise, outliers
+    uo = 1.0 - rng.uniform(E)
+    octave = np.minimum(np.floor(-np.log2(uo)).astype(np.int64), 7)
+    inv_s2 = orb_inv_level_sigma2()
+    info = inv_s2[octave].astype(np.float64)
+    sigma = np.sqrt((np.float32(1.0) / inv_s2[octave]).astype(np.float64))
+    if noise:
+        u = u + sigma * rng.normal(E)
+        v = v + sigma * rng.normal(E)
+        n_out = int(round(outlier_frac * E))
+        if n_out:
+            sel = np.unique(rng.integers(0, E - 1, n_out))
+            mag = 10.0 + rng.uniform(sel.size) * 40.0
+            ang = 2 * np.pi * rng.uniform(sel.size)
+            u[sel] += mag * np.cos(ang)
+            v[sel] += mag * np.sin(ang)
+    uv = np.stack([u, v], axis=1).astype(np.float32).astype(np.float64)
+
+    fixed = np.zeros(n_kf, np.uint8)
+    fixed[:max(1, n_fixed)] = 1
+    gt_q, gt_t = pose_through_f32(R_cw, t_cw)
+    gt_X = X.astype(np.float32).astype(np.float64)
+    R0, t0 = R_cw.copy(), t_cw.copy()
+    X0 = X.copy()
+    if perturb:
+        free = np.nonzero(fixed == 0)[0]
+        dth = rng.normal(3 * free.size).reshape(-1, 3) * np.deg2rad(0.3)
+        dt = rng.normal(3 * free.size).reshape(-1, 3) * 0.05
+        R0[free] = _so3_exp(dth) @ R0[free]
+        t0[free] = t0[free] + dt
+        X0 = X0 + rng.normal(3 * X0.shape[0]).reshape(-1, 3) * 0.1
+    q0, t0 = pose_through_f32(R0, t0)
+    X0 = X0.astype(np.float32).astype(np.float64)
+
+    if huber_delta is None:
+        huber_delta = HUBER_MONO_LBA if pair_window > 0 else HUBER_MONO_GBA
+    delta = np.full(E, huber_delta if robust else 0.0)
+    prob = BAProblem(
+        pose_q=q0, pose_t=t0, pose_fixed=fixed, intr=np.tile(np.array(KITTI_INTR), (n_kf, 1)),
+        pt=X0, obs_pose=kf.astype(np.int32), obs_pt=lm.astype(np.int32), obs_uv=uv, obs_info=info,
+        obs_delta=delta, obs_level=np.zeros(E, np.uint8),
+        meta=dict(gt_q=gt_q, gt_t=gt_t, gt_pt=gt_X, octave=octave, seed=seed),
+    )
+    return prob
+
+
+def config2(seed: int = 2, **kw) -> BAProblem:
+    """BASELINE config 2: synthetic local BA, 50 KF (10 fixed) x 5k landmarks x
+    200 obs/KF, k = 2, Huber (float)sqrt(5.991)."""
+    kw.setdefault("n_fixed", 10)
+    return make_problem(50, 5000, pair_window=5, seed=seed, robust=True, **kw)
+
+
+def config4(seed: int = 4, scale: float = 1.0, **kw) -> BAProblem:
+    """BASELINE config 4: synthetic global BA, 5k poses x 500k landmarks,
+    k ~ U{2..18} consecutive keyframes, KF0 fixed, no robust kernel
+    (LoopClosing.cc:987-991 passes bRobust=false). ``scale`` shrinks both
+    counts proportionally for parity-sized cases."""
+    n_kf = max(20, int(round(5000 * scale)))
+    n_lm = max(100, int(round(500000 * scale)))
+    kw.setdefault("robust", False)
+    return make_problem(n_kf, n_lm, k_min=2, k_max=18, n_fixed=1, seed=seed, **kw)
