@@ -65,6 +65,7 @@ struct sqlm_ctx {
   std::vector<int64_t> dev_lid_edge; // device lidar -> lidar edge id
   int max_row_blocks = 0;
   int n_active_edges = 0;
+  CRPlan cr;
   // ---- device memory ----
   std::vector<DevBuf> bufs;
   double *h_scalars = nullptr;  // pinned
@@ -113,7 +114,7 @@ enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
   B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS,
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
-  B_SCAL, B_MAXD, B_FLAGS
+  B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX
 };
 
 inline int seg_width(int k) {
@@ -236,6 +237,19 @@ int prepare(sqlm_ctx *c, int level) {
       mx = std::max(mx, (int)rows[i].size());
     }
     c->max_row_blocks = mx;
+    // block bandwidth in cameras -> superblock plan
+    int bw = 0;
+    for (int i = 0; i < nP; ++i)
+      for (int k = s_row[i]; k < s_row[i + 1]; ++k) bw = std::max(bw, s_col[k] - i);
+    c->cr = CRPlan{};
+    const int B = std::min(bw + 1, std::max(nP, 1));
+    const int n = (6 * B + 15) / 16 * 16;
+    if (n <= kCRMaxN) {
+      c->cr.enabled = true;
+      c->cr.B = B;
+      c->cr.p = (nP + B - 1) / B;
+      c->cr.n = n;
+    }
   }
   if (c->max_row_blocks > 128) return SQLM_ERR_UNSUPPORTED;
   // lidar edges grouped by free camera
@@ -316,7 +330,18 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_S, 36 * (size_t)d.nnzb, d.S);
   AL(B_G, 6 * (size_t)nP, d.g);
   AL(B_DX, 6 * (size_t)nP, d.dx);
-  AL(B_DENSE, (size_t)6 * nP * 6 * nP, d.dense);
+  if (c->cr.enabled) {
+    const size_t nb = (size_t)c->cr.p * c->cr.n * c->cr.n;
+    AL(B_CRD, nb, d.cr_D);
+    AL(B_CRE, nb, d.cr_E);
+    AL(B_CRA, nb, d.cr_A);
+    AL(B_CRC, nb, d.cr_C);
+    AL(B_CRG, (size_t)c->cr.p * c->cr.n, d.cr_g);
+    AL(B_CRX, (size_t)c->cr.p * c->cr.n, d.cr_x);
+  } else {
+    if ((size_t)6 * nP * sizeof(double) > 150 * 1024) return SQLM_ERR_UNSUPPORTED;
+    AL(B_DENSE, (size_t)6 * nP * 6 * nP, d.dense);
+  }
   AL(B_PART, (size_t)kMaxPartials, d.partials);
   AL(B_SCAL, (size_t)kNScalars, d.scalars);
   AL(B_MAXD, 1, d.maxdiag);
@@ -412,8 +437,8 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   int s = comm_allreduce_rcs(c->comm, d, lambda, c->stream);
   if (s) return s;
   tmark(c, 4, false);
-  s = launch_dense_solve(d, c->stream);
-  if (s) return s;
+  s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream) : launch_dense_solve(d, c->stream);
+  if (s) return s == -2 ? SQLM_ERR_HIP : SQLM_ERR_UNSUPPORTED;
   tmark(c, 4, true);
   tmark(c, 5, false);
   launch_pose_update(d, lambda, c->stream);

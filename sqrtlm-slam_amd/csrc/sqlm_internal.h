@@ -60,6 +60,10 @@ struct DevProblem {
   double *g = nullptr;                      // [6 nP]
   double *dx = nullptr;                     // [6 nP]
   double *dense = nullptr;                  // [n][n] dense workspace (upper)
+  // block-tridiagonal cyclic reduction workspace (sqlm_rcs_solve.hip)
+  double *cr_D = nullptr, *cr_E = nullptr;  // [p][n][n]
+  double *cr_A = nullptr, *cr_C = nullptr;  // [p][n][n]
+  double *cr_g = nullptr, *cr_x = nullptr;  // [p][n]
   // reductions
   double *partials = nullptr;               // [kMaxPartials]
   double *scalars = nullptr;                // [8] see Scalar
@@ -82,6 +86,14 @@ enum PartialRegion {
 constexpr int kMaxPartials = kPartEnd;
 constexpr int kMaxFreePoses = 131072;
 
+// Superblock plan of the reduced camera system: B cameras per superblock
+// (B = block bandwidth + 1), p superblocks of n = roundup(6B, 16) rows.
+struct CRPlan {
+  bool enabled = false;
+  int B = 0, p = 0, n = 0;
+};
+constexpr int kCRMaxN = 128;
+
 struct Bucket {
   int W;            // segment width
   int slot_begin;   // first landmark slot
@@ -96,6 +108,7 @@ void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
 void launch_damp(const DevProblem &d, double lambda, hipStream_t st);
 void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st);
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off,
                             hipStream_t st);

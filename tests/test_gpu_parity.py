@@ -68,3 +68,15 @@ def test_local_ba_schedule(gpu_ctx, oracle):
     _compare_state(gpu_ctx, ref)
     assert np.array_equal(out_g, out_r)
     assert np.array_equal(gpu_ctx.edge_level(), ref.obs_level)
+
+
+def test_global_ba_many_superblocks(gpu_ctx, oracle):
+    """250 poses, bandwidth 17 -> 14 superblocks, 4 cyclic-reduction levels."""
+    prob = synth.config4(scale=0.05, seed=11)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.global_ba(6)
+    gpu_ctx.set_problem(prob)
+    ng, sg = gpu_ctx.global_ba(6)
+    assert ng == nr
+    _compare_stats(sg, sr)
+    _compare_state(gpu_ctx, ref)
