@@ -66,6 +66,8 @@ struct sqlm_ctx {
   int max_row_blocks = 0;
   int n_active_edges = 0;
   CRPlan cr;
+  bool use_tiles = false;
+  int tile_max_cp = 0, tile_max_k = 0;
   // ---- device memory ----
   std::vector<DevBuf> bufs;
   double *h_scalars = nullptr;  // pinned
@@ -114,8 +116,100 @@ enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
   B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS,
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
-  B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX
+  B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
+  B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE
 };
+
+// Landmark tiles for the RCS assembly: runs of consecutive slots whose free
+// cameras fit a window of <= kTileMaxCams cameras (sorted), plus the reduction
+// lists that sum each S block / g row from its tiles in tile order.
+struct TilePlan {
+  std::vector<int> lm_ptr{0}, cam_ptr{0}, cams, obs_local, ld, red_ptr, gred_ptr;
+  std::vector<int2> urange, red_idx, gred_idx;
+  std::vector<int64_t> part_ptr{0}, gpart_ptr{0};
+  int max_cp = 0;
+  bool dups = false;
+};
+
+void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::vector<int> &obs_camh,
+                 const std::vector<int> &s_row, const std::vector<int> &s_col, TilePlan &tp) {
+  const int64_t nE = lm_begin[nL];
+  tp.obs_local.assign(nE, -1);
+  tp.urange.assign(nL, int2{-1, -1});
+  std::vector<int> stamp(nP, -1), lidx(nP, -1), lmst(nP, -1), cur, lcams;
+  std::vector<uint8_t> pst;
+  struct Red { int key, tile, code; };
+  std::vector<Red> red, gred;
+  int t = 0, cur_lm = 0, tile_start = 0;
+  auto close_tile = [&](int s_end) {
+    std::sort(cur.begin(), cur.end());
+    const int cp = (int)cur.size();
+    for (int u = 0; u < cp; ++u) lidx[cur[u]] = u;
+    pst.assign((size_t)cp * cp, 0);
+    for (int sl = tile_start; sl < s_end; ++sl) {
+      lcams.clear();
+      for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+        const int h = obs_camh[o];
+        tp.obs_local[o] = h >= 0 ? lidx[h] : -1;
+        if (h >= 0) lcams.push_back(lidx[h]);
+      }
+      if (lcams.empty()) continue;
+      std::sort(lcams.begin(), lcams.end());
+      lcams.erase(std::unique(lcams.begin(), lcams.end()), lcams.end());
+      tp.urange[sl] = int2{lcams.front(), lcams.back()};
+      for (size_t a = 0; a < lcams.size(); ++a)
+        for (size_t b = a; b < lcams.size(); ++b) pst[(size_t)lcams[a] * cp + lcams[b]] = 1;
+    }
+    for (int u = 0; u < cp; ++u)
+      for (int v = u; v < cp; ++v) {
+        if (!pst[(size_t)u * cp + v]) continue;
+        const int i = cur[u], j = cur[v];
+        const int *b0 = s_col.data() + s_row[i], *b1 = s_col.data() + s_row[i + 1];
+        const int sidx = (int)(std::lower_bound(b0, b1, j) - s_col.data());
+        red.push_back({sidx, t, (u << 8) | v});
+      }
+    for (int u = 0; u < cp; ++u) gred.push_back({cur[u], t, u});
+    const int ld = (6 * cp + 15) / 16 * 16;
+    tp.ld.push_back(ld);
+    tp.part_ptr.push_back(tp.part_ptr.back() + (int64_t)ld * ld);
+    tp.gpart_ptr.push_back(tp.gpart_ptr.back() + ld);
+    tp.cams.insert(tp.cams.end(), cur.begin(), cur.end());
+    tp.cam_ptr.push_back(tp.cam_ptr.back() + cp);
+    tp.lm_ptr.push_back(s_end);
+    tp.max_cp = std::max(tp.max_cp, cp);
+    ++t;
+    cur.clear();
+    cur_lm = 0;
+    tile_start = s_end;
+  };
+  for (int sl = 0; sl < nL; ++sl) {
+    int nnew = 0;
+    for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+      const int h = obs_camh[o];
+      if (h < 0) continue;
+      if (lmst[h] == sl) { tp.dups = true; continue; }
+      lmst[h] = sl;
+      if (stamp[h] != t) ++nnew;
+    }
+    if (cur_lm > 0 && ((int)cur.size() + nnew > kTileMaxCams || cur_lm >= kTileMaxLm)) close_tile(sl);
+    for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+      const int h = obs_camh[o];
+      if (h >= 0 && stamp[h] != t) { stamp[h] = t; cur.push_back(h); }
+    }
+    ++cur_lm;
+  }
+  if (cur_lm > 0) close_tile(nL);
+  auto csr = [](const std::vector<Red> &v, int nkeys, std::vector<int> &ptr, std::vector<int2> &idx) {
+    ptr.assign(nkeys + 1, 0);
+    for (auto &r : v) ptr[r.key + 1]++;
+    for (int k = 0; k < nkeys; ++k) ptr[k + 1] += ptr[k];
+    idx.resize(v.size());
+    std::vector<int> f(ptr.begin(), ptr.end() - 1);
+    for (auto &r : v) idx[f[r.key]++] = int2{r.tile, r.code};
+  };
+  csr(red, s_row[nP], tp.red_ptr, tp.red_idx);
+  csr(gred, nP, tp.gred_ptr, tp.gred_idx);
+}
 
 inline int seg_width(int k) {
   int w = 2;
@@ -251,7 +345,12 @@ int prepare(sqlm_ctx *c, int level) {
       c->cr.n = n;
     }
   }
-  if (c->max_row_blocks > 128) return SQLM_ERR_UNSUPPORTED;
+  TilePlan tp;
+  build_tiles(nP, nL, lm_begin, obs_camh, s_row, s_col, tp);
+  c->use_tiles = nP > 0 && tp.max_cp <= kTileHardCams;
+  c->tile_max_cp = tp.max_cp;
+  c->tile_max_k = 0;
+  if (!c->use_tiles && c->max_row_blocks > 128) return SQLM_ERR_UNSUPPORTED;
   // lidar edges grouped by free camera
   std::vector<int> lid_ptr(nP + 1, 0), lid_pose;
   std::vector<double> lid_data;
@@ -308,6 +407,25 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_LMB, 4 * (size_t)nL, d.lm_b);
   AL(B_LMM, 8 * (size_t)nL, d.lm_M);
   AL(B_LMV, 4 * (size_t)nL, d.lm_v);
+  AL(B_LMRP, 12 * (size_t)nL, d.lm_Rp);
+  d.n_tiles = c->use_tiles ? (int)tp.lm_ptr.size() - 1 : 0;
+  d.tile_dups = tp.dups ? 1 : 0;
+  if (c->use_tiles) {
+    UP(B_TLM, tp.lm_ptr, d.tile_lm_ptr);
+    UP(B_TCAMP, tp.cam_ptr, d.tile_cam_ptr);
+    UP(B_TCAMS, tp.cams, d.tile_cams);
+    UP(B_TPART, tp.part_ptr, d.tile_part_ptr);
+    UP(B_TGPART, tp.gpart_ptr, d.tile_gpart_ptr);
+    UP(B_TLD, tp.ld, d.tile_ld);
+    UP(B_URANGE, tp.urange, d.lm_urange);
+    UP(B_OBSLOC, tp.obs_local, d.obs_local);
+    AL(B_PART2, (size_t)tp.part_ptr.back(), d.part);
+    AL(B_GPART, (size_t)tp.gpart_ptr.back(), d.gpart);
+    UP(B_REDP, tp.red_ptr, d.red_ptr);
+    UP(B_REDI, tp.red_idx, d.red_idx);
+    UP(B_GREDP, tp.gred_ptr, d.gred_ptr);
+    UP(B_GREDI, tp.gred_idx, d.gred_idx);
+  }
   UP(B_OBSLM, obs_lm, d.obs_lm);
   UP(B_OBSCAM, obs_cam, d.obs_cam);
   UP(B_OBSCAMH, obs_camh, d.obs_camh);
@@ -432,7 +550,8 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   launch_damp(d, lambda, c->stream);
   tmark(c, 2, true);
   tmark(c, 3, false);
-  launch_rcs(d, lambda, c->max_row_blocks, c->stream);
+  if (c->use_tiles) launch_rcs_tiles(d, lambda, c->tile_max_cp, c->tile_max_k, c->stream);
+  else launch_rcs(d, lambda, c->max_row_blocks, c->stream);
   tmark(c, 3, true);
   int s = comm_allreduce_rcs(c->comm, d, lambda, c->stream);
   if (s) return s;

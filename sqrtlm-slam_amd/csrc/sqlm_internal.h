@@ -31,6 +31,7 @@ struct DevProblem {
   double *lm_b = nullptr;                   // [nL][4]  b_l = -J_l^T W r
   double *lm_M = nullptr;                   // [nL][8]  (H_ll + lambda I)^-1, sym (6)
   double *lm_v = nullptr;                   // [nL][4]  M b_l
+  double *lm_Rp = nullptr;                  // [nL][12] damped R' (6), w = R'^-T b_l (3)
   // observations
   int *obs_lm = nullptr;                    // [nE] landmark slot
   int *obs_cam = nullptr;                   // [nE] pose id
@@ -60,6 +61,23 @@ struct DevProblem {
   double *g = nullptr;                      // [6 nP]
   double *dx = nullptr;                     // [6 nP]
   double *dense = nullptr;                  // [n][n] dense workspace (upper)
+  // tiled RCS assembly (landmark tiles with a small camera window)
+  int n_tiles = 0;
+  int *tile_lm_ptr = nullptr;               // [T+1] landmark slot ranges
+  int *tile_cam_ptr = nullptr;              // [T+1] into tile_cams / g partials
+  int *tile_cams = nullptr;                 // free hidx, sorted within a tile
+  int64_t *tile_part_ptr = nullptr;         // [T+1] offset (doubles) of the tile's ld x ld partial
+  int64_t *tile_gpart_ptr = nullptr;        // [T+1] offset (doubles) of the tile's g partial
+  int *tile_ld = nullptr;                   // [T] 16 * ceil(6 cp / 16)
+  int2 *lm_urange = nullptr;                // [nL] local camera span (min, max), -1 if none free
+  int *obs_local = nullptr;                 // [nE] local camera index in its tile (-1 fixed)
+  double *part = nullptr;                   // tile partial Gram matrices
+  double *gpart = nullptr;                  // tile partial g
+  int *red_ptr = nullptr;                   // [nnzb+1] S block -> contributions
+  int2 *red_idx = nullptr;                  //   (tile, u << 8 | v)
+  int *gred_ptr = nullptr;                  // [nP+1] camera -> contributions
+  int2 *gred_idx = nullptr;                 //   (tile, u)
+  int tile_dups = 0;                        // some landmark observed twice by one camera
   // block-tridiagonal cyclic reduction workspace (sqlm_rcs_solve.hip)
   double *cr_D = nullptr, *cr_E = nullptr;  // [p][n][n]
   double *cr_A = nullptr, *cr_C = nullptr;  // [p][n][n]
@@ -92,7 +110,7 @@ struct CRPlan {
   bool enabled = false;
   int B = 0, p = 0, n = 0;
 };
-constexpr int kCRMaxN = 128;
+constexpr int kCRMaxN = 112;  // LDS: L (n x n+1) + Dinv (16n) + W (16n) <= 160 KiB
 
 struct Bucket {
   int W;            // segment width
@@ -107,6 +125,8 @@ void launch_camera_pass(const DevProblem &d, hipStream_t st);
 void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
 void launch_damp(const DevProblem &d, double lambda, hipStream_t st);
 void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st);
+void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st);
+constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);

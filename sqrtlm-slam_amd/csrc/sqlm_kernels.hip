@@ -402,6 +402,13 @@ __global__ void k_damp(DevProblem d, double lambda) {
   double *M = d.lm_M + 8 * l;
   store2(M, m00, m01); store2(M + 2, m02, m11); store2(M + 4, m12, m22);
   const double *bl = d.lm_b + 4 * l;
+  // w = R'^-T b_l (forward substitution with the lower factor R'^T)
+  const double w0 = bl[0] / R[0];
+  const double w1 = (bl[1] - R[1] * w0) / R[3];
+  const double w2 = (bl[2] - R[2] * w0 - R[4] * w1) / R[5];
+  double *Rp = d.lm_Rp + 12 * l;
+  store2(Rp, R[0], R[1]); store2(Rp + 2, R[2], R[3]); store2(Rp + 4, R[4], R[5]);
+  store2(Rp + 6, w0, w1); store2(Rp + 8, w2, 0.0);
   const double v0 = m00 * bl[0] + m01 * bl[1] + m02 * bl[2];
   const double v1 = m01 * bl[0] + m11 * bl[1] + m12 * bl[2];
   const double v2 = m02 * bl[0] + m12 * bl[1] + m22 * bl[2];
@@ -498,6 +505,163 @@ void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStrea
   const size_t lds = (size_t)4 * max_row_blocks * 36 * sizeof(double) + 32 * sizeof(double) +
                      (size_t)max_row_blocks * sizeof(int) + 16;
   hipLaunchKernelGGL(k_rcs, dim3(d.nP), dim3(256), lds, st, d, lambda, max_row_blocks);
+}
+
+// Tiled RCS on the FP64 matrix cores. With Y_o = R'^-T P_o (3x6 per
+// observation) and w_l = R'^-T b_l:
+//   S_ij = H_pp,i d_ij + lambda I d_ij - sum_l Y_li^T Y_lj,  g_i = b_p,i - sum_l Y_li^T w_l.
+// A tile is a run of consecutive landmark slots whose free cameras form a small
+// sorted window C_t (|C_t| <= 24, 6|C_t| <= 144 columns). ONE wavefront owns a
+// tile: per landmark it stages the dense 3 x 6|C_t| row block Y_l (plus a zero
+// 4th row) in LDS and accumulates G_t += Y_l^T Y_l with v_mfma_f64_16x16x4_f64
+// into NT(NT+1)/2 upper 16x16 accumulator tiles held in AGPRs, skipping the
+// tiles outside the landmark's column span. Single-wave ownership means no
+// atomics and a fixed summation order (bitwise deterministic).
+typedef double d4v __attribute__((ext_vector_type(4)));
+
+template <int NT>
+__global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
+  // two waves per tile: wave w owns the accumulator tiles q with q % 2 == w
+  constexpr int NQ = NT * (NT + 1) / 2, NQW = (NQ + 1) / 2, NC = NT * 16, NG = (NC + 127) / 128;
+  __shared__ double Ys[4][NC];
+  const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
+  const int ncol = 6 * cp, nt = (ncol + 15) >> 4, ld = nt * 16;
+  const int r16 = lane & 15, k4 = lane >> 4;
+  d4v acc[NQW];
+#pragma unroll
+  for (int q = 0; q < NQW; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
+  double gacc[NG];
+#pragma unroll
+  for (int m = 0; m < NG; ++m) gacc[m] = 0.0;
+  for (int k = tid; k < 4 * NC; k += 128) (&Ys[0][0])[k] = 0.0;
+  __syncthreads();
+  for (int l = d.tile_lm_ptr[t]; l < d.tile_lm_ptr[t + 1]; ++l) {
+    const int2 ur = d.lm_urange[l];  // local camera span of the landmark (-1 if none free)
+    if (ur.x < 0) continue;
+    const int beg = d.lm_begin[l], k = d.lm_begin[l + 1] - beg;
+    const double *Rp = d.lm_Rp + 12 * l;
+    const double r00 = Rp[0], r01 = Rp[1], r02 = Rp[2], r11 = Rp[3], r12 = Rp[4], r22 = Rp[5];
+    const double w0 = Rp[6], w1 = Rp[7], w2 = Rp[8];
+    const int c0 = 6 * ur.x, c1 = 6 * ur.y + 6;  // nonzero column range [c0, c1)
+    // stage Y columns (observations of one camera summed in observation order)
+    if (d.tile_dups) {
+      if (tid < 6)
+        for (int j = 0; j < k; ++j) {
+          const int u = d.obs_local[beg + j];
+          if (u < 0) continue;
+          const double *P = d.obs_P + 18 * (size_t)(beg + j);
+          const double y0 = P[tid] / r00;
+          const double y1 = (P[6 + tid] - r01 * y0) / r11;
+          const double y2 = (P[12 + tid] - r02 * y0 - r12 * y1) / r22;
+          Ys[0][6 * u + tid] += y0; Ys[1][6 * u + tid] += y1; Ys[2][6 * u + tid] += y2;
+        }
+    } else {
+      for (int it = tid; it < k * 6; it += 128) {
+        const int j = it / 6, c = it - 6 * j;
+        const int u = d.obs_local[beg + j];
+        if (u < 0) continue;
+        const double *P = d.obs_P + 18 * (size_t)(beg + j);
+        const double y0 = P[c] / r00;
+        const double y1 = (P[6 + c] - r01 * y0) / r11;
+        const double y2 = (P[12 + c] - r02 * y0 - r12 * y1) / r22;
+        Ys[0][6 * u + c] = y0; Ys[1][6 * u + c] = y1; Ys[2][6 * u + c] = y2;
+      }
+    }
+    __syncthreads();
+    const int tmin = c0 >> 4, tmax = (c1 - 1) >> 4;
+    int q = 0;
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+#pragma unroll
+      for (int tj = ti; tj < NT; ++tj, ++q) {
+        if ((q & 1) == wave && ti >= tmin && tj <= tmax) {
+          const double a = Ys[k4][ti * 16 + r16];
+          const double b = Ys[k4][tj * 16 + r16];
+          acc[q >> 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[q >> 1], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < NG; ++m) {
+      const int col = tid + 128 * m;
+      if (col < NC) gacc[m] -= Ys[0][col] * w0 + Ys[1][col] * w1 + Ys[2][col] * w2;
+    }
+    __syncthreads();
+    for (int it = tid; it < 3 * (c1 - c0); it += 128) {  // clear this landmark's columns
+      const int row = it / (c1 - c0), col = c0 + it % (c1 - c0);
+      Ys[row][col] = 0.0;
+    }
+    __syncthreads();
+  }
+  // write -G_t (upper tiles) as the tile's partial, ld = 16 nt
+  double *out = d.part + d.tile_part_ptr[t];
+  int q = 0;
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+    for (int tj = ti; tj < NT; ++tj, ++q) {
+      if ((q & 1) == wave && tj < nt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) out[(size_t)(ti * 16 + k4 + 4 * j) * ld + tj * 16 + r16] = -acc[q >> 1][j];
+      }
+    }
+  double *go = d.gpart + d.tile_gpart_ptr[t];
+#pragma unroll
+  for (int m = 0; m < NG; ++m) {
+    const int col = tid + 128 * m;
+    if (col < ncol) go[col] = gacc[m];
+  }
+}
+
+// S block s = sum of its tile partials (tile order) + H_pp + lambda I on the
+// diagonal; g row i likewise. Partials are symmetric: entries that fall in a
+// lower 16x16 tile are read from their transpose.
+__global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool own = !d.sharded || d.rank == 0;
+  if (gid < d.nnzb * 36) {
+    const int s = (int)(gid / 36), e = (int)(gid % 36), r = e / 6, c = e % 6;
+    double v = 0.0;
+    for (int k = d.red_ptr[s]; k < d.red_ptr[s + 1]; ++k) {
+      const int2 ct = d.red_idx[k];
+      const int u = ct.y >> 8, w = ct.y & 255;
+      const int ld = d.tile_ld[ct.x];
+      int R = 6 * u + r, C = 6 * w + c;
+      if ((R >> 4) > (C >> 4)) { const int tmp = R; R = C; C = tmp; }
+      v += d.part[d.tile_part_ptr[ct.x] + (int64_t)R * ld + C];
+    }
+    const int j = d.s_col[s];
+    if (own && s == d.s_row_ptr[j]) {  // diagonal block (first block of row j)
+      v += d.Hpp[36 * j + e];
+      if (r == c) v += lambda;
+    }
+    d.S[gid] = v;
+  }
+  const int64_t g2 = gid - d.nnzb * 36;
+  if (g2 >= 0 && g2 < (int64_t)d.nP * 6) {
+    const int i = (int)(g2 / 6), r = (int)(g2 % 6);
+    double v = 0.0;
+    for (int k = d.gred_ptr[i]; k < d.gred_ptr[i + 1]; ++k) {
+      const int2 ct = d.gred_idx[k];
+      v += d.gpart[d.tile_gpart_ptr[ct.x] + 6 * ct.y + r];
+    }
+    d.g[6 * i + r] = (own ? d.bp[8 * i + r] : 0.0) + v;
+  }
+}
+
+void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st) {
+  if (d.nP == 0) return;
+  (void)max_k;
+  const int nt = (6 * max_cp + 15) / 16;
+  if (d.n_tiles > 0) {
+    if (nt <= 3) hipLaunchKernelGGL(k_rcs_tile<3>, dim3(d.n_tiles), dim3(128), 0, st, d);
+    else if (nt <= 5) hipLaunchKernelGGL(k_rcs_tile<5>, dim3(d.n_tiles), dim3(128), 0, st, d);
+    else if (nt <= 7) hipLaunchKernelGGL(k_rcs_tile<7>, dim3(d.n_tiles), dim3(128), 0, st, d);
+    else hipLaunchKernelGGL(k_rcs_tile<9>, dim3(d.n_tiles), dim3(128), 0, st, d);
+  }
+  const int64_t items = d.nnzb * 36 + (int64_t)d.nP * 6;
+  hipLaunchKernelGGL(k_rcs_reduce, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, d, lambda);
 }
 
 // ---------------------------------------------------------------- dense solve

@@ -276,3 +276,29 @@ def config4(seed: int = 4, scale: float = 1.0, **kw) -> BAProblem:
     n_lm = max(100, int(round(500000 * scale)))
     kw.setdefault("robust", False)
     return make_problem(n_kf, n_lm, k_min=2, k_max=18, n_fixed=1, seed=seed, **kw)
+
+
+def add_lidar_flat(prob: BAProblem, pose: int, n: int, *, seed: int = 0, noise: float = 0.01,
+                   weight: float = 50.0) -> BAProblem:
+    """Attach ``n`` EdgeLidarFlatPoint unary edges to ``pose`` (the current KF of
+    local-BA pass 3, g2oOptimizer.cc:1034-1070): a current-frame point p_c with
+    its plane normal n_c and a map point p_w on the same plane, so that
+    e = (T_cw p_w - p_c) . n_c is zero at the ground-truth pose up to ``noise``.
+    Information = flat_optimized_weight (cfg/lidar_slam.yaml:58)."""
+    rng = SplitMix64(seed ^ 0x5EED)
+    gq, gt = prob.meta["gt_q"][pose], prob.meta["gt_t"][pose]
+    R = quat_to_mat(gq)[0]
+    nrm = rng.normal(3 * n).reshape(-1, 3)
+    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+    pc = np.stack([rng.uniform(n) * 20 - 10, rng.uniform(n) * 4 - 2, 2 + rng.uniform(n) * 30], axis=1)
+    tang = rng.normal(3 * n).reshape(-1, 3) * 0.3
+    tang -= np.sum(tang * nrm, axis=1, keepdims=True) * nrm
+    on_plane = pc + tang + noise * rng.normal(n)[:, None] * nrm
+    pw = (on_plane - gt) @ R  # R^T (p - t)
+    prob.lid_pose = np.full(n, pose, np.int32)
+    prob.lid_pc = pc.astype(np.float32).astype(np.float64)
+    prob.lid_pw = pw.astype(np.float32).astype(np.float64)
+    prob.lid_n = nrm.astype(np.float32).astype(np.float64)
+    prob.lid_info = np.full(n, weight)
+    prob.validate()
+    return prob
