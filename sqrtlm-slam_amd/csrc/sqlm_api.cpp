@@ -410,6 +410,11 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_LMRP, 12 * (size_t)nL, d.lm_Rp);
   d.n_tiles = c->use_tiles ? (int)tp.lm_ptr.size() - 1 : 0;
   d.tile_dups = tp.dups ? 1 : 0;
+  {
+    int mk = 0;
+    for (int sl = 0; sl < nL; ++sl) mk = std::max(mk, lm_begin[sl + 1] - lm_begin[sl]);
+    d.tile_maxk = mk;
+  }
   if (c->use_tiles) {
     UP(B_TLM, tp.lm_ptr, d.tile_lm_ptr);
     UP(B_TCAMP, tp.cam_ptr, d.tile_cam_ptr);

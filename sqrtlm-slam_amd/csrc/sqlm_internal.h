@@ -78,6 +78,7 @@ struct DevProblem {
   int *gred_ptr = nullptr;                  // [nP+1] camera -> contributions
   int2 *gred_idx = nullptr;                 //   (tile, u)
   int tile_dups = 0;                        // some landmark observed twice by one camera
+  int tile_maxk = 0;                        // longest track (staging fast path needs <= 21)
   // block-tridiagonal cyclic reduction workspace (sqlm_rcs_solve.hip)
   double *cr_D = nullptr, *cr_E = nullptr;  // [p][n][n]
   double *cr_A = nullptr, *cr_C = nullptr;  // [p][n][n]

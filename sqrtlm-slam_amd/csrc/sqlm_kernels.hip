@@ -519,11 +519,21 @@ void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStrea
 // atomics and a fixed summation order (bitwise deterministic).
 typedef double d4v __attribute__((ext_vector_type(4)));
 
+// Landmarks are consumed in batches of 4: landmark li of a batch occupies rows
+// 4li..4li+2 of the staged block (row 4li+3 stays zero), i.e. exactly one
+// K=4 step of v_mfma_f64_16x16x4_f64, so one batch = 4 K-steps per 16x16 tile.
+// The raw P columns of the next batch are prefetched into registers while the
+// current batch runs on the matrix cores.
+constexpr int kTileBL = 4, kTileIPT = 4;  // fast path: k <= 128 * 4 / (6 * 4) = 21
+
 template <int NT>
 __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
   // two waves per tile: wave w owns the accumulator tiles q with q % 2 == w
   constexpr int NQ = NT * (NT + 1) / 2, NQW = (NQ + 1) / 2, NC = NT * 16, NG = (NC + 127) / 128;
-  __shared__ double Ys[4][NC];
+  constexpr int BL = kTileBL, IPT = kTileIPT;
+  __shared__ double Ys[2][4 * BL][NC];
+  __shared__ double Ws[2][BL][4];
+  __shared__ int2 Us[2][BL];
   const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
   const int ncol = 6 * cp, nt = (ncol + 15) >> 4, ld = nt * 16;
@@ -534,65 +544,113 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
   double gacc[NG];
 #pragma unroll
   for (int m = 0; m < NG; ++m) gacc[m] = 0.0;
-  for (int k = tid; k < 4 * NC; k += 128) (&Ys[0][0])[k] = 0.0;
+  for (int k = tid; k < 2 * 4 * BL * NC; k += 128) (&Ys[0][0][0])[k] = 0.0;
+  const int l0 = d.tile_lm_ptr[t], l1 = d.tile_lm_ptr[t + 1];
+  const int nbatch = (l1 - l0 + BL - 1) / BL;
+  const bool slow = d.tile_dups || d.tile_maxk > 21;
+  // prefetched raw inputs of one batch (fast path)
+  double pp[IPT][3];
+  int pu[IPT], pli[IPT], pc[IPT];
+  auto fetch = [&](int bt) {
+    const int lb = l0 + BL * bt, nl = min(BL, l1 - lb);
+    const int b0 = d.lm_begin[lb], bn = d.lm_begin[lb + nl];
+    const int e1 = nl > 1 ? d.lm_begin[lb + 1] : bn, e2 = nl > 2 ? d.lm_begin[lb + 2] : bn,
+              e3 = nl > 3 ? d.lm_begin[lb + 3] : bn;
+#pragma unroll
+    for (int m = 0; m < IPT; ++m) {
+      const int it = tid + 128 * m, o = b0 + it / 6;
+      pu[m] = -1;
+      if (!slow && o < bn) {
+        pli[m] = (o >= e1) + (o >= e2) + (o >= e3);
+        pc[m] = it % 6;
+        pu[m] = d.obs_local[o];
+        const double *P = d.obs_P + 18 * (size_t)o;
+        pp[m][0] = P[pc[m]]; pp[m][1] = P[6 + pc[m]]; pp[m][2] = P[12 + pc[m]];
+      }
+    }
+  };
+  if (nbatch > 0) fetch(0);
+  int2 prev = int2{-1, -1};
   __syncthreads();
-  for (int l = d.tile_lm_ptr[t]; l < d.tile_lm_ptr[t + 1]; ++l) {
-    const int2 ur = d.lm_urange[l];  // local camera span of the landmark (-1 if none free)
-    if (ur.x < 0) continue;
-    const int beg = d.lm_begin[l], k = d.lm_begin[l + 1] - beg;
-    const double *Rp = d.lm_Rp + 12 * l;
-    const double r00 = Rp[0], r01 = Rp[1], r02 = Rp[2], r11 = Rp[3], r12 = Rp[4], r22 = Rp[5];
-    const double w0 = Rp[6], w1 = Rp[7], w2 = Rp[8];
-    const int c0 = 6 * ur.x, c1 = 6 * ur.y + 6;  // nonzero column range [c0, c1)
-    // stage Y columns (observations of one camera summed in observation order)
-    if (d.tile_dups) {
-      if (tid < 6)
-        for (int j = 0; j < k; ++j) {
-          const int u = d.obs_local[beg + j];
+  for (int bt = 0; bt < nbatch; ++bt) {
+    const int buf = bt & 1, lb = l0 + BL * bt, nl = min(BL, l1 - lb);
+    double (*Y)[NC] = Ys[buf];
+    if (tid < nl) Us[buf][tid] = d.lm_urange[lb + tid];
+    if (tid < 3 * nl) Ws[buf][tid / 3][tid % 3] = d.lm_Rp[12 * (lb + tid / 3) + 6 + tid % 3];
+    // ---- stage Y rows 4li..4li+2 = R'^-T P for every landmark li of the batch
+    if (!slow) {
+#pragma unroll
+      for (int m = 0; m < IPT; ++m) {
+        if (pu[m] >= 0) {
+          const double *Rp = d.lm_Rp + 12 * (lb + pli[m]);
+          const double y0 = pp[m][0] / Rp[0];
+          const double y1 = (pp[m][1] - Rp[1] * y0) / Rp[3];
+          const double y2 = (pp[m][2] - Rp[2] * y0 - Rp[4] * y1) / Rp[5];
+          const int col = 6 * pu[m] + pc[m], row = 4 * pli[m];
+          Y[row][col] = y0; Y[row + 1][col] = y1; Y[row + 2][col] = y2;
+        }
+      }
+    } else if (tid < 6) {  // repeated cameras / long tracks: serial, observation order
+      for (int li = 0; li < nl; ++li) {
+        const int l = lb + li;
+        const double *Rp = d.lm_Rp + 12 * l;
+        for (int o = d.lm_begin[l]; o < d.lm_begin[l + 1]; ++o) {
+          const int u = d.obs_local[o];
           if (u < 0) continue;
-          const double *P = d.obs_P + 18 * (size_t)(beg + j);
-          const double y0 = P[tid] / r00;
-          const double y1 = (P[6 + tid] - r01 * y0) / r11;
-          const double y2 = (P[12 + tid] - r02 * y0 - r12 * y1) / r22;
-          Ys[0][6 * u + tid] += y0; Ys[1][6 * u + tid] += y1; Ys[2][6 * u + tid] += y2;
+          const double *P = d.obs_P + 18 * (size_t)o;
+          const double y0 = P[tid] / Rp[0];
+          const double y1 = (P[6 + tid] - Rp[1] * y0) / Rp[3];
+          const double y2 = (P[12 + tid] - Rp[2] * y0 - Rp[4] * y1) / Rp[5];
+          Y[4 * li][6 * u + tid] += y0; Y[4 * li + 1][6 * u + tid] += y1; Y[4 * li + 2][6 * u + tid] += y2;
         }
+      }
+    }
+    __syncthreads();  // (A) batch staged; every thread is done with the previous batch
+    if (bt + 1 < nbatch) fetch(bt + 1);  // in flight during the MFMAs below
+    if (prev.x >= 0) {  // clear the previous batch's columns in the other buffer
+      const int c0 = prev.x, w = prev.y - prev.x;
+      for (int it = tid; it < 4 * BL * w; it += 128) Ys[buf ^ 1][it / w][c0 + it % w] = 0.0;
+    }
+    int cmin = 1 << 30, cmax = -1;
+    for (int li = 0; li < nl; ++li) {
+      const int2 ur = Us[buf][li];
+      if (ur.x >= 0) { cmin = min(cmin, 6 * ur.x); cmax = max(cmax, 6 * ur.y + 6); }
+    }
+    if (cmax > 0) {
+      const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
+      int q = 0;
+#pragma unroll
+      for (int ti = 0; ti < NT; ++ti) {
+#pragma unroll
+        for (int tj = ti; tj < NT; ++tj, ++q) {
+          if ((q & 1) == wave && ti >= tmin && tj <= tmax) {
+#pragma unroll
+            for (int ks = 0; ks < BL; ++ks) {
+              if (ks < nl) {
+                const double a = Y[4 * ks + k4][ti * 16 + r16];
+                const double bb = Y[4 * ks + k4][tj * 16 + r16];
+                acc[q >> 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc[q >> 1], 0, 0, 0);
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < NG; ++m) {
+        const int col = tid + 128 * m;
+        if (col >= cmin && col < cmax) {
+          double gs = 0.0;
+          for (int li = 0; li < nl; ++li)
+            gs += Y[4 * li][col] * Ws[buf][li][0] + Y[4 * li + 1][col] * Ws[buf][li][1] +
+                  Y[4 * li + 2][col] * Ws[buf][li][2];
+          gacc[m] -= gs;
+        }
+      }
+      prev = int2{cmin, cmax};
     } else {
-      for (int it = tid; it < k * 6; it += 128) {
-        const int j = it / 6, c = it - 6 * j;
-        const int u = d.obs_local[beg + j];
-        if (u < 0) continue;
-        const double *P = d.obs_P + 18 * (size_t)(beg + j);
-        const double y0 = P[c] / r00;
-        const double y1 = (P[6 + c] - r01 * y0) / r11;
-        const double y2 = (P[12 + c] - r02 * y0 - r12 * y1) / r22;
-        Ys[0][6 * u + c] = y0; Ys[1][6 * u + c] = y1; Ys[2][6 * u + c] = y2;
-      }
+      prev = int2{-1, -1};
     }
-    __syncthreads();
-    const int tmin = c0 >> 4, tmax = (c1 - 1) >> 4;
-    int q = 0;
-#pragma unroll
-    for (int ti = 0; ti < NT; ++ti) {
-#pragma unroll
-      for (int tj = ti; tj < NT; ++tj, ++q) {
-        if ((q & 1) == wave && ti >= tmin && tj <= tmax) {
-          const double a = Ys[k4][ti * 16 + r16];
-          const double b = Ys[k4][tj * 16 + r16];
-          acc[q >> 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[q >> 1], 0, 0, 0);
-        }
-      }
-    }
-#pragma unroll
-    for (int m = 0; m < NG; ++m) {
-      const int col = tid + 128 * m;
-      if (col < NC) gacc[m] -= Ys[0][col] * w0 + Ys[1][col] * w1 + Ys[2][col] * w2;
-    }
-    __syncthreads();
-    for (int it = tid; it < 3 * (c1 - c0); it += 128) {  // clear this landmark's columns
-      const int row = it / (c1 - c0), col = c0 + it % (c1 - c0);
-      Ys[row][col] = 0.0;
-    }
-    __syncthreads();
+    __syncthreads();  // (B) the other buffer is clear before it is staged
   }
   // write -G_t (upper tiles) as the tile's partial, ld = 16 nt
   double *out = d.part + d.tile_part_ptr[t];

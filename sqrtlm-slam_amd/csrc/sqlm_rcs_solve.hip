@@ -254,43 +254,110 @@ __global__ __launch_bounds__(256) void k_cr_scatter(DevProblem d, CRView v) {
   if (i == 0 && threadIdx.x == 0) v.flags[0] = 1;
 }
 
-// Level h: every odd superblock I (I = h, 3h, 5h, ...) is eliminated:
-// Linv = chol(D_I)^-1, A_I = Linv S(I, I-h), C_I = Linv S(I, I+h), z_I = Linv g_I.
-__global__ __launch_bounds__(512) void k_cr_elim(CRView v, int h) {
+// Level h, step 1: every odd superblock I (I = h, 3h, 5h, ...) is factored:
+// D_I <- Linv_I = chol(D_I)^-1 (in place), g_I <- z_I = Linv_I g_I.
+__global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int fail;
   const int I = h + 2 * h * blockIdx.x, n = v.n, ld = n + 1;
   double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n, *W = Dinv + 16 * n;
   double *Dg = blk(v.D, I, n);
   for (int k = threadIdx.x; k < n * n; k += blockDim.x) L[(k / n) * ld + k % n] = Dg[k];
+  for (int k = threadIdx.x; k < n; k += blockDim.x) tmp[k] = v.g[(size_t)I * n + k];
   __syncthreads();
   if (!wg_potrf_trtri(L, ld, n, Dinv, W, &fail) && threadIdx.x == 0) v.flags[0] = 0;
   for (int k = threadIdx.x; k < n * n; k += blockDim.x) Dg[k] = L[(k / n) * ld + k % n];
-  // S(I, I-h) = E_{I-h}^T
-  wg_gemm<false, true, kCRMaxN>(blk(v.A, I, n), n, L, ld, blk(v.E, I - h, n), n, n, 1.0, 0.0);
-  if (I + h < v.p) wg_gemm<false, false, kCRMaxN>(blk(v.C, I, n), n, L, ld, blk(v.E, I, n), n, n, 1.0, 0.0);
-  __syncthreads();
-  for (int k = threadIdx.x; k < n; k += blockDim.x) tmp[k] = v.g[(size_t)I * n + k];
-  __syncthreads();
   wg_gemv<false>(v.g + (size_t)I * n, L, ld, tmp, n, 1.0, 0.0);
 }
 
-// Level h: every even superblock J absorbs its eliminated neighbours:
+// One wavefront computes one 16x16 tile C[ti][tj] (+)= alpha * op(A) op(B) over K = n,
+// skipping K blocks that are zero because A is lower triangular (LA) or
+// A^T is upper triangular... (lower-triangular A used un-transposed only).
+template <bool TA, bool TB, bool LA>
+__device__ __forceinline__ d4 tile_gemm(const double *A, const double *B, int n, int ti, int tj) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  const int ar = ti * 16 + r16, bc = tj * 16 + r16;
+  const int kend = LA ? 16 * (ti + 1) : n;
+  double av[kCRMaxN / 4], bv[kCRMaxN / 4];
+#pragma unroll
+  for (int s = 0; s < kCRMaxN / 4; ++s) {
+    const int k = 4 * s + k4;
+    if (4 * s < kend) {
+      av[s] = TA ? A[k * n + ar] : A[ar * n + k];
+      bv[s] = TB ? B[bc * n + k] : B[k * n + bc];
+    }
+  }
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < kCRMaxN / 4; ++s)
+    if (4 * s < kend) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ void tile_store(double *C, int n, int ti, int tj, const d4 &acc, double alpha,
+                                           bool accumulate) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double *c = C + (ti * 16 + k4 + 4 * j) * n + tj * 16 + r16;
+    *c = accumulate ? *c + alpha * acc[j] : alpha * acc[j];
+  }
+}
+
+// Level h, step 2: A_I = Linv_I S(I, I-h) = Linv_I E_{I-h}^T and
+// C_I = Linv_I S(I, I+h) = Linv_I E_I, one 16x16 tile per wavefront.
+__global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h) {
+  const int n = v.n, nt = n >> 4, per = nt * nt;
+  const int odd = blockIdx.x / (2 * per), rem = blockIdx.x - odd * 2 * per;
+  const int which = rem / per, t = rem - which * per, ti = t / nt, tj = t - ti * nt;
+  const int I = h + 2 * h * odd;
+  if (which == 0) {
+    const d4 acc = tile_gemm<false, true, true>(blk(v.D, I, n), blk(v.E, I - h, n), n, ti, tj);
+    tile_store(blk(v.A, I, n), n, ti, tj, acc, 1.0, false);
+  } else if (I + h < v.p) {
+    const d4 acc = tile_gemm<false, false, true>(blk(v.D, I, n), blk(v.E, I, n), n, ti, tj);
+    tile_store(blk(v.C, I, n), n, ti, tj, acc, 1.0, false);
+  }
+}
+
+// Level h, step 3: every even superblock J absorbs its eliminated neighbours:
 // D_J -= A_{J+h}^T A_{J+h} + C_{J-h}^T C_{J-h};  E_J = -A_{J+h}^T C_{J+h};
-// g_J -= A_{J+h}^T z_{J+h} + C_{J-h}^T z_{J-h}.
-__global__ __launch_bounds__(512) void k_cr_update(CRView v, int h) {
-  const int J = 2 * h * blockIdx.x, n = v.n;
-  double *Dj = blk(v.D, J, n);
+// g_J -= A_{J+h}^T z_{J+h} + C_{J-h}^T z_{J-h}. One wavefront per output tile
+// (plus one per block for g).
+__global__ __launch_bounds__(64) void k_cr_update_gemm(CRView v, int h) {
+  const int n = v.n, nt = n >> 4, per = nt * nt;
+  const int ev = blockIdx.x / (2 * per + 1), rem = blockIdx.x - ev * (2 * per + 1);
+  const int J = 2 * h * ev;
   const bool right = J + h < v.p, left = J >= h;
-  if (right) wg_gemm<true, false, kCRMaxN>(Dj, n, blk(v.A, J + h, n), n, blk(v.A, J + h, n), n, n, -1.0, 1.0);
-  __syncthreads();
-  if (left) wg_gemm<true, false, kCRMaxN>(Dj, n, blk(v.C, J - h, n), n, blk(v.C, J - h, n), n, n, -1.0, 1.0);
-  if (right && J + 2 * h < v.p)
-    wg_gemm<true, false, kCRMaxN>(blk(v.E, J, n), n, blk(v.A, J + h, n), n, blk(v.C, J + h, n), n, n, -1.0, 0.0);
-  double *gj = v.g + (size_t)J * n;
-  if (right) wg_gemv<true>(gj, blk(v.A, J + h, n), n, v.g + (size_t)(J + h) * n, n, -1.0, 1.0);
-  __syncthreads();
-  if (left) wg_gemv<true>(gj, blk(v.C, J - h, n), n, v.g + (size_t)(J - h) * n, n, -1.0, 1.0);
+  if (rem == 2 * per) {  // right-hand side
+    double *gj = v.g + (size_t)J * n;
+    for (int r = threadIdx.x; r < n; r += 64) {
+      double s = gj[r];
+      if (right) {
+        const double *A = blk(v.A, J + h, n), *z = v.g + (size_t)(J + h) * n;
+        for (int k = 0; k < n; ++k) s -= A[k * n + r] * z[k];
+      }
+      if (left) {
+        const double *C = blk(v.C, J - h, n), *z = v.g + (size_t)(J - h) * n;
+        for (int k = 0; k < n; ++k) s -= C[k * n + r] * z[k];
+      }
+      gj[r] = s;
+    }
+    return;
+  }
+  const int which = rem / per, t = rem - which * per, ti = t / nt, tj = t - ti * nt;
+  if (which == 0) {
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (right) acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.A, J + h, n), n, ti, tj);
+    if (left) {
+      const d4 a2 = tile_gemm<true, false, false>(blk(v.C, J - h, n), blk(v.C, J - h, n), n, ti, tj);
+      acc += a2;
+    }
+    if (right || left) tile_store(blk(v.D, J, n), n, ti, tj, acc, -1.0, true);
+  } else if (right && J + 2 * h < v.p) {
+    const d4 acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.C, J + h, n), n, ti, tj);
+    tile_store(blk(v.E, J, n), n, ti, tj, acc, -1.0, false);
+  }
 }
 
 // Last remaining superblock 0: x_0 = D_0^-1 g_0.
@@ -342,8 +409,10 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
   for (; h < pl.p; h *= 2) {
     const int n_odd = (pl.p - h + 2 * h - 1) / (2 * h);
     const int n_even = (pl.p + 2 * h - 1) / (2 * h);
-    hipLaunchKernelGGL(k_cr_elim, dim3(n_odd), dim3(512), lds, st, v, h);
-    hipLaunchKernelGGL(k_cr_update, dim3(n_even), dim3(512), 0, st, v, h);
+    const int per = (pl.n / 16) * (pl.n / 16);
+    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
+    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(n_odd * 2 * per), dim3(64), 0, st, v, h);
+    hipLaunchKernelGGL(k_cr_update_gemm, dim3(n_even * (2 * per + 1)), dim3(64), 0, st, v, h);
   }
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
   for (h /= 2; h >= 1; h /= 2) {
