@@ -68,13 +68,13 @@ def shard(prob, rank: int, world: int):
 
 def algorithmic_bytes_linearize(p) -> float:
     """Bytes k_linearize must move per launch: per observation
-    reads cam id, free-camera id, uv, info, delta (40 B) and writes the error
-    (16 B); per observation of a FREE camera it writes the 3x6 H_lp block
-    (144 B) and the weighted pose Jacobian + residual (112 B); per landmark it
-    reads X (24 B) + offset (4 B) and writes R (48 B) + b_l (24 B)."""
+    it reads cam id, free-camera id, uv, info, delta (40 B) and writes the
+    error (16 B); per observation of a FREE camera it writes the 3x6 H_lp block
+    (144 B); per landmark it reads X (24 B) + offset (4 B) and writes the QR
+    factor R (48 B) + b_l (24 B). Pose reads (<1 MB, L2-resident) excluded."""
     free = p.pose_fixed[p.obs_pose] == 0
     E, Ef, L = p.n_obs, int(free.sum()), p.n_pt
-    return E * (40 + 16) + Ef * (144 + 112) + L * (24 + 4 + 48 + 24)
+    return E * (40 + 16) + Ef * 144 + L * (24 + 4 + 48 + 24)
 
 
 def survey_bytes_linearize(p) -> float:

@@ -438,7 +438,6 @@ int prepare(sqlm_ctx *c, int level) {
   UP(B_OBSINFO, obs_info, d.obs_info);
   UP(B_OBSDELTA, obs_delta, d.obs_delta);
   AL(B_OBSP, 18 * (size_t)nE, d.obs_P);
-  AL(B_OBSJP, 16 * (size_t)nE, d.obs_jp);
   AL(B_OBSERR, 2 * (size_t)nE, d.obs_err);
   UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
   UP(B_CAMOBS, cam_obs, d.cam_obs);

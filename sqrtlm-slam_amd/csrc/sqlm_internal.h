@@ -31,7 +31,7 @@ struct DevProblem {
   double *lm_b = nullptr;                   // [nL][4]  b_l = -J_l^T W r
   double *lm_M = nullptr;                   // [nL][8]  (H_ll + lambda I)^-1, sym (6)
   double *lm_v = nullptr;                   // [nL][4]  M b_l
-  double *lm_Rp = nullptr;                  // [nL][12] damped R' (6), w = R'^-T b_l (3)
+  double *lm_Rp = nullptr;                  // [nL][12] R'^-1 of the damped factor (6), w = R'^-T b_l (3)
   // observations
   int *obs_lm = nullptr;                    // [nE] landmark slot
   int *obs_cam = nullptr;                   // [nE] pose id
@@ -39,8 +39,7 @@ struct DevProblem {
   double *obs_uv = nullptr;                 // [nE][2]
   double *obs_info = nullptr;               // [nE]
   double *obs_delta = nullptr;              // [nE] Huber delta, 0 = none
-  double *obs_P = nullptr;                  // [nE][18] H_pl^T block J_l^T W J_p (3x6)
-  double *obs_jp = nullptr;                 // [nE][16] sqrt(w) J_p (12), sqrt(w) r (2)
+  double *obs_P = nullptr;                  // [18][nE] H_lp block J_l^T W J_p (3x6), SoA
   double *obs_err = nullptr;                // [nE][2] last computed error (g2o _error)
   // cameras
   int *cam_obs_ptr = nullptr;               // [nP+1]

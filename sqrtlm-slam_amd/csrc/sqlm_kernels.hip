@@ -143,6 +143,14 @@ __device__ __forceinline__ void mono_jac(const double *__restrict__ prt, const M
   jp[11] = s * (y / z_2 * fy);
 }
 
+// Workgroup barrier that orders LDS only: global loads issued before it stay in
+// flight (a __syncthreads() fence would wait vmcnt(0) and drain the prefetch).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void store2(double *p, double a, double b) {
   *reinterpret_cast<double2 *>(p) = make_double2(a, b);
 }
@@ -222,17 +230,12 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
         givens_add_row(R, jl[0], jl[1], jl[2]);
         givens_add_row(R, jl[3], jl[4], jl[5]);
         if (d.obs_camh[e] >= 0) {
-          double *P = d.obs_P + 18 * e;  // H_lp block: jl^T jp, 3x6 row-major
+          // H_lp block jl^T jp (3x6), structure of arrays: entry (a,c) at P[(6a+c) nE + e]
+          double *P = d.obs_P + e;
 #pragma unroll
           for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int c = 0; c < 6; c += 2)
-              store2(P + 6 * a + c, jl[a] * jp[c] + jl[3 + a] * jp[6 + c],
-                     jl[a] * jp[c + 1] + jl[3 + a] * jp[6 + c + 1]);
-          double *J = d.obs_jp + 16 * e;
-#pragma unroll
-          for (int c = 0; c < 12; c += 2) store2(J + c, jp[c], jp[c + 1]);
-          store2(J + 12, r0, r1);
+            for (int c = 0; c < 6; ++c) P[(6 * a + c) * d.nE] = jl[a] * jp[c] + jl[3 + a] * jp[6 + c];
         }
       }
     }
@@ -286,8 +289,10 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
 
 // ---------------------------------------------------------------- camera pass
 
-// One wave per free camera: H_pp = sum jp^T jp, b_p = -sum jp^T r, plus the
-// camera's LiDAR unary edges (numeric Jacobian, base_unary_edge.hpp:82-122).
+// One wave per free camera: H_pp = sum jp^T jp, b_p = -sum jp^T r with the
+// weighted pose Jacobian recomputed from the inputs (the same device code as
+// k_linearize, so bit-identical), plus the camera's LiDAR unary edges
+// (numeric Jacobian, base_unary_edge.hpp:82-122).
 __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + wave;
@@ -297,14 +302,17 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
 #pragma unroll
   for (int k = 0; k < 6; ++k) b[k] = 0.0;
   if (i < d.nP) {
+    const double *prt = d.pose_rt[0] + 16 * d.hidx_pose[i];
     for (int t = d.cam_obs_ptr[i] + lane; t < d.cam_obs_ptr[i + 1]; t += 64) {
-      const double *J = d.obs_jp + 16 * d.cam_obs[t];
-      double j[14];
-#pragma unroll
-      for (int k = 0; k < 14; k += 2) {
-        const double2 v = *reinterpret_cast<const double2 *>(J + k);
-        j[k] = v.x; j[k + 1] = v.y;
-      }
+      const int e = d.cam_obs[t];
+      const double *X = d.X[0] + 4 * d.obs_lm[e];
+      const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
+      MonoEval m;
+      mono_error(prt, X[0], X[1], X[2], uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
+      double jl[6], j[14];
+      mono_jac(prt, m, jl, j);
+      j[12] = m.s * m.e0;
+      j[13] = m.s * m.e1;
       int k = 0;
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
@@ -402,12 +410,12 @@ __global__ void k_damp(DevProblem d, double lambda) {
   double *M = d.lm_M + 8 * l;
   store2(M, m00, m01); store2(M + 2, m02, m11); store2(M + 4, m12, m22);
   const double *bl = d.lm_b + 4 * l;
-  // w = R'^-T b_l (forward substitution with the lower factor R'^T)
-  const double w0 = bl[0] / R[0];
-  const double w1 = (bl[1] - R[1] * w0) / R[3];
-  const double w2 = (bl[2] - R[2] * w0 - R[4] * w1) / R[5];
+  // R'^-1 (upper) and w = R'^-T b_l; the RCS tiles stage Y = R'^-T P as (R'^-1)^T P
+  const double w0 = i00 * bl[0];
+  const double w1 = i01 * bl[0] + i11 * bl[1];
+  const double w2 = i02 * bl[0] + i12 * bl[1] + i22 * bl[2];
   double *Rp = d.lm_Rp + 12 * l;
-  store2(Rp, R[0], R[1]); store2(Rp + 2, R[2], R[3]); store2(Rp + 4, R[4], R[5]);
+  store2(Rp, i00, i01); store2(Rp + 2, i02, i11); store2(Rp + 4, i12, i22);
   store2(Rp + 6, w0, w1); store2(Rp + 8, w2, 0.0);
   const double v0 = m00 * bl[0] + m01 * bl[1] + m02 * bl[2];
   const double v1 = m01 * bl[0] + m11 * bl[1] + m12 * bl[2];
@@ -445,12 +453,12 @@ __global__ __launch_bounds__(256) void k_rcs(DevProblem d, double lambda, int ns
     const int l = d.obs_lm[oi];
     const double *Ml = d.lm_M + 8 * l;
     const double M00 = Ml[0], M01 = Ml[1], M02 = Ml[2], M11 = Ml[3], M12 = Ml[4], M22 = Ml[5];
-    const double *Pi = d.obs_P + 18 * oi;
+    const double *Pi = d.obs_P + oi;  // SoA: entry (a,c) at Pi[(6a+c) nE]
     // lanes 0..17 compute Z[zr][zc] = (P_i^T M)[zr][zc], zr in 0..5, zc in 0..2
     double zval = 0.0;
     if (lane < 18) {
       const int zr = lane / 3, zc = lane % 3;
-      const double p0 = Pi[zr], p1 = Pi[6 + zr], p2 = Pi[12 + zr];
+      const double p0 = Pi[zr * d.nE], p1 = Pi[(6 + zr) * d.nE], p2 = Pi[(12 + zr) * d.nE];
       const double m0 = zc == 0 ? M00 : (zc == 1 ? M01 : M02);
       const double m1 = zc == 0 ? M01 : (zc == 1 ? M11 : M12);
       const double m2 = zc == 0 ? M02 : (zc == 1 ? M12 : M22);
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(256) void k_rcs(DevProblem d, double lambda, int ns
     }
     if (lane < 6) {
       const double *v = d.lm_v + 4 * l;
-      gacc -= Pi[lane] * v[0] + Pi[6 + lane] * v[1] + Pi[12 + lane] * v[2];
+      gacc -= Pi[lane * d.nE] * v[0] + Pi[(6 + lane) * d.nE] * v[1] + Pi[(12 + lane) * d.nE] * v[2];
     }
     const int rr = lane < 36 ? r : 0;
     const double z0 = __shfl(zval, 3 * rr, 64);
@@ -475,8 +483,8 @@ __global__ __launch_bounds__(256) void k_rcs(DevProblem d, double lambda, int ns
         if (cols[mid] < cj) lo = mid + 1; else hi = mid;
       }
       if (lane < 36) {
-        const double *Pj = d.obs_P + 18 * o;
-        const double v = z0 * Pj[c] + z1 * Pj[6 + c] + z2 * Pj[12 + c];
+        const double *Pj = d.obs_P + o;
+        const double v = z0 * Pj[c * d.nE] + z1 * Pj[(6 + c) * d.nE] + z2 * Pj[(12 + c) * d.nE];
         acc[lo * 36 + lane] -= v;
       }
     }
@@ -526,6 +534,35 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 // current batch runs on the matrix cores.
 constexpr int kTileBL = 4, kTileIPT = 4;  // fast path: k <= 128 * 4 / (6 * 4) = 21
 
+// MFMA phase of one batch for the accumulator tiles of wave parity P:
+// acc[q/2] += sum_ks Y[4ks..4ks+3][ti-tile]^T Y[4ks..4ks+3][tj-tile].
+// Both operands of every MFMA are entries Y[4ks + (lane>>4)][16t + (lane&15)],
+// so the lane's NT x 4 values are read from LDS once and the MFMAs then issue
+// back to back from registers.
+template <int NT, int P, int NC>
+__device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int tmin, int tmax, int nl, int r16,
+                                          int k4) {
+  double op[NT][kTileBL];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < kTileBL; ++ks) op[t][ks] = Y[4 * ks + k4][t * 16 + r16];
+  int q = 0;
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti) {
+#pragma unroll
+    for (int tj = ti; tj < NT; ++tj, ++q) {
+      if ((q & 1) == P) {
+        if (ti >= tmin && tj <= tmax) {
+#pragma unroll
+          for (int ks = 0; ks < kTileBL; ++ks)
+            if (ks < nl) acc[q >> 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti][ks], op[tj][ks], acc[q >> 1], 0, 0, 0);
+        }
+      }
+    }
+  }
+}
+
 template <int NT>
 __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
   // two waves per tile: wave w owns the accumulator tiles q with q % 2 == w
@@ -549,7 +586,7 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
   const int nbatch = (l1 - l0 + BL - 1) / BL;
   const bool slow = d.tile_dups || d.tile_maxk > 21;
   // prefetched raw inputs of one batch (fast path)
-  double pp[IPT][3];
+  double pp[IPT][3], pr[IPT][6];
   int pu[IPT], pli[IPT], pc[IPT];
   auto fetch = [&](int bt) {
     const int lb = l0 + BL * bt, nl = min(BL, l1 - lb);
@@ -564,14 +601,17 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
         pli[m] = (o >= e1) + (o >= e2) + (o >= e3);
         pc[m] = it % 6;
         pu[m] = d.obs_local[o];
-        const double *P = d.obs_P + 18 * (size_t)o;
-        pp[m][0] = P[pc[m]]; pp[m][1] = P[6 + pc[m]]; pp[m][2] = P[12 + pc[m]];
+        const double *P = d.obs_P + o;
+        pp[m][0] = P[pc[m] * d.nE]; pp[m][1] = P[(6 + pc[m]) * d.nE]; pp[m][2] = P[(12 + pc[m]) * d.nE];
+        const double *Ri = d.lm_Rp + 12 * (lb + pli[m]);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) pr[m][i] = Ri[i];
       }
     }
   };
   if (nbatch > 0) fetch(0);
   int2 prev = int2{-1, -1};
-  __syncthreads();
+  lds_barrier();
   for (int bt = 0; bt < nbatch; ++bt) {
     const int buf = bt & 1, lb = l0 + BL * bt, nl = min(BL, l1 - lb);
     double (*Y)[NC] = Ys[buf];
@@ -581,11 +621,10 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
     if (!slow) {
 #pragma unroll
       for (int m = 0; m < IPT; ++m) {
-        if (pu[m] >= 0) {
-          const double *Rp = d.lm_Rp + 12 * (lb + pli[m]);
-          const double y0 = pp[m][0] / Rp[0];
-          const double y1 = (pp[m][1] - Rp[1] * y0) / Rp[3];
-          const double y2 = (pp[m][2] - Rp[2] * y0 - Rp[4] * y1) / Rp[5];
+        if (pu[m] >= 0) {  // y = (R'^-1)^T p
+          const double y0 = pr[m][0] * pp[m][0];
+          const double y1 = pr[m][1] * pp[m][0] + pr[m][3] * pp[m][1];
+          const double y2 = pr[m][2] * pp[m][0] + pr[m][4] * pp[m][1] + pr[m][5] * pp[m][2];
           const int col = 6 * pu[m] + pc[m], row = 4 * pli[m];
           Y[row][col] = y0; Y[row + 1][col] = y1; Y[row + 2][col] = y2;
         }
@@ -597,19 +636,21 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
         for (int o = d.lm_begin[l]; o < d.lm_begin[l + 1]; ++o) {
           const int u = d.obs_local[o];
           if (u < 0) continue;
-          const double *P = d.obs_P + 18 * (size_t)o;
-          const double y0 = P[tid] / Rp[0];
-          const double y1 = (P[6 + tid] - Rp[1] * y0) / Rp[3];
-          const double y2 = (P[12 + tid] - Rp[2] * y0 - Rp[4] * y1) / Rp[5];
+          const double *P = d.obs_P + o;
+          const double p0 = P[tid * d.nE], p1 = P[(6 + tid) * d.nE], p2 = P[(12 + tid) * d.nE];
+          const double y0 = Rp[0] * p0;
+          const double y1 = Rp[1] * p0 + Rp[3] * p1;
+          const double y2 = Rp[2] * p0 + Rp[4] * p1 + Rp[5] * p2;
           Y[4 * li][6 * u + tid] += y0; Y[4 * li + 1][6 * u + tid] += y1; Y[4 * li + 2][6 * u + tid] += y2;
         }
       }
     }
-    __syncthreads();  // (A) batch staged; every thread is done with the previous batch
+    lds_barrier();  // (A) batch staged; every thread is done with the previous batch
     if (bt + 1 < nbatch) fetch(bt + 1);  // in flight during the MFMAs below
     if (prev.x >= 0) {  // clear the previous batch's columns in the other buffer
-      const int c0 = prev.x, w = prev.y - prev.x;
-      for (int it = tid; it < 4 * BL * w; it += 128) Ys[buf ^ 1][it / w][c0 + it % w] = 0.0;
+#pragma unroll
+      for (int row = 0; row < 4 * BL; ++row)
+        for (int col = prev.x + tid; col < prev.y; col += 128) Ys[buf ^ 1][row][col] = 0.0;
     }
     int cmin = 1 << 30, cmax = -1;
     for (int li = 0; li < nl; ++li) {
@@ -618,23 +659,8 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
     }
     if (cmax > 0) {
       const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
-      int q = 0;
-#pragma unroll
-      for (int ti = 0; ti < NT; ++ti) {
-#pragma unroll
-        for (int tj = ti; tj < NT; ++tj, ++q) {
-          if ((q & 1) == wave && ti >= tmin && tj <= tmax) {
-#pragma unroll
-            for (int ks = 0; ks < BL; ++ks) {
-              if (ks < nl) {
-                const double a = Y[4 * ks + k4][ti * 16 + r16];
-                const double bb = Y[4 * ks + k4][tj * 16 + r16];
-                acc[q >> 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc[q >> 1], 0, 0, 0);
-              }
-            }
-          }
-        }
-      }
+      if (wave == 0) tile_mfma<NT, 0>(acc, Y, tmin, tmax, nl, r16, k4);
+      else tile_mfma<NT, 1>(acc, Y, tmin, tmax, nl, r16, k4);
 #pragma unroll
       for (int m = 0; m < NG; ++m) {
         const int col = tid + 128 * m;
@@ -650,7 +676,7 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
     } else {
       prev = int2{-1, -1};
     }
-    __syncthreads();  // (B) the other buffer is clear before it is staged
+    lds_barrier();  // (B) the other buffer is clear before it is staged
   }
   // write -G_t (upper tiles) as the tile's partial, ld = 16 nt
   double *out = d.part + d.tile_part_ptr[t];
@@ -855,13 +881,16 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
       for (int e = beg + lane; e < end; e += W) {
         const int h = d.obs_camh[e];
         if (h < 0) continue;
-        const double *P = d.obs_P + 18 * e, *dx = d.dx + 6 * h;
-        double x[6];
+        const double *P = d.obs_P + e, *dx = d.dx + 6 * h;
+        const int64_t nE = d.nE;
+        double x[6], p[18];
 #pragma unroll
         for (int k = 0; k < 6; ++k) x[k] = dx[k];
-        a0 += P[0] * x[0] + P[1] * x[1] + P[2] * x[2] + P[3] * x[3] + P[4] * x[4] + P[5] * x[5];
-        a1 += P[6] * x[0] + P[7] * x[1] + P[8] * x[2] + P[9] * x[3] + P[10] * x[4] + P[11] * x[5];
-        a2 += P[12] * x[0] + P[13] * x[1] + P[14] * x[2] + P[15] * x[3] + P[16] * x[4] + P[17] * x[5];
+#pragma unroll
+        for (int k = 0; k < 18; ++k) p[k] = P[k * nE];
+        a0 += p[0] * x[0] + p[1] * x[1] + p[2] * x[2] + p[3] * x[3] + p[4] * x[4] + p[5] * x[5];
+        a1 += p[6] * x[0] + p[7] * x[1] + p[8] * x[2] + p[9] * x[3] + p[10] * x[4] + p[11] * x[5];
+        a2 += p[12] * x[0] + p[13] * x[1] + p[14] * x[2] + p[15] * x[3] + p[16] * x[4] + p[17] * x[5];
       }
     }
 #pragma unroll
