@@ -144,7 +144,7 @@ int sqlm_ctx_set_comm(sqlm_ctx *ctx, const char *unique_id, int rank, int nranks
  * problem with data already in HBM (bench.py). Per-kernel averaged durations
  * (HIP events on the context stream) are returned through kernel_ms
  * [SQLM_NKERNEL_TIMERS] when non-NULL. */
-#define SQLM_NKERNEL_TIMERS 8
+#define SQLM_NKERNEL_TIMERS 9
 int sqlm_bench_iterations(sqlm_ctx *ctx, int warmup, int n, double *ms_per_iter, double *kernel_ms,
                           sqlm_stats *stats);
 const char *sqlm_kernel_timer_name(int i);

@@ -35,8 +35,9 @@ struct Timer {
   }
 };
 
-const char *kTimerNames[SQLM_NKERNEL_TIMERS] = {"k_linearize", "k_camera_pass", "k_damp", "k_rcs",
-                                                "k_solve", "k_pose_update", "k_landmark_update", "reduce+sync"};
+const char *kTimerNames[SQLM_NKERNEL_TIMERS] = {"k_linearize", "k_camera_pass", "k_damp", "k_rcs_tile",
+                                                "k_solve", "k_pose_update", "k_landmark_update", "reduce+sync",
+                                                "k_rcs_reduce"};
 
 }  // namespace
 
@@ -557,6 +558,9 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   if (c->use_tiles) launch_rcs_tiles(d, lambda, c->tile_max_cp, c->tile_max_k, c->stream);
   else launch_rcs(d, lambda, c->max_row_blocks, c->stream);
   tmark(c, 3, true);
+  tmark(c, 8, false);
+  if (c->use_tiles) launch_rcs_reduce(d, lambda, c->stream);
+  tmark(c, 8, true);
   int s = comm_allreduce_rcs(c->comm, d, lambda, c->stream);
   if (s) return s;
   tmark(c, 4, false);

@@ -126,6 +126,7 @@ void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
 void launch_damp(const DevProblem &d, double lambda, hipStream_t st);
 void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st);
 void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st);
+void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st);
 constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);

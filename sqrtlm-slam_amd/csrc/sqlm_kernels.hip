@@ -744,6 +744,10 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     else if (nt <= 7) hipLaunchKernelGGL(k_rcs_tile<7>, dim3(d.n_tiles), dim3(128), 0, st, d);
     else hipLaunchKernelGGL(k_rcs_tile<9>, dim3(d.n_tiles), dim3(128), 0, st, d);
   }
+}
+
+void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st) {
+  if (d.nP == 0) return;
   const int64_t items = d.nnzb * 36 + (int64_t)d.nP * 6;
   hipLaunchKernelGGL(k_rcs_reduce, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, d, lambda);
 }

@@ -14,7 +14,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libsqrtlm.so")
 TRACE_MAX = 256
-NKERNEL_TIMERS = 8
+NKERNEL_TIMERS = 9
 
 SQLM_OK = 0
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "not SPD", -4: "out of device memory",
