@@ -53,24 +53,6 @@ def make_workload(name: str, scale: float):
     return prob, desc
 
 
-def shard(prob, rank: int, world: int):
-    """Landmark shard: contiguous landmark ranges (landmarks are sorted by first
-    observing keyframe) balanced by observation count. All poses replicated."""
-    from sqrtlm.problem import BAProblem
-    if world == 1:
-        return prob
-    counts = np.bincount(prob.obs_pt, minlength=prob.n_pt)
-    cum = np.cumsum(counts)
-    bounds = np.searchsorted(cum, np.linspace(0, cum[-1], world + 1)[1:-1])
-    lo = 0 if rank == 0 else int(bounds[rank - 1]) + 1
-    hi = prob.n_pt if rank == world - 1 else int(bounds[rank]) + 1
-    sel = (prob.obs_pt >= lo) & (prob.obs_pt < hi)
-    return BAProblem(pose_q=prob.pose_q, pose_t=prob.pose_t, pose_fixed=prob.pose_fixed, intr=prob.intr,
-                     pt=prob.pt[lo:hi], obs_pose=prob.obs_pose[sel], obs_pt=prob.obs_pt[sel] - lo,
-                     obs_uv=prob.obs_uv[sel], obs_info=prob.obs_info[sel], obs_delta=prob.obs_delta[sel],
-                     obs_level=prob.obs_level[sel])
-
-
 def algorithmic_bytes_linearize(p) -> float:
     """Bytes k_linearize must move per launch: per observation
     it reads cam id, free-camera id, uv, info, delta (40 B) and writes the
@@ -93,7 +75,8 @@ def algorithmic_flops_rcs(p) -> float:
 
 
 def pmc_traffic(kernel_prefix: str, workload: str, n_obs: int):
-    """Per-launch HBM bytes of `kernel_prefix` from the committed rocprofv3 PMC
+    """Per-launch HBM bytes of `kernel_prefix` (summed over its template
+    instances, e.g. the three k_linearize<W> buckets) from the committed rocprofv3 PMC
     summary (scripts/gpu_pmc.sh + scripts/pmc_summary.py: separate FETCH_SIZE
     and WRITE_SIZE passes, FETCH_SIZE doubled for gfx950). None if the summary
     was not taken on this exact workload."""
@@ -103,10 +86,9 @@ def pmc_traffic(kernel_prefix: str, workload: str, n_obs: int):
     summ = json.load(open(path))
     if int(summ.get("meta", {}).get("n_obs", -1)) != n_obs:
         return None, None
-    for k, e in summ["kernels"].items():
-        if k.startswith(kernel_prefix) and "traffic_bytes" in e:
-            return e["traffic_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+    hits = [e["traffic_bytes"] for k, e in summ["kernels"].items()
+            if k.startswith(kernel_prefix) and "traffic_bytes" in e]  # all template instances (buckets)
+    return (float(sum(hits)), os.path.relpath(path, ROOT)) if hits else (None, None)
 
 
 def survey_bytes_linearize(p) -> float:
@@ -117,14 +99,26 @@ def survey_bytes_linearize(p) -> float:
     return float(np.sum(28 * k + 28 + 16 * k * (6 * m + 4)))
 
 
-def reprojection_rmse(p, q, t, X) -> float:
-    """sqrt(mean ||obs - proj||^2) over all edges at the given state (px)."""
+def _gloo_allreduce(arr, op):
+    """Host collective for --comm host (sqlm_ctx_set_host_comm)."""
+    import torch
+    import torch.distributed as dist
+    rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
+    t = torch.from_numpy(arr.astype(np.int32) if arr.dtype == np.uint8 else arr)
+    dist.all_reduce(t, op=rop)
+    if arr.dtype == np.uint8:
+        arr[:] = t.numpy().astype(np.uint8)
+
+
+def reprojection_sse(p, q, t, X):
+    """(sum ||obs - proj||^2, number of edges) at the given state; the RMSE
+    over all shards is sqrt(sum sse / sum n)."""
     from sqrtlm.synth import quat_to_mat
     R = quat_to_mat(q)
     Xc = np.einsum("nij,nj->ni", R[p.obs_pose], X[p.obs_pt]) + t[p.obs_pose]
     fx, fy, cx, cy = (p.intr[p.obs_pose, k] for k in range(4))
     e = p.obs_uv - np.stack([Xc[:, 0] / Xc[:, 2] * fx + cx, Xc[:, 1] / Xc[:, 2] * fy + cy], axis=1)
-    return float(np.sqrt(np.mean(np.sum(e * e, axis=1))))
+    return float(np.sum(e * e)), float(p.n_obs)
 
 
 def cpu_baseline(prob, name: str):
@@ -158,6 +152,8 @@ def main():
     ap.add_argument("--config", choices=["gba", "lba"], default="gba")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink config 4 (parity / debugging only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                    help="host = exchange through gloo on the host, all ranks on GPU 0 (1-GPU rehearsal of N>1)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,22 +165,30 @@ def main():
         dist.init_process_group("gloo", init_method="env://")
 
     from sqrtlm.optimizer import Context, comm_unique_id
+    from sqrtlm.shard import shard
     prob, desc = make_workload(args.config, args.scale)
     local = shard(prob, rank, world)
-    ctx = Context(local_rank)
-    if world > 1:
+    ctx = Context(local_rank if args.comm == "rccl" else 0)
+    if world > 1 and args.comm == "rccl":
         import torch
-        uid = comm_unique_id() if rank == 0 else bytes(128)
+        from sqrtlm._lib import lib
+        uid = comm_unique_id() if rank == 0 else bytes(lib().sqlm_comm_id_size())
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
         ctx.set_comm(bytes(t.tolist()), rank, world)
+    elif world > 1:
+        ctx.set_host_comm(rank, world, _gloo_allreduce)
     ctx.set_problem(local)
     ms, kms, st = ctx.bench(args.warmup, args.steps)
+    sse, nres = reprojection_sse(local, *ctx.poses(), ctx.points())
     if dist is not None:
         import torch
         tt = torch.tensor([ms], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ms = float(tt.item())
+        tt = torch.tensor([sse, nres], dtype=torch.float64)
+        dist.all_reduce(tt)
+        sse, nres = float(tt[0]), float(tt[1])
 
     if rank == 0:
         launches = max(1.0, st["trials"] / max(1, st["iterations"]))  # k_rcs_tile runs once per trial
@@ -225,7 +229,7 @@ def main():
                                    "survey_basis_GBps": survey_bytes_linearize(local) / (t_lin * 1e-3) / 1e9
                                    if t_lin else None},
         }
-        out["final_rmse_px"] = reprojection_rmse(local, *ctx.poses(), ctx.points())
+        out["final_rmse_px"] = float(np.sqrt(sse / max(1.0, nres)))
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(prob, args.config)
         print(json.dumps(out))

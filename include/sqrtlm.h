@@ -140,6 +140,20 @@ int sqlm_comm_id_size(void);
 int sqlm_comm_get_unique_id(char *id_out);
 int sqlm_ctx_set_comm(sqlm_ctx *ctx, const char *unique_id, int rank, int nranks);
 
+/* Same sharded algorithm over a caller-provided host collective (for example
+ * torch.distributed gloo): the library stages each exchange through host
+ * memory and calls fn(user, buf, count, dtype, op), which must all-reduce
+ * `count` elements of `buf` in place across the ranks and return 0. Used to
+ * run several ranks on one GPU (tests); production uses sqlm_ctx_set_comm.
+ * LiDAR unary edges are owned by rank 0 (ignored on other ranks). */
+#define SQLM_DT_F64 0
+#define SQLM_DT_U8 1
+#define SQLM_DT_I32 2
+#define SQLM_OP_SUM 0
+#define SQLM_OP_MAX 1
+typedef int (*sqlm_allreduce_fn)(void *user, void *buf, int64_t count, int dtype, int op);
+int sqlm_ctx_set_host_comm(sqlm_ctx *ctx, int rank, int nranks, sqlm_allreduce_fn fn, void *user);
+
 /* Device-resident benchmarking hooks: time `n` LM iterations on the set
  * problem with data already in HBM (bench.py). Per-kernel averaged durations
  * (HIP events on the context stream) are returned through kernel_ms

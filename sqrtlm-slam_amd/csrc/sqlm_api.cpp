@@ -236,11 +236,17 @@ int prepare(sqlm_ctx *c, int level) {
     ++n_ae;
   }
   std::vector<int64_t> lid_act;
+  const bool sharded = c->comm.enabled();
   for (int64_t e = 0; e < c->n_lid; ++e) {
+    if (sharded && c->comm.rank != 0) break;  // unary pose edges live on rank 0
     if (c->lid_level[e] != level || c->pose_fixed[c->lid_pose[e]]) continue;
     lid_act.push_back(e);
     pose_act[c->lid_pose[e]] = 1;
   }
+  // sharded: every rank must index the same free cameras (union of shards)
+  if (sharded &&
+      comm_allreduce_host(c->comm, pose_act.data(), c->n_pose, SQLM_DT_U8, SQLM_OP_MAX, c->stream))
+    return SQLM_ERR_COMM;
   c->n_active_edges = (int)(n_ae + (int64_t)lid_act.size());
   std::vector<int> phidx(c->n_pose, -1), hidxp;
   for (int p = 0; p < c->n_pose; ++p)
@@ -323,6 +329,17 @@ int prepare(sqlm_ctx *c, int level) {
       }
       std::sort(row.begin() + 1, row.end());
       rows[i] = row;
+    }
+    if (sharded) {
+      // a common pattern for the S all-reduce: the band of the widest shard
+      int bw = 0;
+      for (int i = 0; i < nP; ++i)
+        if (rows[i].size() > 1) bw = std::max(bw, rows[i].back() - i);
+      if (comm_allreduce_host(c->comm, &bw, 1, SQLM_DT_I32, SQLM_OP_MAX, c->stream)) return SQLM_ERR_COMM;
+      for (int i = 0; i < nP; ++i) {
+        rows[i].clear();
+        for (int j = i; j <= std::min(nP - 1, i + bw); ++j) rows[i].push_back(j);
+      }
     }
     for (int i = 0; i < nP; ++i) s_row[i + 1] = s_row[i] + (int)rows[i].size();
     s_col.resize(s_row[nP]);
@@ -561,7 +578,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   tmark(c, 8, false);
   if (c->use_tiles) launch_rcs_reduce(d, lambda, c->stream);
   tmark(c, 8, true);
-  int s = comm_allreduce_rcs(c->comm, d, lambda, c->stream);
+  int s = comm_allreduce_rcs(c->comm, d, c->stream);
   if (s) return s;
   tmark(c, 4, false);
   s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream) : launch_dense_solve(d, c->stream);
@@ -934,6 +951,11 @@ void sqlm_pose_to_Tcw_f32(const double q[4], const double t[3], float T[16]) {
     T[r * 4 + 3] = (float)t[r];
   }
   T[12] = 0.f; T[13] = 0.f; T[14] = 0.f; T[15] = 1.f;
+}
+
+int sqlm_ctx_set_host_comm(sqlm_ctx *c, int rank, int nranks, sqlm_allreduce_fn fn, void *user) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return SQLM_ERR_INVALID_ARG;
+  return comm_init_host(c->comm, rank, nranks, fn, user);
 }
 
 int sqlm_comm_id_size(void) { return comm_id_size(); }

@@ -26,7 +26,8 @@ EXPORTS = [
     "sqlm_set_lidar", "sqlm_set_edge_level", "sqlm_set_robust", "sqlm_set_lidar_level", "sqlm_optimize",
     "sqlm_local_ba", "sqlm_global_ba", "sqlm_get_poses", "sqlm_get_points", "sqlm_get_edge_chi2",
     "sqlm_get_edge_depth_positive", "sqlm_get_edge_level", "sqlm_pose_from_Tcw_f32", "sqlm_pose_to_Tcw_f32",
-    "sqlm_comm_id_size", "sqlm_comm_get_unique_id", "sqlm_ctx_set_comm", "sqlm_bench_iterations",
+    "sqlm_comm_id_size", "sqlm_comm_get_unique_id", "sqlm_ctx_set_comm", "sqlm_ctx_set_host_comm",
+    "sqlm_bench_iterations",
     "sqlm_kernel_timer_name",
 ]
 
@@ -77,6 +78,11 @@ def lib() -> C.CDLL:
 def check(status: int, what: str) -> None:
     if status != SQLM_OK:
         raise SqlmError(status, what)
+
+
+# int (*sqlm_allreduce_fn)(void *user, void *buf, int64_t count, int dtype, int op)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int)
+DTYPES = {0: np.float64, 1: np.uint8, 2: np.int32}
 
 
 def ptr(a):

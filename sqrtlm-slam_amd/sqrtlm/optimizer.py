@@ -107,6 +107,24 @@ class Context:
         buf = C.create_string_buffer(unique_id, len(unique_id))
         check(lib().sqlm_ctx_set_comm(self._h, buf, int(rank), int(nranks)), "sqlm_ctx_set_comm")
 
+    def set_host_comm(self, rank: int, nranks: int, allreduce) -> None:
+        """Shard over a host collective: ``allreduce(arr, op)`` must reduce the
+        numpy array ``arr`` in place across ranks (op "sum" or "max"), e.g.
+        with torch.distributed gloo. Runs several ranks on one GPU (tests)."""
+        def _cb(_user, buf, count, dtype, op):
+            try:
+                dt = _lib.DTYPES[dtype]
+                arr = np.ctypeslib.as_array((C.c_char * (int(count) * np.dtype(dt).itemsize)).from_address(buf))
+                allreduce(arr.view(dt), "max" if op == 1 else "sum")
+                return 0
+            except Exception:  # noqa: BLE001 — never unwind through the C ABI
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._host_cb = _lib.ALLREDUCE_FN(_cb)  # keep alive while the context lives
+        check(lib().sqlm_ctx_set_host_comm(self._h, int(rank), int(nranks), self._host_cb, None),
+              "sqlm_ctx_set_host_comm")
+
     # ------------------------------------------------------------- results
     def poses(self):
         n = self.problem.n_pose

@@ -1,0 +1,67 @@
+"""Multi-rank host logic of the landmark-sharded global BA, world size 2 over
+gloo on CPU. The GPU counterpart, which runs the library's
+sharded solve on two ranks and compares it with one rank, is
+test_gpu_sharded.py."""
+import numpy as np
+import pytest
+
+from dist_util import gloo_allreduce, run_ranks
+from sqrtlm import synth
+from sqrtlm.shard import landmark_ranges, shard
+
+
+def _sse(p):
+    R = synth.quat_to_mat(p.pose_q)
+    Xc = np.einsum("nij,nj->ni", R[p.obs_pose], p.pt[p.obs_pt]) + p.pose_t[p.obs_pose]
+    fx, fy, cx, cy = (p.intr[p.obs_pose, k] for k in range(4))
+    e = p.obs_uv - np.stack([Xc[:, 0] / Xc[:, 2] * fx + cx, Xc[:, 1] / Xc[:, 2] * fy + cy], axis=1)
+    return float(np.sum(p.obs_info * np.sum(e * e, axis=1)))
+
+
+def _rank_work(rank, world, scale):
+    prob = synth.config4(seed=4, scale=scale)
+    loc = shard(prob, rank, world)
+    # the exchanges prepare() performs, through the same host collective
+    act = np.zeros(prob.n_pose, np.uint8)
+    act[np.unique(loc.obs_pose)] = 1
+    gloo_allreduce(act, "max")
+    cnt = np.array([loc.n_obs, loc.n_pt], np.int64).astype(np.float64)
+    gloo_allreduce(cnt, "sum")
+    chi = np.array([_sse(loc)])
+    gloo_allreduce(chi, "sum")
+    bw = np.array([int(np.max(np.bincount(loc.obs_pt, minlength=loc.n_pt)))], np.int32)  # longest track
+    gloo_allreduce(bw, "max")
+    return dict(act=act, cnt=cnt, chi=float(chi[0]), bw=int(bw[0]), n_obs=loc.n_obs,
+                lid=loc.n_lid, first_pose=int(loc.obs_pose.min()), last_pose=int(loc.obs_pose.max()))
+
+
+def test_ranges_cover_and_balance():
+    prob = synth.config4(seed=4, scale=0.01)
+    for world in (1, 2, 3, 8):
+        rng = landmark_ranges(prob, world)
+        assert rng[0][0] == 0 and rng[-1][1] == prob.n_pt
+        assert all(a[1] == b[0] for a, b in zip(rng, rng[1:]))
+        obs = [int(np.sum((prob.obs_pt >= lo) & (prob.obs_pt < hi))) for lo, hi in rng]
+        assert sum(obs) == prob.n_obs
+        assert max(obs) - min(obs) <= 2 * 18 + 1  # one landmark's track of slack per cut
+
+
+def test_two_rank_exchanges_match_single_process():
+    prob = synth.config4(seed=4, scale=0.01)
+    res = run_ranks(_rank_work, 2, 0.01)
+    full_act = np.zeros(prob.n_pose, np.uint8)
+    full_act[np.unique(prob.obs_pose)] = 1
+    for r in res:
+        np.testing.assert_array_equal(r["act"], full_act)         # global camera set
+        assert r["cnt"][0] == prob.n_obs and r["cnt"][1] == prob.n_pt
+        assert r["chi"] == pytest.approx(_sse(prob), rel=1e-12)   # chi2 sums across shards
+        assert r["bw"] == int(np.max(np.bincount(prob.obs_pt)))
+    assert res[0]["n_obs"] + res[1]["n_obs"] == prob.n_obs
+    # contiguous landmark ranges in trajectory order touch overlapping camera bands
+    assert res[0]["first_pose"] == 0 and res[1]["last_pose"] == prob.n_pose - 1
+
+
+def test_lidar_edges_only_on_rank0():
+    prob = synth.add_lidar_flat(synth.config4(seed=4, scale=0.01), pose=5, n=20, seed=1)
+    assert shard(prob, 0, 2).n_lid == prob.n_lid
+    assert shard(prob, 1, 2).n_lid == 0
