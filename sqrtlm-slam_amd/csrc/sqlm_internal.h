@@ -130,6 +130,9 @@ void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st);
 constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);
+// CR levels + top + back substitution on blocks already in CR layout (microbench / tests)
+void launch_cr_core(double *D, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
+                    hipStream_t st);
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off,
                             hipStream_t st);

@@ -7,11 +7,23 @@
 // TRIDIAGONAL with p superblocks of n = 6B (padded to a multiple of 16) rows.
 // That system is solved by block cyclic reduction (an odd-even nested
 // dissection): log2(p) levels, each eliminating every other superblock in
-// parallel (one workgroup per superblock), so the critical path is
-// O(log p) dense block operations instead of the O(p) of a banded Cholesky.
+// parallel, so the critical path is O(log p) dense block operations instead of
+// the O(p) of a banded Cholesky.
 //
-// Per superblock the dense work is Cholesky + triangular inverse in LDS and
-// n x n x n products on the FP64 matrix cores (v_mfma_f64_16x16x4_f64).
+// The solve is latency-bound (≈3.4 GFLOP at config 4, spread over 9 levels),
+// so every kernel is shaped for a short critical path:
+//   * k_cr_factor: Cholesky + triangular inverse of one n x n block in LDS.
+//     16x16 diagonal blocks are factored by one wavefront with readlane
+//     broadcasts; the panel solve is row-parallel; the trailing update runs on
+//     the FP64 matrix cores while wave 0 already factors the next diagonal
+//     block (look-ahead); the diagonal inverses are formed in parallel.
+//   * k_cr_elim_gemm / k_cr_update_gemm: one wavefront per 16x16 output tile
+//     (v_mfma_f64_16x16x4f64), workgroups remapped so that the tiles of one
+//     superblock run on one XCD and share its L2; only the lower triangle of
+//     the symmetric diagonal blocks is formed.
+//   * matrix-vector steps (right-hand side, back substitution) are VALU dot
+//     products with the 16x4 lane map of the MFMA tiles and a two-step
+//     cross-lane reduction.
 #include <hip/hip_runtime.h>
 
 #include "sqlm_internal.h"
@@ -20,83 +32,107 @@ namespace sqlm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// C = alpha * op(A) * op(B) + beta * C, n x n row-major; lda/ldb/ldc leading
-// dimensions (LDS operands use an odd stride to stay bank-conflict free).
-// Any number of waves; each wave owns 16x16 output tiles. MFMA f64 16x16x4
-// operand map: lane l holds A[l&15][k + (l>>4)] and B[k + (l>>4)][l&15];
-// result register j holds C[(l>>4) + 4j][l&15]. All K-step operands of a tile
-// are fetched before the MFMA chain so the loads overlap.
-template <bool TA, bool TB, int NMAX>
-__device__ void wg_gemm(double *C, int ldc, const double *A, int lda, const double *B, int ldb, int n, double alpha,
-                        double beta) {
-  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int nt = n >> 4, r16 = lane & 15, k4 = lane >> 4;
-  for (int t = wave; t < nt * nt; t += nw) {
-    const int ti = t / nt, tj = t - ti * nt;
-    const int ar = ti * 16 + r16, bc = tj * 16 + r16;
-    double av[NMAX / 4], bv[NMAX / 4];
-#pragma unroll
-    for (int s = 0; s < NMAX / 4; ++s) {
-      const int k = 4 * s + k4;
-      if (4 * s < n) {
-        av[s] = TA ? A[k * lda + ar] : A[ar * lda + k];
-        bv[s] = TB ? B[bc * ldb + k] : B[k * ldb + bc];
-      }
-    }
-    d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int s = 0; s < NMAX / 4; ++s)
-      if (4 * s < n) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      double *c = C + (ti * 16 + k4 + 4 * j) * ldc + bc;
-      *c = beta == 0.0 ? alpha * acc[j] : alpha * acc[j] + beta * *c;
-    }
-  }
+// Phase timestamps for tools/cr_bench (compiled with -DSQLM_CR_PROF only).
+#ifdef SQLM_CR_PROF
+__device__ long long *g_cr_prof;
+#define CR_PROF(i)                                                                    \
+  do {                                                                                \
+    if (threadIdx.x == 0 && g_cr_prof) g_cr_prof[blockIdx.x * 64 + (i)] = clock64(); \
+  } while (0)
+#else
+#define CR_PROF(i) \
+  do {             \
+  } while (0)
+#endif
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
 }
 
-// y = alpha * op(A) x + beta * y (n x n), one thread per output row.
-template <bool TA>
-__device__ void wg_gemv(double *y, const double *A, int lda, const double *x, int n, double alpha, double beta) {
-  for (int r = threadIdx.x; r < n; r += blockDim.x) {
-    double s = 0.0;
-    for (int k = 0; k < n; ++k) s += (TA ? A[k * lda + r] : A[r * lda + k]) * x[k];
-    y[r] = beta == 0.0 ? alpha * s : alpha * s + beta * y[r];
-  }
+// Dot-product helpers: k runs over 4u + k4 < kCRMaxN with the index clamped
+// to n-1 and a zero weight past n, so every load is unconditional and the
+// compiler issues them all before the first use.
+__device__ __forceinline__ int kclamp(int k, int n) { return k < n ? k : n - 1; }
+
+// sum over the four k4 groups of a wave (lanes r16, r16+16, r16+32, r16+48)
+__device__ __forceinline__ double k4_sum(double s) {
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  return s;
 }
 
-// ---- 16x16 diagonal-block helpers (one wavefront) -------------------------
+// Logical block id with the workgroups that the dispatcher sends to one XCD
+// (hardware id mod 8) made contiguous, so a superblock's tiles share one L2.
+__device__ __forceinline__ int xcd_block(int total) {
+  const int b = blockIdx.x, chunk = (total + 7) >> 3;
+  return (b & 7) * chunk + (b >> 3);
+}
+inline unsigned xcd_grid(int total) { return (unsigned)((total + 7) & ~7); }
 
-// Cholesky of the 16x16 block at (c0, c0) of the LDS matrix L (row r held by
-// lane r in registers), written back lower-triangular.
-__device__ void diag_potrf16(double *L, int ld, int c0, int *fail) {
-  const int lane = threadIdx.x & 63, r = lane & 15;
+// ---- dense block factorization in LDS --------------------------------------
+
+// Panel factorization of block column kb (columns c0 .. c0+15, rows c0 .. n-1):
+// right-looking Cholesky of the 16x16 diagonal block fused with the solve of
+// the rows below it. Wave w holds the 16 diagonal rows in lanes 0..15
+// (redundantly in every participating wave, so no cross-wave traffic) and the
+// rows c0+16+48w .. +48 in lanes 16..63. Column k is broadcast with readlane;
+// 1/l_kk comes from v_rsq_f64 plus one Newton step (no divides).
+__device__ __forceinline__ void panel_factor(double *L, int ld, int n, int c0, double *invd, int *fail, int wave) {
+  const int lane = threadIdx.x & 63;
+  const int i = lane < 16 ? lane : 16 + 48 * wave + (lane - 16);  // row within the panel
+  const bool has = c0 + i < n;
+  double *Lr = L + (c0 + i) * ld + c0;
   double row[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) row[j] = L[(c0 + r) * ld + c0 + j];
+  for (int j = 0; j < 16; ++j) row[j] = has ? Lr[j] : 0.0;
+  bool bad = false;
+  double myinv = 0.0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const double piv = __shfl(row[k], k, 64);
-    if (lane == 0 && !(piv > 0.0)) *fail = 1;
-    const double lkk = piv > 0.0 ? sqrt(piv) : 1.0;
-    if (r == k) row[k] = lkk;
-    if (r > k) row[k] /= lkk;
-    const double lk = row[k];
+    const double piv = readlane_d(row[k], k);
+    double col[16];
 #pragma unroll
-    for (int j = k + 1; j < 16; ++j) {
-      const double ljk = __shfl(row[k], j, 64);
-      if (r >= j) row[j] -= lk * ljk;
-    }
+    for (int j = k + 1; j < 16; ++j) col[j] = readlane_d(row[k], j);
+    bad |= !(piv > 0.0);
+    const double pv = piv > 0.0 ? piv : 1.0;
+    double y = __builtin_amdgcn_rsq(pv);
+    const double h = 0.5 * pv * y;
+    y = fma(y, fma(-h, y, 0.5), y);  // one Newton step on 1/sqrt
+    // row[j] -= l_ik l_jk = (a_ik y)(a_jk y); entries (i, j > i) of the diagonal rows
+    // collect garbage here, they are never read
+    const double t = row[k] * (y * y);
+#pragma unroll
+    for (int j = k + 1; j < 16; ++j) row[j] = fma(-t, col[j], row[j]);
+    row[k] = i == k ? pv * y : (i > k ? row[k] * y : row[k]);
+    if (lane == k) myinv = y;
   }
   if (lane < 16) {
+    if (wave == 0) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) L[(c0 + r) * ld + c0 + j] = j <= r ? row[j] : 0.0;
+      for (int j = 0; j < 16; ++j) Lr[j] = j <= i ? row[j] : 0.0;
+      invd[c0 + lane] = myinv;
+      if (lane == 0 && bad) *fail = 1;
+    }
+  } else if (has) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) Lr[j] = row[j];
   }
+}
+
+__device__ __forceinline__ int panel_waves(int n, int c0) {
+  const int below = n - c0 - 16;
+  return below <= 48 ? 1 : (below + 47) / 48;
 }
 
 // X = inverse of the lower-triangular 16x16 block at (c0, c0) of L; lane c
 // owns column c of X (forward substitution, L rows read as LDS broadcasts).
-__device__ void diag_trtri16(const double *L, int ld, int c0, double *X /*16x16*/) {
+constexpr int kT = 17;  // row stride of the 16x16 LDS scratch tiles (odd: conflict free)
+constexpr int kTile = 16 * kT;
+
+__device__ __forceinline__ void diag_trtri16(const double *L, int ld, int c0, const double *invd,
+                                             double *X /*16 x kT*/) {
   const int lane = threadIdx.x & 63, c = lane & 15;
   double x[16];
 #pragma unroll
@@ -105,114 +141,137 @@ __device__ void diag_trtri16(const double *L, int ld, int c0, double *X /*16x16*
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < rr; ++k) s += lr[k] * x[k];
-    const double inv = 1.0 / lr[rr];
+    const double inv = invd[c0 + rr];
     x[rr] = rr == c ? inv : (rr > c ? -s * inv : 0.0);
   }
   if (lane < 16) {
 #pragma unroll
-    for (int rr = 0; rr < 16; ++rr) X[rr * 16 + c] = x[rr];
+    for (int rr = 0; rr < 16; ++rr) X[rr * kT + c] = x[rr];
   }
 }
 
-// In-LDS blocked Cholesky L L^T = A (lower, n = 16 nt, odd leading dim ld),
-// then L <- L^-1 in place (LAPACK dtrtri lower-blocked order). Diagonal
-// 16x16 blocks are factored / inverted by one wavefront in registers; panel
-// solves, trailing SYRK updates and the off-diagonal inverse products run on
-// the FP64 matrix cores. Dinv: [nt][16][16] LDS scratch, W: [n][16] scratch.
+// One 16x16 trailing-update tile: L[I][J] -= L[I][kb] L[J][kb]^T (one wavefront).
+__device__ __forceinline__ void syrk_tile(double *L, int ld, int c0, int I, int J) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  double a[4], b[4];
+  d4 acc;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    a[s] = -L[(16 * I + r16) * ld + c0 + 4 * s + k4];
+    b[s] = L[(16 * J + r16) * ld + c0 + 4 * s + k4];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = L[(16 * I + k4 + 4 * j) * ld + 16 * J + r16];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) L[(16 * I + k4 + 4 * j) * ld + 16 * J + r16] = acc[j];
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// In-LDS Cholesky L L^T = A (lower block triangle of A read, n = 16 nt <=
+// kCRMaxN, odd leading dim ld), then L <- L^-1 in place (blocked, LAPACK
+// dtrtri lower order). The strict upper block triangle is left undefined.
+// Needs 8 waves. Dinv, W: [nt][16][kT], invd: [n] LDS scratch.
 // Returns false (for every thread) if a pivot is not positive.
-__device__ bool wg_potrf_trtri(double *L, int ld, int n, double *Dinv, double *W, int *fail) {
+__device__ __forceinline__ bool wg_potrf_trtri(double *L, int ld, int n, double *Dinv, double *W, double *invd,
+                                               int *fail) {
   const int tid = threadIdx.x, nw = blockDim.x >> 6, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, k4 = lane >> 4, nt = n >> 4;
   if (tid == 0) *fail = 0;
   __syncthreads();
-  for (int kb = 0; kb < nt; ++kb) {
-    const int c0 = 16 * kb;
-    if (wave == 0) {
-      diag_potrf16(L, ld, c0, fail);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      diag_trtri16(L, ld, c0, Dinv + kb * 256);
+  CR_PROF(1);
+  if (wave < panel_waves(n, 0)) panel_factor(L, ld, n, 0, invd, fail, wave);
+  __syncthreads();
+  CR_PROF(2);
+  for (int kb = 0; kb + 1 < nt; ++kb) {
+    const int c0 = 16 * kb, m = nt - kb - 1;
+    // (A) block column kb+1 absorbs column kb
+    for (int t = wave; t < m; t += nw) syrk_tile(L, ld, c0, kb + 1 + t, kb + 1);
+    __syncthreads();
+    CR_PROF(3 + 2 * kb);
+    // (B) panel kb+1, while the other waves apply column kb to the rest of the trailing matrix
+    const int pw = panel_waves(n, c0 + 16);
+    if (wave < pw) {
+      panel_factor(L, ld, n, c0 + 16, invd, fail, wave);
+    } else {
+      const int mm = m - 1, ntile = mm * (mm + 1) / 2;
+      for (int q = wave - pw; q < ntile; q += nw - pw) {
+        int ib = 0, rem = q;
+        while (rem > ib) { rem -= ib + 1; ++ib; }
+        syrk_tile(L, ld, c0, kb + 2 + ib, kb + 2 + rem);
+      }
     }
     __syncthreads();
-    // panel: L[ib][kb] = A[ib][kb] * Dinv_kb^T  (ib > kb)
-    for (int ib = kb + 1 + wave; ib < nt; ib += nw) {
-      double a[4], b[4];
+    CR_PROF(4 + 2 * kb);
+  }
+  // diagonal inverses, one wave per block
+  for (int kb = wave; kb < nt; kb += nw) diag_trtri16(L, ld, 16 * kb, invd, Dinv + kb * kTile);
+  __syncthreads();
+  CR_PROF(31);
+  // inverse: for jb from last to first, Linv[ib][jb] = -(sum_{kb=jb+1..ib} Linv[ib][kb] L[kb][jb]) Dinv_jb
+  for (int jb = nt - 2; jb >= 0; --jb) {
+    const int c0 = 16 * jb;
+    for (int ib = jb + 1 + wave; ib < nt; ib += nw) {
+      double a[4 * (kCRMaxN / 16)], b[4 * (kCRMaxN / 16)];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        a[s] = L[(16 * ib + r16) * ld + c0 + 4 * s + k4];
-        b[s] = Dinv[kb * 256 + r16 * 16 + 4 * s + k4];  // B[k][col] = Dinv[col][k]
+      for (int t = 0; t < kCRMaxN / 16; ++t) {
+        const int kb = jb + 1 + t;
+        if (kb <= ib) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            a[4 * t + s] = kb == ib ? Dinv[ib * kTile + r16 * kT + 4 * s + k4]
+                                    : L[(16 * kb + r16) * ld + 16 * ib + 4 * s + k4];  // Linv[ib][kb] parked at (kb, ib)
+            b[4 * t + s] = L[(16 * kb + 4 * s + k4) * ld + c0 + r16];
+          }
+        }
       }
       d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+      for (int t = 0; t < kCRMaxN / 16; ++t)
+        if (jb + 1 + t <= ib) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) L[(16 * ib + k4 + 4 * j) * ld + c0 + r16] = acc[j];
-    }
-    __syncthreads();
-    // trailing SYRK: L[ib][jb] -= L[ib][kb] L[jb][kb]^T, kb < jb <= ib
-    const int m = nt - kb - 1, ntile = m * (m + 1) / 2;
-    for (int q = wave; q < ntile; q += nw) {
-      int ib = 0, rem = q;
-      while (rem > ib) { rem -= ib + 1; ++ib; }
-      const int jb = rem;  // 0 <= jb <= ib within the trailing matrix
-      const int I = kb + 1 + ib, J = kb + 1 + jb;
-      double a[4], b[4];
+          for (int s = 0; s < 4; ++s)
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[4 * t + s], b[4 * t + s], acc, 0, 0, 0);
+        }
+      double *Wi = W + kTile * ib;  // wave-private (one ib per wave)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Wi[(k4 + 4 * j) * kT + r16] = acc[j];
+      wave_sync();
+      double a2[4], b2[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        a[s] = -L[(16 * I + r16) * ld + c0 + 4 * s + k4];
-        b[s] = L[(16 * J + r16) * ld + c0 + 4 * s + k4];
+        a2[s] = -Wi[r16 * kT + 4 * s + k4];
+        b2[s] = Dinv[jb * kTile + (4 * s + k4) * kT + r16];
       }
-      d4 acc;
+      d4 acc2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = L[(16 * I + k4 + 4 * j) * ld + 16 * J + r16];
+      for (int s = 0; s < 4; ++s) acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], b2[s], acc2, 0, 0, 0);
+      // park Linv[ib][jb] in the unused upper block (jb, ib): other waves still read L[ib][jb]
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) L[(16 * I + k4 + 4 * j) * ld + 16 * J + r16] = acc[j];
+      for (int j = 0; j < 4; ++j) L[(c0 + k4 + 4 * j) * ld + 16 * ib + r16] = acc2[j];
     }
     __syncthreads();
   }
-  for (int idx = tid; idx < n * n; idx += blockDim.x) {  // strict upper triangle -> 0
-    const int i = idx / n, j = idx - i * n;
-    if (j > i) L[i * ld + j] = 0.0;
+  CR_PROF(32);
+  // move the parked blocks down, diagonal blocks <- Dinv
+  for (int t = wave; t < nt * (nt + 1) / 2; t += nw) {  // lower tiles (ib >= jb), one wave each
+    int ib = 0, jb = t;
+    while (jb > ib) { jb -= ib + 1; ++ib; }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int q = lane + 64 * u, r = q >> 4, c = q & 15;
+      L[(16 * ib + r) * ld + 16 * jb + c] =
+          ib > jb ? L[(16 * jb + r) * ld + 16 * ib + c] : Dinv[ib * kTile + r * kT + c];
+    }
   }
   __syncthreads();
-  // inverse: for jb from last to first, Linv21 = -(Linv22 L21) Dinv_jb, Linv11 = Dinv_jb
-  for (int jb = nt - 1; jb >= 0; --jb) {
-    const int c0 = 16 * jb;
-    for (int ib = jb + 1 + wave; ib < nt; ib += nw) {  // W[ib] = sum_{kb=jb+1..ib} Linv[ib][kb] L[kb][jb]
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-      for (int kb = jb + 1; kb <= ib; ++kb) {
-        double a[4], b[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          a[s] = L[(16 * ib + r16) * ld + 16 * kb + 4 * s + k4];
-          b[s] = L[(16 * kb + 4 * s + k4) * ld + c0 + r16];
-        }
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) W[(16 * ib + k4 + 4 * j) * 16 + r16] = acc[j];
-    }
-    __syncthreads();
-    for (int ib = jb + 1 + wave; ib < nt; ib += nw) {  // L[ib][jb] = -W[ib] Dinv_jb
-      double a[4], b[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        a[s] = -W[(16 * ib + r16) * 16 + 4 * s + k4];
-        b[s] = Dinv[jb * 256 + (4 * s + k4) * 16 + r16];
-      }
-      d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) L[(16 * ib + k4 + 4 * j) * ld + c0 + r16] = acc[j];
-    }
-    for (int e = tid; e < 256; e += blockDim.x) L[(c0 + e / 16) * ld + c0 + e % 16] = Dinv[jb * 256 + e];
-    __syncthreads();
-  }
+  CR_PROF(33);
   return *fail == 0;
 }
 
@@ -223,6 +282,9 @@ struct CRView {
 };
 
 __device__ __forceinline__ double *blk(double *base, int I, int n) { return base + (size_t)I * n * n; }
+
+// LDS footprint of the factor kernels: L (n x (n+1)) + tmp (2n) + Dinv (17n) + W (17n) + invd (n)
+inline size_t cr_factor_lds(int n) { return ((size_t)n * (n + 1) + 37 * (size_t)n) * sizeof(double); }
 
 // BSR (upper, 6x6 blocks) -> superblock D_I (symmetric) and E_I = S(I, I+1); g -> g_I.
 __global__ __launch_bounds__(256) void k_cr_scatter(DevProblem d, CRView v) {
@@ -254,25 +316,56 @@ __global__ __launch_bounds__(256) void k_cr_scatter(DevProblem d, CRView v) {
   if (i == 0 && threadIdx.x == 0) v.flags[0] = 1;
 }
 
+// Factor superblock I into LDS: L <- chol(D_I)^-1; z = L g_I kept in LDS (tmp).
+// Every wave returns; afterwards L holds Linv (lower) and tmp[0:n] = g_I.
+__device__ __forceinline__ void cr_factor_block(const CRView &v, int I, double *lds, int *fail) {
+  const int n = v.n, ld = n + 1, nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n, *W = Dinv + 17 * n, *invd = W + 17 * n;
+  const double *Dg = blk(v.D, I, n);
+  CR_PROF(0);
+  {  // lower block triangle only; all loads in flight before the LDS stores
+    constexpr int kRows = (kCRMaxN + 7) / 8;
+    double v0[kRows], v1[kRows];
+#pragma unroll
+    for (int t = 0; t < kRows; ++t) {
+      const int r = wave + nw * t, cend = (r | 15) + 1;
+      v0[t] = (r < n && lane < cend) ? Dg[r * n + lane] : 0.0;
+      v1[t] = (r < n && lane + 64 < cend) ? Dg[r * n + lane + 64] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < kRows; ++t) {
+      const int r = wave + nw * t, cend = (r | 15) + 1;
+      if (r < n && lane < cend) L[r * ld + lane] = v0[t];
+      if (r < n && lane + 64 < cend) L[r * ld + lane + 64] = v1[t];
+    }
+  }
+  for (int k = threadIdx.x; k < n; k += blockDim.x) tmp[k] = v.g[(size_t)I * n + k];
+  if (!wg_potrf_trtri(L, ld, n, Dinv, W, invd, fail) && threadIdx.x == 0) v.flags[0] = 0;
+}
+
 // Level h, step 1: every odd superblock I (I = h, 3h, 5h, ...) is factored:
-// D_I <- Linv_I = chol(D_I)^-1 (in place), g_I <- z_I = Linv_I g_I.
+// D_I <- Linv_I = chol(D_I)^-1 (lower block triangle, zero above), g_I <- z_I = Linv_I g_I.
 __global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int fail;
-  const int I = h + 2 * h * blockIdx.x, n = v.n, ld = n + 1;
-  double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n, *W = Dinv + 16 * n;
+  const int I = h + 2 * h * blockIdx.x, n = v.n, ld = n + 1, nt = n >> 4;
+  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  cr_factor_block(v, I, lds, &fail);
+  const double *L = lds, *tmp = lds + n * ld;
   double *Dg = blk(v.D, I, n);
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x) L[(k / n) * ld + k % n] = Dg[k];
-  for (int k = threadIdx.x; k < n; k += blockDim.x) tmp[k] = v.g[(size_t)I * n + k];
-  __syncthreads();
-  if (!wg_potrf_trtri(L, ld, n, Dinv, W, &fail) && threadIdx.x == 0) v.flags[0] = 0;
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x) Dg[k] = L[(k / n) * ld + k % n];
-  wg_gemv<false>(v.g + (size_t)I * n, L, ld, tmp, n, 1.0, 0.0);
+  for (int r = wave; r < n; r += nw)
+    for (int c = lane; c < n; c += 64) Dg[r * n + c] = c <= (r | 15) ? L[r * ld + c] : 0.0;
+  if (wave < nt) {  // z = Linv g, rows 16 wave .. +16
+    const int ar = 16 * wave + r16;
+    double s = 0.0;
+    for (int k = k4; k < 16 * (wave + 1); k += 4) s += L[ar * ld + k] * tmp[k];
+    s = k4_sum(s);
+    if (k4 == 0) v.g[(size_t)I * n + ar] = s;
+  }
 }
 
-// One wavefront computes one 16x16 tile C[ti][tj] (+)= alpha * op(A) op(B) over K = n,
-// skipping K blocks that are zero because A is lower triangular (LA) or
-// A^T is upper triangular... (lower-triangular A used un-transposed only).
+// One wavefront computes one 16x16 tile acc = op(A) op(B) over K = n,
+// skipping K blocks that are zero because A is lower triangular (LA).
 template <bool TA, bool TB, bool LA>
 __device__ __forceinline__ d4 tile_gemm(const double *A, const double *B, int n, int ti, int tj) {
   const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
@@ -306,9 +399,11 @@ __device__ __forceinline__ void tile_store(double *C, int n, int ti, int tj, con
 
 // Level h, step 2: A_I = Linv_I S(I, I-h) = Linv_I E_{I-h}^T and
 // C_I = Linv_I S(I, I+h) = Linv_I E_I, one 16x16 tile per wavefront.
-__global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h) {
+__global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
   const int n = v.n, nt = n >> 4, per = nt * nt;
-  const int odd = blockIdx.x / (2 * per), rem = blockIdx.x - odd * 2 * per;
+  const int odd = lb / (2 * per), rem = lb - odd * 2 * per;
   const int which = rem / per, t = rem - which * per, ti = t / nt, tj = t - ti * nt;
   const int I = h + 2 * h * odd;
   if (which == 0) {
@@ -321,32 +416,20 @@ __global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h) {
 }
 
 // Level h, step 3: every even superblock J absorbs its eliminated neighbours:
-// D_J -= A_{J+h}^T A_{J+h} + C_{J-h}^T C_{J-h};  E_J = -A_{J+h}^T C_{J+h};
-// g_J -= A_{J+h}^T z_{J+h} + C_{J-h}^T z_{J-h}. One wavefront per output tile
-// (plus one per block for g).
-__global__ __launch_bounds__(64) void k_cr_update_gemm(CRView v, int h) {
-  const int n = v.n, nt = n >> 4, per = nt * nt;
-  const int ev = blockIdx.x / (2 * per + 1), rem = blockIdx.x - ev * (2 * per + 1);
+// D_J -= A_{J+h}^T A_{J+h} + C_{J-h}^T C_{J-h} (lower tiles only);
+// E_J = -A_{J+h}^T C_{J+h}; g_J -= A_{J+h}^T z_{J+h} + C_{J-h}^T z_{J-h}.
+// Work items per even block: nt(nt+1)/2 D tiles, nt^2 E tiles, nt g slices.
+__global__ __launch_bounds__(64) void k_cr_update_gemm(CRView v, int h, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int n = v.n, nt = n >> 4, nd = nt * (nt + 1) / 2, items = nd + nt * nt + nt;
+  const int ev = lb / items, rem = lb - ev * items;
   const int J = 2 * h * ev;
   const bool right = J + h < v.p, left = J >= h;
-  if (rem == 2 * per) {  // right-hand side
-    double *gj = v.g + (size_t)J * n;
-    for (int r = threadIdx.x; r < n; r += 64) {
-      double s = gj[r];
-      if (right) {
-        const double *A = blk(v.A, J + h, n), *z = v.g + (size_t)(J + h) * n;
-        for (int k = 0; k < n; ++k) s -= A[k * n + r] * z[k];
-      }
-      if (left) {
-        const double *C = blk(v.C, J - h, n), *z = v.g + (size_t)(J - h) * n;
-        for (int k = 0; k < n; ++k) s -= C[k * n + r] * z[k];
-      }
-      gj[r] = s;
-    }
-    return;
-  }
-  const int which = rem / per, t = rem - which * per, ti = t / nt, tj = t - ti * nt;
-  if (which == 0) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  if (rem < nd) {
+    int ti = 0, tj = rem;
+    while (tj > ti) { tj -= ti + 1; ++ti; }
     d4 acc = {0.0, 0.0, 0.0, 0.0};
     if (right) acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.A, J + h, n), n, ti, tj);
     if (left) {
@@ -354,40 +437,99 @@ __global__ __launch_bounds__(64) void k_cr_update_gemm(CRView v, int h) {
       acc += a2;
     }
     if (right || left) tile_store(blk(v.D, J, n), n, ti, tj, acc, -1.0, true);
-  } else if (right && J + 2 * h < v.p) {
-    const d4 acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.C, J + h, n), n, ti, tj);
-    tile_store(blk(v.E, J, n), n, ti, tj, acc, -1.0, false);
+  } else if (rem < nd + nt * nt) {
+    const int t = rem - nd, ti = t / nt, tj = t - ti * nt;
+    if (right && J + 2 * h < v.p) {
+      const d4 acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.C, J + h, n), n, ti, tj);
+      tile_store(blk(v.E, J, n), n, ti, tj, acc, -1.0, false);
+    }
+  } else {  // right-hand side rows 16 ti .. +16
+    const int ar = 16 * (rem - nd - nt * nt) + r16;
+    double s = 0.0;
+    if (right) {
+      const double *A = blk(v.A, J + h, n), *z = v.g + (size_t)(J + h) * n;
+#pragma unroll
+      for (int u = 0; u < kCRMaxN / 4; ++u) {
+        const int k = kclamp(4 * u + k4, n);
+        s += A[k * n + ar] * (4 * u < n ? z[k] : 0.0);
+      }
+    }
+    if (left) {
+      const double *C = blk(v.C, J - h, n), *z = v.g + (size_t)(J - h) * n;
+#pragma unroll
+      for (int u = 0; u < kCRMaxN / 4; ++u) {
+        const int k = kclamp(4 * u + k4, n);
+        s += C[k * n + ar] * (4 * u < n ? z[k] : 0.0);
+      }
+    }
+    s = k4_sum(s);
+    if (k4 == 0) v.g[(size_t)J * n + ar] -= s;
   }
 }
 
-// Last remaining superblock 0: x_0 = D_0^-1 g_0.
+// Last remaining superblock 0: x_0 = D_0^-1 g_0 = Linv^T (Linv g).
 __global__ __launch_bounds__(512) void k_cr_top(CRView v) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int fail;
-  const int n = v.n, ld = n + 1;
-  double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n, *W = Dinv + 16 * n;
-  for (int k = threadIdx.x; k < n * n; k += blockDim.x) L[(k / n) * ld + k % n] = v.D[k];
+  const int n = v.n, ld = n + 1, nt = n >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  cr_factor_block(v, 0, lds, &fail);
+  const double *L = lds;
+  double *tmp = lds + n * ld, *z = tmp + n;
+  const int ar = 16 * wave + r16;
+  if (wave < nt) {
+    double s = 0.0;
+    for (int k = k4; k < 16 * (wave + 1); k += 4) s += L[ar * ld + k] * tmp[k];
+    s = k4_sum(s);
+    if (k4 == 0) z[ar] = s;
+  }
   __syncthreads();
-  if (!wg_potrf_trtri(L, ld, n, Dinv, W, &fail) && threadIdx.x == 0) v.flags[0] = 0;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) tmp[k] = v.g[k];
-  __syncthreads();
-  double *z = tmp + n;
-  wg_gemv<false>(z, L, ld, tmp, n, 1.0, 0.0);
-  __syncthreads();
-  wg_gemv<true>(v.x, L, ld, z, n, 1.0, 0.0);
+  if (wave < nt) {
+    double s = 0.0;
+    for (int k = 16 * wave + k4; k < n; k += 4) s += L[k * ld + ar] * z[k];
+    s = k4_sum(s);
+    if (k4 == 0) v.x[ar] = s;
+  }
+  CR_PROF(34);
 }
 
 // Back substitution at level h: x_I = Linv_I^T (z_I - A_I x_{I-h} - C_I x_{I+h}).
-__global__ __launch_bounds__(256) void k_cr_back(CRView v, int h) {
+// One wave per 16-row slice (blockDim = 64 nt).
+__global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
   extern __shared__ __attribute__((aligned(16))) double t[];
   const int I = h + 2 * h * blockIdx.x, n = v.n;
-  for (int k = threadIdx.x; k < n; k += blockDim.x) t[k] = v.g[(size_t)I * n + k];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  const int ar = 16 * wave + r16;
+  const bool right = I + h < v.p;
+  {
+    const double *A = blk(v.A, I, n) + ar * n, *xl = v.x + (size_t)(I - h) * n;
+    const double *C = blk(v.C, I, n) + ar * n, *xr = v.x + (size_t)(I + h) * n;
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < kCRMaxN / 4; ++u) {
+      const int k = kclamp(4 * u + k4, n);
+      s += A[k] * (4 * u < n ? xl[k] : 0.0);
+    }
+    if (right) {
+#pragma unroll
+      for (int u = 0; u < kCRMaxN / 4; ++u) {
+        const int k = kclamp(4 * u + k4, n);
+        s += C[k] * (4 * u < n ? xr[k] : 0.0);
+      }
+    }
+    s = k4_sum(s);
+    if (k4 == 0) t[ar] = v.g[(size_t)I * n + ar] - s;
+  }
   __syncthreads();
-  wg_gemv<false>(t, blk(v.A, I, n), n, v.x + (size_t)(I - h) * n, n, -1.0, 1.0);
-  __syncthreads();
-  if (I + h < v.p) wg_gemv<false>(t, blk(v.C, I, n), n, v.x + (size_t)(I + h) * n, n, -1.0, 1.0);
-  __syncthreads();
-  wg_gemv<true>(v.x + (size_t)I * n, blk(v.D, I, n), n, t, n, 1.0, 0.0);
+  const double *Li = blk(v.D, I, n);
+  double s = 0.0;  // Linv is lower triangular: k >= 16 wave
+#pragma unroll
+  for (int u = 0; u < kCRMaxN / 4; ++u) {
+    const int k = kclamp(4 * u + k4, n);
+    s += Li[k * n + ar] * ((4 * u >= 16 * wave && 4 * u < n) ? t[k] : 0.0);
+  }
+  s = k4_sum(s);
+  if (k4 == 0) v.x[(size_t)I * n + ar] = s;
 }
 
 __global__ void k_cr_gather(DevProblem d, CRView v) {
@@ -397,28 +539,34 @@ __global__ void k_cr_gather(DevProblem d, CRView v) {
   d.dx[k] = v.flags[0] ? v.x[(size_t)I * v.n + 6 * li + r] : 0.0;
 }
 
+// Levels, top solve and back substitution on D/E/g already in CR layout.
+void launch_cr_core(double *D, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
+                    hipStream_t st) {
+  CRView v{p, n, 0, 0, D, E, A, C, g, x, flags};
+  const size_t lds = cr_factor_lds(n);
+  const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt;
+  int h = 1;
+  for (; h < p; h *= 2) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
+    const int n_even = (p + 2 * h - 1) / (2 * h);
+    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
+    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
+    hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
+  }
+  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
+  for (h /= 2; h >= 1; h /= 2) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
+    hipLaunchKernelGGL(k_cr_back, dim3(n_odd), dim3(64 * nt), (size_t)n * sizeof(double), st, v, h);
+  }
+}
+
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
   CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags};
   const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
   if (hipMemsetAsync(d.cr_D, 0, blkbytes, st) != hipSuccess) return -2;
   if (hipMemsetAsync(d.cr_E, 0, blkbytes, st) != hipSuccess) return -2;
   hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
-  // L (n x (n+1)) + tmp (2n) + Dinv (nt x 256 = 16n) + W (16n)
-  const size_t lds = ((size_t)pl.n * (pl.n + 1) + 2 * pl.n + 32 * (size_t)pl.n) * sizeof(double);
-  int h = 1;
-  for (; h < pl.p; h *= 2) {
-    const int n_odd = (pl.p - h + 2 * h - 1) / (2 * h);
-    const int n_even = (pl.p + 2 * h - 1) / (2 * h);
-    const int per = (pl.n / 16) * (pl.n / 16);
-    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
-    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(n_odd * 2 * per), dim3(64), 0, st, v, h);
-    hipLaunchKernelGGL(k_cr_update_gemm, dim3(n_even * (2 * per + 1)), dim3(64), 0, st, v, h);
-  }
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
-  for (h /= 2; h >= 1; h /= 2) {
-    const int n_odd = (pl.p - h + 2 * h - 1) / (2 * h);
-    hipLaunchKernelGGL(k_cr_back, dim3(n_odd), dim3(256), (size_t)pl.n * sizeof(double), st, v, h);
-  }
+  launch_cr_core(d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
   hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }

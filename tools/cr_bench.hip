@@ -1,0 +1,194 @@
+// cr_bench — microbenchmark + residual check of the block-cyclic-reduction
+// solve (sqlm_rcs_solve.hip) on a random SPD block-tridiagonal system of p
+// superblocks of n rows: D_I = 2n I + sym(U[-.5,.5]), E_I = U[-.5,.5].
+// Usage: cr_bench [p] [n] [reps]. Prints one JSON line.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#define SQLM_CR_PROF 1
+#include "../sqrtlm-slam_amd/csrc/sqlm_rcs_solve.hip"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 2; } } while (0)
+
+int main(int argc, char **argv) {
+  const int p = argc > 1 ? std::atoi(argv[1]) : 278, n = argc > 2 ? std::atoi(argv[2]) : 112;
+  const int reps = argc > 3 ? std::atoi(argv[3]) : 20;
+  if (n % 16 || n > sqlm::kCRMaxN || p < 1) { std::printf("bad shape\n"); return 1; }
+  const size_t nb = (size_t)p * n * n;
+  std::mt19937_64 rng(7);
+  std::uniform_real_distribution<double> U(-0.5, 0.5);
+  std::vector<double> D(nb), E(nb, 0.0), g((size_t)p * n);
+  for (int I = 0; I < p; ++I) {
+    double *d = D.data() + (size_t)I * n * n;
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c <= r; ++c) d[r * n + c] = d[c * n + r] = (r == c ? 2.0 * n : 0.0) + U(rng);
+    if (I + 1 < p)
+      for (size_t k = 0; k < (size_t)n * n; ++k) E[(size_t)I * n * n + k] = U(rng);
+  }
+  for (auto &v : g) v = U(rng);
+  double *dD, *dE, *dA, *dC, *dg, *dx;
+  int *dflags;
+  CK(hipMalloc(&dD, nb * 8)); CK(hipMalloc(&dE, nb * 8)); CK(hipMalloc(&dA, nb * 8)); CK(hipMalloc(&dC, nb * 8));
+  CK(hipMalloc(&dg, g.size() * 8)); CK(hipMalloc(&dx, g.size() * 8)); CK(hipMalloc(&dflags, 16));
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  {  // phase profile of one k_cr_top launch (single block, thread 0 timestamps)
+    long long *dprof, zero[64] = {0}, prof[64];
+    CK(hipMalloc(&dprof, 64 * 8));
+    CK(hipMemcpy(dprof, zero, 64 * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(sqlm::g_cr_prof), &dprof, sizeof(dprof)));
+    CK(hipMemcpy(dD, D.data(), (size_t)n * n * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dg, g.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    sqlm::CRView v{1, n, 0, 0, dD, dE, dA, dC, dg, dx, dflags};
+    hipLaunchKernelGGL(sqlm::k_cr_top, dim3(1), dim3(512), sqlm::cr_factor_lds(n), st, v);
+    CK(hipStreamSynchronize(st));
+    CK(hipMemcpy(prof, dprof, 64 * 8, hipMemcpyDeviceToHost));
+    long long *nul = nullptr;
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(sqlm::g_cr_prof), &nul, sizeof(nul)));
+    std::printf("{\"top_phase_cycles\": {");
+    for (int i = 1; i < 64; ++i)
+      if (prof[i]) std::printf("\"%d\": %lld, ", i, prof[i] - prof[0]);
+    std::printf("\"end\": 0}}\n");
+  }
+  {  // k_cr_factor alone (h = 1): Linv D Linv^T == I and z == Linv g on every odd block
+    CK(hipMemcpy(dD, D.data(), nb * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice));
+    sqlm::CRView v{p, n, 0, 0, dD, dE, dA, dC, dg, dx, dflags};
+    const int n_odd = p / 2;
+    if (n_odd > 0) {
+      hipLaunchKernelGGL(sqlm::k_cr_factor, dim3(n_odd), dim3(512), sqlm::cr_factor_lds(n), st, v, 1);
+      CK(hipStreamSynchronize(st));
+      std::vector<double> Li(nb), z(g.size());
+      CK(hipMemcpy(Li.data(), dD, nb * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(z.data(), dg, z.size() * 8, hipMemcpyDeviceToHost));
+      double emax = 0.0, zmax = 0.0;
+      for (int I = 1; I < p; I += 2) {
+        const double *Lb = Li.data() + (size_t)I * n * n, *Db = D.data() + (size_t)I * n * n;
+        std::vector<double> T((size_t)n * n, 0.0);  // T = Linv D
+        for (int r = 0; r < n; ++r)
+          for (int k = 0; k < n; ++k) {
+            const double a = Lb[r * n + k];
+            if (a != 0.0) for (int c = 0; c < n; ++c) T[r * n + c] += a * Db[k * n + c];
+          }
+        for (int r = 0; r < n; ++r)
+          for (int c = 0; c < n; ++c) {
+            double sum = 0.0;
+            for (int k = 0; k < n; ++k) sum += T[r * n + k] * Lb[c * n + k];
+            emax = std::max(emax, std::fabs(sum - (r == c ? 1.0 : 0.0)));
+          }
+        for (int r = 0; r < n; ++r) {
+          double sum = 0.0;
+          for (int k = 0; k < n; ++k) sum += Lb[r * n + k] * g[(size_t)I * n + k];
+          zmax = std::max(zmax, std::fabs(sum - z[(size_t)I * n + r]));
+        }
+      }
+      std::printf("{\"factor_check\": {\"blocks\": %d, \"max_err_LDLt_I\": %.3e, \"max_err_z\": %.3e}}\n", n_odd,
+                  emax, zmax);
+    }
+  }
+  const int one = 1;
+  double best = 1e30, sum = 0.0;
+  for (int it = 0; it < reps + 2; ++it) {  // 2 warmups
+    CK(hipMemcpyAsync(dD, D.data(), nb * 8, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(dE, E.data(), nb * 8, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(dflags, &one, 4, hipMemcpyHostToDevice, st));
+    CK(hipEventRecord(e0, st));
+    sqlm::launch_cr_core(dD, dE, dA, dC, dg, dx, dflags, p, n, st);
+    CK(hipEventRecord(e1, st));
+    CK(hipStreamSynchronize(st));
+    CK(hipGetLastError());
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (it >= 2) { best = std::min(best, (double)ms); sum += ms; }
+  }
+  std::vector<double> x(g.size());
+  int flag = 0;
+  CK(hipMemcpy(x.data(), dx, x.size() * 8, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(&flag, dflags, 4, hipMemcpyDeviceToHost));
+  if (p == 2) {  // stage-by-stage host check of the one-level solve
+    std::vector<double> dDh(nb), dAh(nb), dgh(g.size());
+    CK(hipMemcpy(dDh.data(), dD, nb * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(dAh.data(), dA, nb * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(dgh.data(), dg, g.size() * 8, hipMemcpyDeviceToHost));
+    const size_t nn = (size_t)n * n;
+    const double *L1 = dDh.data() + nn, *E0 = E.data(), *A1 = dAh.data() + nn;
+    double ea = 0, ed = 0, eg = 0, ex0 = 0, ex1 = 0;
+    std::vector<double> Ae(nn, 0.0), D0((size_t)nn), g0(n), z1(n);
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        double sum = 0;
+        for (int k = 0; k < n; ++k) sum += L1[r * n + k] * E0[c * n + k];
+        Ae[r * n + c] = sum;
+        ea = std::max(ea, std::fabs(sum - A1[r * n + c]));
+      }
+    for (int r = 0; r < n; ++r) {
+      double sum = 0;
+      for (int k = 0; k < n; ++k) sum += L1[r * n + k] * g[n + k];
+      z1[r] = sum;
+    }
+    for (int r = 0; r < n; ++r)
+      for (int c = 0; c < n; ++c) {
+        double sum = 0;
+        for (int k = 0; k < n; ++k) sum += Ae[k * n + r] * Ae[k * n + c];
+        D0[r * n + c] = D[r * n + c] - sum;
+        if (c <= (r | 15)) ed = std::max(ed, std::fabs(D0[r * n + c] - dDh[r * n + c]));
+      }
+    for (int r = 0; r < n; ++r) {
+      double sum = 0;
+      for (int k = 0; k < n; ++k) sum += Ae[k * n + r] * z1[k];
+      g0[r] = g[r] - sum;
+      eg = std::max(eg, std::fabs(g0[r] - dgh[r]));
+    }
+    // x0 = D0^-1 g0 by host Cholesky
+    std::vector<double> C(D0), y(g0);
+    for (int k = 0; k < n; ++k) {
+      C[k * n + k] = std::sqrt(C[k * n + k]);
+      for (int i = k + 1; i < n; ++i) C[i * n + k] /= C[k * n + k];
+      for (int j = k + 1; j < n; ++j)
+        for (int i = j; i < n; ++i) C[i * n + j] -= C[i * n + k] * C[j * n + k];
+    }
+    for (int i = 0; i < n; ++i) { for (int k = 0; k < i; ++k) y[i] -= C[i * n + k] * y[k]; y[i] /= C[i * n + i]; }
+    for (int i = n - 1; i >= 0; --i) { for (int k = i + 1; k < n; ++k) y[i] -= C[k * n + i] * y[k]; y[i] /= C[i * n + i]; }
+    std::vector<double> xh(2 * n);
+    CK(hipMemcpy(xh.data(), dx, 2 * n * 8, hipMemcpyDeviceToHost));
+    for (int r = 0; r < n; ++r) ex0 = std::max(ex0, std::fabs(y[r] - xh[r]));
+    for (int r = 0; r < n; ++r) {
+      double t = z1[r];
+      for (int k = 0; k < n; ++k) t -= Ae[r * n + k] * y[k];
+      z1[r] = t;
+    }
+    for (int r = 0; r < n; ++r) {
+      double sum = 0;
+      for (int k = 0; k < n; ++k) sum += L1[k * n + r] * z1[k];
+      ex1 = std::max(ex1, std::fabs(sum - xh[n + r]));
+    }
+    std::printf("{\"stages\": {\"A1\": %.3e, \"D0_lower\": %.3e, \"g0\": %.3e, \"x0\": %.3e, \"x1\": %.3e}}\n", ea,
+                ed, eg, ex0, ex1);
+  }
+  // residual r = T x - g with T block tridiagonal (D_I, E_I above, E_{I-1}^T below)
+  double rmax = 0.0, gmax = 0.0;
+  for (int I = 0; I < p; ++I)
+    for (int r = 0; r < n; ++r) {
+      const double *d = D.data() + (size_t)I * n * n;
+      double s = 0.0;
+      for (int c = 0; c < n; ++c) s += d[r * n + c] * x[(size_t)I * n + c];
+      if (I + 1 < p)
+        for (int c = 0; c < n; ++c) s += E[(size_t)I * n * n + r * n + c] * x[(size_t)(I + 1) * n + c];
+      if (I > 0)
+        for (int c = 0; c < n; ++c) s += E[(size_t)(I - 1) * n * n + c * n + r] * x[(size_t)(I - 1) * n + c];
+      rmax = std::max(rmax, std::fabs(s - g[(size_t)I * n + r]));
+      gmax = std::max(gmax, std::fabs(g[(size_t)I * n + r]));
+    }
+  std::printf("{\"p\": %d, \"n\": %d, \"ms_best\": %.4f, \"ms_avg\": %.4f, \"flag\": %d, \"rel_residual\": %.3e}\n", p, n,
+              best, sum / reps, flag, rmax / gmax);
+  return (flag == 1 && rmax / gmax < 1e-10) ? 0 : 3;
+}
