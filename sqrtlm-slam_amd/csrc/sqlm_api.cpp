@@ -1001,6 +1001,11 @@ int sqlm_bench_iterations(sqlm_ctx *c, int warmup, int n, double *ms_per_iter, d
   return SQLM_OK;
 }
 
+#ifdef SQLM_TILE_PROF
+// Diagnostic build only: 64 tiles x 8 phase cycle sums of k_rcs_tile.
+int sqlm_debug_tile_profile(long long *out) { return sqlm::tile_profile_read(out); }
+#endif
+
 const char *sqlm_kernel_timer_name(int i) {
   return (i >= 0 && i < SQLM_NKERNEL_TIMERS) ? kTimerNames[i] : "";
 }

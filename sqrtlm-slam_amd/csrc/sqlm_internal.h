@@ -127,6 +127,9 @@ void launch_damp(const DevProblem &d, double lambda, hipStream_t st);
 void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st);
 void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st);
 void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st);
+#ifdef SQLM_TILE_PROF
+int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase counters
+#endif
 constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);

@@ -519,12 +519,13 @@ void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStrea
 // observation) and w_l = R'^-T b_l:
 //   S_ij = H_pp,i d_ij + lambda I d_ij - sum_l Y_li^T Y_lj,  g_i = b_p,i - sum_l Y_li^T w_l.
 // A tile is a run of consecutive landmark slots whose free cameras form a small
-// sorted window C_t (|C_t| <= 24, 6|C_t| <= 144 columns). ONE wavefront owns a
-// tile: per landmark it stages the dense 3 x 6|C_t| row block Y_l (plus a zero
-// 4th row) in LDS and accumulates G_t += Y_l^T Y_l with v_mfma_f64_16x16x4_f64
-// into NT(NT+1)/2 upper 16x16 accumulator tiles held in AGPRs, skipping the
-// tiles outside the landmark's column span. Single-wave ownership means no
-// atomics and a fixed summation order (bitwise deterministic).
+// sorted window C_t (|C_t| <= 24, 6|C_t| <= 144 columns). One workgroup of
+// kTileWaves wavefronts owns a tile: per landmark it stages the dense
+// 3 x 6|C_t| row block Y_l (plus a zero 4th row) in LDS and accumulates
+// G_t += Y_l^T Y_l with v_mfma_f64_16x16x4_f64 into NT(NT+1)/2 upper 16x16
+// accumulator tiles held in AGPRs (tile q owned by wave q % kTileWaves),
+// skipping the tiles outside the landmark's column span. Fixed ownership
+// means no atomics and a fixed summation order (bitwise deterministic).
 typedef double d4v __attribute__((ext_vector_type(4)));
 
 // Landmarks are consumed in batches of 4: landmark li of a batch occupies rows
@@ -532,13 +533,46 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 // K=4 step of v_mfma_f64_16x16x4_f64, so one batch = 4 K-steps per 16x16 tile.
 // The raw P columns of the next batch are prefetched into registers while the
 // current batch runs on the matrix cores.
-constexpr int kTileBL = 4, kTileIPT = 4;  // fast path: k <= 128 * 4 / (6 * 4) = 21
+constexpr int kTileWaves = 4, kTileThreads = 64 * kTileWaves;
 
-// MFMA phase of one batch for the accumulator tiles of wave parity P:
-// acc[q/2] += sum_ks Y[4ks..4ks+3][ti-tile]^T Y[4ks..4ks+3][tj-tile].
+// Phase cycle counters of the first kTileProfTiles tiles (diagnostic build
+// -DSQLM_TILE_PROF only; read with sqlm_debug_tile_profile).
+#ifdef SQLM_TILE_PROF
+constexpr int kTileProfTiles = 64, kTileProfSlots = 8;
+__device__ long long g_tile_prof[kTileProfTiles][kTileProfSlots];
+#define TP_DECL                \
+  long long tp_acc[kTileProfSlots] = {}; \
+  long long tp_last = clock64();
+#define TP(slot)                          \
+  do {                                    \
+    const long long tp_now = clock64();   \
+    tp_acc[slot] += tp_now - tp_last;     \
+    tp_last = tp_now;                     \
+  } while (0)
+#define TP_STORE                                                        \
+  do {                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < kTileProfTiles)                \
+      for (int i_ = 0; i_ < kTileProfSlots; ++i_) g_tile_prof[blockIdx.x][i_] += tp_acc[i_]; \
+  } while (0)
+#else
+#define TP_DECL
+#define TP(slot) \
+  do {           \
+  } while (0)
+#define TP_STORE \
+  do {           \
+  } while (0)
+#endif
+constexpr int kTileBL = 4, kTileIPT = 512 / kTileThreads;  // fast path: k <= 512 / (6 * 4) = 21
+
+// MFMA phase of one batch for the accumulator tiles q = P (mod kTileWaves):
+// acc[q/W] += sum_ks Y[4ks..4ks+3][ti-tile]^T Y[4ks..4ks+3][tj-tile].
 // Both operands of every MFMA are entries Y[4ks + (lane>>4)][16t + (lane&15)],
 // so the lane's NT x 4 values are read from LDS once and the MFMAs then issue
 // back to back from registers.
+// The pair loop runs over the union span [tmin, tmax] of the batch with all K
+// steps branch-free (per-landmark spans would save MFMAs but split the chain
+// into basic blocks the compiler cannot interleave: measured slower).
 template <int NT, int P, int NC>
 __device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int tmin, int tmax, int nl, int r16,
                                           int k4) {
@@ -552,25 +586,29 @@ __device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int t
   for (int ti = 0; ti < NT; ++ti) {
 #pragma unroll
     for (int tj = ti; tj < NT; ++tj, ++q) {
-      if ((q & 1) == P) {
-        if (ti >= tmin && tj <= tmax) {
+      if (q % kTileWaves == P && ti >= tmin && tj <= tmax) {
 #pragma unroll
-          for (int ks = 0; ks < kTileBL; ++ks)
-            if (ks < nl) acc[q >> 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti][ks], op[tj][ks], acc[q >> 1], 0, 0, 0);
-        }
+        for (int ks = 0; ks < kTileBL; ++ks)
+          if (ks < nl)
+            acc[q / kTileWaves] =
+                __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti][ks], op[tj][ks], acc[q / kTileWaves], 0, 0, 0);
       }
     }
   }
 }
 
 template <int NT>
-__global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
-  // two waves per tile: wave w owns the accumulator tiles q with q % 2 == w
-  constexpr int NQ = NT * (NT + 1) / 2, NQW = (NQ + 1) / 2, NC = NT * 16, NG = (NC + 127) / 128;
+__global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
+  // wave w owns the accumulator tiles q with q % kTileWaves == w
+  constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
+  constexpr int NC = NT * 16, NG = (NC + TH - 1) / TH;
   constexpr int BL = kTileBL, IPT = kTileIPT;
   __shared__ double Ys[2][4 * BL][NC];
-  __shared__ double Ws[2][BL][4];
-  __shared__ int2 Us[2][BL];
+  // per-landmark data of the whole tile, loaded once: offsets, camera span, w, R'^-1
+  __shared__ int Lb[kTileMaxLm + 1];
+  __shared__ int2 Lu[kTileMaxLm];
+  __shared__ double Lw[kTileMaxLm][3];
+  __shared__ double Lr[kTileMaxLm][6];
   const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
   const int ncol = 6 * cp, nt = (ncol + 15) >> 4, ld = nt * 16;
@@ -581,59 +619,71 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
   double gacc[NG];
 #pragma unroll
   for (int m = 0; m < NG; ++m) gacc[m] = 0.0;
-  for (int k = tid; k < 2 * 4 * BL * NC; k += 128) (&Ys[0][0][0])[k] = 0.0;
-  const int l0 = d.tile_lm_ptr[t], l1 = d.tile_lm_ptr[t + 1];
-  const int nbatch = (l1 - l0 + BL - 1) / BL;
+  for (int k = tid; k < 2 * 4 * BL * NC; k += TH) (&Ys[0][0][0])[k] = 0.0;
+  const int l0 = d.tile_lm_ptr[t], l1 = d.tile_lm_ptr[t + 1], ntl = l1 - l0;
+  const int nbatch = (ntl + BL - 1) / BL;
   const bool slow = d.tile_dups || d.tile_maxk > 21;
+  for (int k = tid; k <= ntl; k += TH) Lb[k] = d.lm_begin[l0 + k];
+  for (int k = tid; k < ntl; k += TH) Lu[k] = d.lm_urange[l0 + k];
+  for (int k = tid; k < 9 * ntl; k += TH) {
+    const int li = k / 9, c = k - 9 * li;
+    const double v = d.lm_Rp[12 * (l0 + li) + c];
+    if (c < 6) Lr[li][c] = v; else Lw[li][c - 6] = v;
+  }
+  __syncthreads();
   // prefetched raw inputs of one batch (fast path)
-  double pp[IPT][3], pr[IPT][6];
+  double pp[IPT][3];
   int pu[IPT], pli[IPT], pc[IPT];
   auto fetch = [&](int bt) {
-    const int lb = l0 + BL * bt, nl = min(BL, l1 - lb);
-    const int b0 = d.lm_begin[lb], bn = d.lm_begin[lb + nl];
-    const int e1 = nl > 1 ? d.lm_begin[lb + 1] : bn, e2 = nl > 2 ? d.lm_begin[lb + 2] : bn,
-              e3 = nl > 3 ? d.lm_begin[lb + 3] : bn;
+    const int lb = BL * bt, nl = min(BL, ntl - lb);
+    const int b0 = Lb[lb], bn = Lb[lb + nl];
+    const int e1 = nl > 1 ? Lb[lb + 1] : bn, e2 = nl > 2 ? Lb[lb + 2] : bn, e3 = nl > 3 ? Lb[lb + 3] : bn;
 #pragma unroll
     for (int m = 0; m < IPT; ++m) {
-      const int it = tid + 128 * m, o = b0 + it / 6;
+      const int it = tid + TH * m, o = b0 + it / 6;
       pu[m] = -1;
       if (!slow && o < bn) {
-        pli[m] = (o >= e1) + (o >= e2) + (o >= e3);
+        pli[m] = lb + (o >= e1) + (o >= e2) + (o >= e3);  // tile-local landmark
         pc[m] = it % 6;
         pu[m] = d.obs_local[o];
         const double *P = d.obs_P + o;
         pp[m][0] = P[pc[m] * d.nE]; pp[m][1] = P[(6 + pc[m]) * d.nE]; pp[m][2] = P[(12 + pc[m]) * d.nE];
-        const double *Ri = d.lm_Rp + 12 * (lb + pli[m]);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) pr[m][i] = Ri[i];
       }
     }
   };
   if (nbatch > 0) fetch(0);
   int2 prev = int2{-1, -1};
+  int wrote[IPT];  // fast path: offset in Ys[buf] of this thread's staged entries (row 4li), -1 none
+#pragma unroll
+  for (int m = 0; m < IPT; ++m) wrote[m] = -1;
   lds_barrier();
+  int wrote_prev[IPT];
+  TP_DECL
   for (int bt = 0; bt < nbatch; ++bt) {
-    const int buf = bt & 1, lb = l0 + BL * bt, nl = min(BL, l1 - lb);
+    const int buf = bt & 1, lb = BL * bt, nl = min(BL, ntl - lb);
+#pragma unroll
+    for (int m = 0; m < IPT; ++m) wrote_prev[m] = wrote[m];
     double (*Y)[NC] = Ys[buf];
-    if (tid < nl) Us[buf][tid] = d.lm_urange[lb + tid];
-    if (tid < 3 * nl) Ws[buf][tid / 3][tid % 3] = d.lm_Rp[12 * (lb + tid / 3) + 6 + tid % 3];
     // ---- stage Y rows 4li..4li+2 = R'^-T P for every landmark li of the batch
     if (!slow) {
 #pragma unroll
       for (int m = 0; m < IPT; ++m) {
         if (pu[m] >= 0) {  // y = (R'^-1)^T p
-          const double y0 = pr[m][0] * pp[m][0];
-          const double y1 = pr[m][1] * pp[m][0] + pr[m][3] * pp[m][1];
-          const double y2 = pr[m][2] * pp[m][0] + pr[m][4] * pp[m][1] + pr[m][5] * pp[m][2];
-          const int col = 6 * pu[m] + pc[m], row = 4 * pli[m];
+          const double *r = Lr[pli[m]];
+          const double y0 = r[0] * pp[m][0];
+          const double y1 = r[1] * pp[m][0] + r[3] * pp[m][1];
+          const double y2 = r[2] * pp[m][0] + r[4] * pp[m][1] + r[5] * pp[m][2];
+          const int col = 6 * pu[m] + pc[m], row = 4 * (pli[m] - lb);
           Y[row][col] = y0; Y[row + 1][col] = y1; Y[row + 2][col] = y2;
+          wrote[m] = row * NC + col;
+        } else {
+          wrote[m] = -1;
         }
       }
     } else if (tid < 6) {  // repeated cameras / long tracks: serial, observation order
       for (int li = 0; li < nl; ++li) {
-        const int l = lb + li;
-        const double *Rp = d.lm_Rp + 12 * l;
-        for (int o = d.lm_begin[l]; o < d.lm_begin[l + 1]; ++o) {
+        const double *Rp = Lr[lb + li];
+        for (int o = Lb[lb + li]; o < Lb[lb + li + 1]; ++o) {
           const int u = d.obs_local[o];
           if (u < 0) continue;
           const double *P = d.obs_P + o;
@@ -645,30 +695,46 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
         }
       }
     }
+    TP(0);
     lds_barrier();  // (A) batch staged; every thread is done with the previous batch
+    TP(1);
     if (bt + 1 < nbatch) fetch(bt + 1);  // in flight during the MFMAs below
-    if (prev.x >= 0) {  // clear the previous batch's columns in the other buffer
+    TP(2);
+    if (!slow) {  // zero exactly the entries this thread staged into the other buffer last batch
+      double *Yo = &Ys[buf ^ 1][0][0];
+#pragma unroll
+      for (int m = 0; m < IPT; ++m)
+        if (bt > 0 && wrote_prev[m] >= 0) {
+          Yo[wrote_prev[m]] = 0.0; Yo[wrote_prev[m] + NC] = 0.0; Yo[wrote_prev[m] + 2 * NC] = 0.0;
+        }
+    } else if (prev.x >= 0) {  // clear the previous batch's columns in the other buffer
 #pragma unroll
       for (int row = 0; row < 4 * BL; ++row)
-        for (int col = prev.x + tid; col < prev.y; col += 128) Ys[buf ^ 1][row][col] = 0.0;
+        for (int col = prev.x + tid; col < prev.y; col += TH) Ys[buf ^ 1][row][col] = 0.0;
     }
+    TP(3);
     int cmin = 1 << 30, cmax = -1;
     for (int li = 0; li < nl; ++li) {
-      const int2 ur = Us[buf][li];
+      const int2 ur = Lu[lb + li];
       if (ur.x >= 0) { cmin = min(cmin, 6 * ur.x); cmax = max(cmax, 6 * ur.y + 6); }
     }
     if (cmax > 0) {
       const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
-      if (wave == 0) tile_mfma<NT, 0>(acc, Y, tmin, tmax, nl, r16, k4);
-      else tile_mfma<NT, 1>(acc, Y, tmin, tmax, nl, r16, k4);
+      switch (wave) {
+        case 0: tile_mfma<NT, 0>(acc, Y, tmin, tmax, nl, r16, k4); break;
+        case 1: tile_mfma<NT, 1>(acc, Y, tmin, tmax, nl, r16, k4); break;
+        case 2: tile_mfma<NT, 2>(acc, Y, tmin, tmax, nl, r16, k4); break;
+        default: tile_mfma<NT, 3>(acc, Y, tmin, tmax, nl, r16, k4); break;
+      }
+      TP(4);
 #pragma unroll
       for (int m = 0; m < NG; ++m) {
-        const int col = tid + 128 * m;
+        const int col = tid + TH * m;
         if (col >= cmin && col < cmax) {
           double gs = 0.0;
           for (int li = 0; li < nl; ++li)
-            gs += Y[4 * li][col] * Ws[buf][li][0] + Y[4 * li + 1][col] * Ws[buf][li][1] +
-                  Y[4 * li + 2][col] * Ws[buf][li][2];
+            gs += Y[4 * li][col] * Lw[lb + li][0] + Y[4 * li + 1][col] * Lw[lb + li][1] +
+                  Y[4 * li + 2][col] * Lw[lb + li][2];
           gacc[m] -= gs;
         }
       }
@@ -676,8 +742,11 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
     } else {
       prev = int2{-1, -1};
     }
+    TP(5);
     lds_barrier();  // (B) the other buffer is clear before it is staged
+    TP(6);
   }
+  TP_STORE;
   // write -G_t (upper tiles) as the tile's partial, ld = 16 nt
   double *out = d.part + d.tile_part_ptr[t];
   int q = 0;
@@ -685,15 +754,16 @@ __global__ __launch_bounds__(128) void k_rcs_tile(DevProblem d) {
   for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
     for (int tj = ti; tj < NT; ++tj, ++q) {
-      if ((q & 1) == wave && tj < nt) {
+      if (q % kTileWaves == wave && tj < nt) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) out[(size_t)(ti * 16 + k4 + 4 * j) * ld + tj * 16 + r16] = -acc[q >> 1][j];
+        for (int j = 0; j < 4; ++j)
+          out[(size_t)(ti * 16 + k4 + 4 * j) * ld + tj * 16 + r16] = -acc[q / kTileWaves][j];
       }
     }
   double *go = d.gpart + d.tile_gpart_ptr[t];
 #pragma unroll
   for (int m = 0; m < NG; ++m) {
-    const int col = tid + 128 * m;
+    const int col = tid + TH * m;
     if (col < ncol) go[col] = gacc[m];
   }
 }
@@ -739,12 +809,18 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
   (void)max_k;
   const int nt = (6 * max_cp + 15) / 16;
   if (d.n_tiles > 0) {
-    if (nt <= 3) hipLaunchKernelGGL(k_rcs_tile<3>, dim3(d.n_tiles), dim3(128), 0, st, d);
-    else if (nt <= 5) hipLaunchKernelGGL(k_rcs_tile<5>, dim3(d.n_tiles), dim3(128), 0, st, d);
-    else if (nt <= 7) hipLaunchKernelGGL(k_rcs_tile<7>, dim3(d.n_tiles), dim3(128), 0, st, d);
-    else hipLaunchKernelGGL(k_rcs_tile<9>, dim3(d.n_tiles), dim3(128), 0, st, d);
+    if (nt <= 3) hipLaunchKernelGGL(k_rcs_tile<3>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
+    else if (nt <= 5) hipLaunchKernelGGL(k_rcs_tile<5>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
+    else if (nt <= 7) hipLaunchKernelGGL(k_rcs_tile<7>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
+    else hipLaunchKernelGGL(k_rcs_tile<9>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
   }
 }
+
+#ifdef SQLM_TILE_PROF
+int tile_profile_read(long long *out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_prof), sizeof(g_tile_prof)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st) {
   if (d.nP == 0) return;

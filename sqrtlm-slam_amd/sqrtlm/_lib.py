@@ -12,7 +12,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsqrtlm.so")
+# SQLM_LIB_PATH selects a diagnostic build of the same library (libsqrtlm_prof.so)
+LIB_PATH = os.environ.get("SQLM_LIB_PATH", os.path.join(_HERE, "libsqrtlm.so"))
 TRACE_MAX = 256
 NKERNEL_TIMERS = 9
 
