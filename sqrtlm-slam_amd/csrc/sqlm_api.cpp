@@ -253,12 +253,24 @@ int prepare(sqlm_ctx *c, int level) {
     if (pose_act[p] && !c->pose_fixed[p]) { phidx[p] = (int)hidxp.size(); hidxp.push_back(p); }
   const int nP = (int)hidxp.size();
   if (nP > kMaxFreePoses) return SQLM_ERR_UNSUPPORTED;
-  // landmark slots: bucket by segment width, point-id order inside a bucket
-  std::vector<int> pts;
+  // landmark slots: bucket by segment width; inside a bucket by camera span
+  // (first, last observing pose, then id), so a batch of consecutive slots in
+  // the RCS tiles shares nearly one span (dense MFMA panels)
+  std::vector<int> pts, span_lo(c->n_pt, std::numeric_limits<int>::max()), span_hi(c->n_pt, -1);
+  for (int64_t e = 0; e < c->n_obs; ++e) {
+    if (c->obs_level[e] != level) continue;
+    const int l = c->obs_pt[e], pp = c->obs_pose[e];
+    span_lo[l] = std::min(span_lo[l], pp);
+    span_hi[l] = std::max(span_hi[l], pp);
+  }
   for (int l = 0; l < c->n_pt; ++l)
     if (pt_act[l]) pts.push_back(l);
-  std::stable_sort(pts.begin(), pts.end(),
-                   [&](int a, int b) { return seg_width(kcount[a]) < seg_width(kcount[b]); });
+  std::stable_sort(pts.begin(), pts.end(), [&](int a, int b) {
+    const int wa = seg_width(kcount[a]), wb = seg_width(kcount[b]);
+    if (wa != wb) return wa < wb;
+    if (span_lo[a] != span_lo[b]) return span_lo[a] < span_lo[b];
+    return span_hi[a] < span_hi[b];
+  });
   const int nL = (int)pts.size();
   if (nP + nL == 0) return SQLM_ERR_STATE;  // "0 vertices to optimize"
   std::vector<int> pt_slot(c->n_pt, -1);

@@ -529,8 +529,8 @@ void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStrea
 typedef double d4v __attribute__((ext_vector_type(4)));
 
 // Landmarks are consumed in batches of 4: landmark li of a batch occupies rows
-// 4li..4li+2 of the staged block (row 4li+3 stays zero), i.e. exactly one
-// K=4 step of v_mfma_f64_16x16x4_f64, so one batch = 4 K-steps per 16x16 tile.
+// 3li..3li+2 of the staged block, so one batch = 3 K-steps of
+// v_mfma_f64_16x16x4_f64 per 16x16 tile (no padding rows).
 // The raw P columns of the next batch are prefetched into registers while the
 // current batch runs on the matrix cores.
 constexpr int kTileWaves = 4, kTileThreads = 64 * kTileWaves;
@@ -563,7 +563,10 @@ __device__ long long g_tile_prof[kTileProfTiles][kTileProfSlots];
   do {           \
   } while (0)
 #endif
-constexpr int kTileBL = 4, kTileIPT = 512 / kTileThreads;  // fast path: k <= 512 / (6 * 4) = 21
+// A batch of kTileBL landmarks fills 3 kTileBL rows of the staged block
+// (landmark li in rows 3li..3li+2), i.e. kTileKS K-steps of 4 rows.
+constexpr int kTileBL = 4, kTileKS = (3 * kTileBL + 3) / 4, kTileRows = 4 * kTileKS;
+constexpr int kTileIPT = 512 / kTileThreads;  // fast path: k <= 512 / (6 * 4) = 21
 
 // MFMA phase of one batch for the accumulator tiles q = P (mod kTileWaves):
 // acc[q/W] += sum_ks Y[4ks..4ks+3][ti-tile]^T Y[4ks..4ks+3][tj-tile].
@@ -574,13 +577,13 @@ constexpr int kTileBL = 4, kTileIPT = 512 / kTileThreads;  // fast path: k <= 51
 // steps branch-free (per-landmark spans would save MFMAs but split the chain
 // into basic blocks the compiler cannot interleave: measured slower).
 template <int NT, int P, int NC>
-__device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int tmin, int tmax, int nl, int r16,
+__device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int tmin, int tmax, int nks, int r16,
                                           int k4) {
-  double op[NT][kTileBL];
+  double op[NT][kTileKS];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int ks = 0; ks < kTileBL; ++ks) op[t][ks] = Y[4 * ks + k4][t * 16 + r16];
+    for (int ks = 0; ks < kTileKS; ++ks) op[t][ks] = Y[4 * ks + k4][t * 16 + r16];
   int q = 0;
 #pragma unroll
   for (int ti = 0; ti < NT; ++ti) {
@@ -588,8 +591,8 @@ __device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int t
     for (int tj = ti; tj < NT; ++tj, ++q) {
       if (q % kTileWaves == P && ti >= tmin && tj <= tmax) {
 #pragma unroll
-        for (int ks = 0; ks < kTileBL; ++ks)
-          if (ks < nl)
+        for (int ks = 0; ks < kTileKS; ++ks)
+          if (ks < nks)
             acc[q / kTileWaves] =
                 __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti][ks], op[tj][ks], acc[q / kTileWaves], 0, 0, 0);
       }
@@ -603,7 +606,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
   constexpr int NC = NT * 16, NG = (NC + TH - 1) / TH;
   constexpr int BL = kTileBL, IPT = kTileIPT;
-  __shared__ double Ys[2][4 * BL][NC];
+  __shared__ double Ys[2][kTileRows][NC];
   // per-landmark data of the whole tile, loaded once: offsets, camera span, w, R'^-1
   __shared__ int Lb[kTileMaxLm + 1];
   __shared__ int2 Lu[kTileMaxLm];
@@ -619,7 +622,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
   double gacc[NG];
 #pragma unroll
   for (int m = 0; m < NG; ++m) gacc[m] = 0.0;
-  for (int k = tid; k < 2 * 4 * BL * NC; k += TH) (&Ys[0][0][0])[k] = 0.0;
+  for (int k = tid; k < 2 * kTileRows * NC; k += TH) (&Ys[0][0][0])[k] = 0.0;
   const int l0 = d.tile_lm_ptr[t], l1 = d.tile_lm_ptr[t + 1], ntl = l1 - l0;
   const int nbatch = (ntl + BL - 1) / BL;
   const bool slow = d.tile_dups || d.tile_maxk > 21;
@@ -673,7 +676,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
           const double y0 = r[0] * pp[m][0];
           const double y1 = r[1] * pp[m][0] + r[3] * pp[m][1];
           const double y2 = r[2] * pp[m][0] + r[4] * pp[m][1] + r[5] * pp[m][2];
-          const int col = 6 * pu[m] + pc[m], row = 4 * (pli[m] - lb);
+          const int col = 6 * pu[m] + pc[m], row = 3 * (pli[m] - lb);
           Y[row][col] = y0; Y[row + 1][col] = y1; Y[row + 2][col] = y2;
           wrote[m] = row * NC + col;
         } else {
@@ -691,7 +694,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
           const double y0 = Rp[0] * p0;
           const double y1 = Rp[1] * p0 + Rp[3] * p1;
           const double y2 = Rp[2] * p0 + Rp[4] * p1 + Rp[5] * p2;
-          Y[4 * li][6 * u + tid] += y0; Y[4 * li + 1][6 * u + tid] += y1; Y[4 * li + 2][6 * u + tid] += y2;
+          Y[3 * li][6 * u + tid] += y0; Y[3 * li + 1][6 * u + tid] += y1; Y[3 * li + 2][6 * u + tid] += y2;
         }
       }
     }
@@ -709,7 +712,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
         }
     } else if (prev.x >= 0) {  // clear the previous batch's columns in the other buffer
 #pragma unroll
-      for (int row = 0; row < 4 * BL; ++row)
+      for (int row = 0; row < kTileRows; ++row)
         for (int col = prev.x + tid; col < prev.y; col += TH) Ys[buf ^ 1][row][col] = 0.0;
     }
     TP(3);
@@ -721,10 +724,10 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
     if (cmax > 0) {
       const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
       switch (wave) {
-        case 0: tile_mfma<NT, 0>(acc, Y, tmin, tmax, nl, r16, k4); break;
-        case 1: tile_mfma<NT, 1>(acc, Y, tmin, tmax, nl, r16, k4); break;
-        case 2: tile_mfma<NT, 2>(acc, Y, tmin, tmax, nl, r16, k4); break;
-        default: tile_mfma<NT, 3>(acc, Y, tmin, tmax, nl, r16, k4); break;
+        case 0: tile_mfma<NT, 0>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
+        case 1: tile_mfma<NT, 1>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
+        case 2: tile_mfma<NT, 2>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
+        default: tile_mfma<NT, 3>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
       }
       TP(4);
 #pragma unroll
@@ -733,8 +736,8 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
         if (col >= cmin && col < cmax) {
           double gs = 0.0;
           for (int li = 0; li < nl; ++li)
-            gs += Y[4 * li][col] * Lw[lb + li][0] + Y[4 * li + 1][col] * Lw[lb + li][1] +
-                  Y[4 * li + 2][col] * Lw[lb + li][2];
+            gs += Y[3 * li][col] * Lw[lb + li][0] + Y[3 * li + 1][col] * Lw[lb + li][1] +
+                  Y[3 * li + 2][col] * Lw[lb + li][2];
           gacc[m] -= gs;
         }
       }
