@@ -56,12 +56,12 @@ def make_workload(name: str, scale: float):
 def algorithmic_bytes_linearize(p) -> float:
     """Bytes k_linearize must move per launch: per observation
     it reads cam id, free-camera id, uv, info, delta (40 B) and writes the
-    error (16 B); per observation of a FREE camera it writes the 3x6 H_lp block
-    (144 B); per landmark it reads X (24 B) + offset (4 B) and writes the QR
-    factor R (48 B) + b_l (24 B). Pose reads (<1 MB, L2-resident) excluded."""
-    free = p.pose_fixed[p.obs_pose] == 0
-    E, Ef, L = p.n_obs, int(free.sum()), p.n_pt
-    return E * (40 + 16) + Ef * 144 + L * (24 + 4 + 48 + 24)
+    error (16 B) and the weight sqrt(rho' info) (8 B) from which the consumers
+    recompute the H_lp blocks; per landmark it reads X (24 B) + offset (4 B)
+    and writes the QR factor R (48 B) + b_l (24 B). Pose reads (<1 MB,
+    L2-resident) excluded."""
+    E, L = p.n_obs, p.n_pt
+    return E * (40 + 16 + 8) + L * (24 + 4 + 48 + 24)
 
 
 def algorithmic_flops_rcs(p) -> float:

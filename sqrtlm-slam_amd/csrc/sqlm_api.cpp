@@ -115,7 +115,7 @@ int upload(sqlm_ctx *c, int idx, const std::vector<T> &v, T **out) {
 
 enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
-  B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS,
+  B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS,
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE
@@ -467,7 +467,12 @@ int prepare(sqlm_ctx *c, int level) {
   UP(B_OBSUV, obs_uv, d.obs_uv);
   UP(B_OBSINFO, obs_info, d.obs_info);
   UP(B_OBSDELTA, obs_delta, d.obs_delta);
-  AL(B_OBSP, 18 * (size_t)nE, d.obs_P);
+  AL(B_OBSS, (size_t)nE, d.obs_s);
+  if (c->use_tiles) {
+    d.obs_P = nullptr;  // consumers recompute the H_lp blocks from obs_s
+  } else {
+    AL(B_OBSP, 18 * (size_t)nE, d.obs_P);
+  }
   AL(B_OBSERR, 2 * (size_t)nE, d.obs_err);
   UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
   UP(B_CAMOBS, cam_obs, d.cam_obs);

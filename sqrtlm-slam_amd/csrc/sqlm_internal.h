@@ -39,7 +39,8 @@ struct DevProblem {
   double *obs_uv = nullptr;                 // [nE][2]
   double *obs_info = nullptr;               // [nE]
   double *obs_delta = nullptr;              // [nE] Huber delta, 0 = none
-  double *obs_P = nullptr;                  // [18][nE] H_lp block J_l^T W J_p (3x6), SoA
+  double *obs_s = nullptr;                  // [nE] sqrt(rho' info) at the linearization point
+  double *obs_P = nullptr;                  // [18][nE] H_lp blocks, SoA: row-kernel fallback only (else null)
   double *obs_err = nullptr;                // [nE][2] last computed error (g2o _error)
   // cameras
   int *cam_obs_ptr = nullptr;               // [nP+1]
@@ -77,7 +78,7 @@ struct DevProblem {
   int *gred_ptr = nullptr;                  // [nP+1] camera -> contributions
   int2 *gred_idx = nullptr;                 //   (tile, u)
   int tile_dups = 0;                        // some landmark observed twice by one camera
-  int tile_maxk = 0;                        // longest track (staging fast path needs <= 21)
+  int tile_maxk = 0;                        // longest track (staging fast path needs <= kTileFastK = 64)
   // block-tridiagonal cyclic reduction workspace (sqlm_rcs_solve.hip)
   double *cr_D = nullptr, *cr_E = nullptr;  // [p][n][n]
   double *cr_A = nullptr, *cr_C = nullptr;  // [p][n][n]

@@ -143,6 +143,28 @@ __device__ __forceinline__ void mono_jac(const double *__restrict__ prt, const M
   jp[11] = s * (y / z_2 * fy);
 }
 
+// Column c of an observation's H_lp block P = jl^T jp (3 values), recomputed
+// from the linearization point (pose prt, landmark X, stored weight s) by the
+// same device code k_linearize used, so the consumers need not store P.
+__device__ __forceinline__ void hlp_col(const double *prt, double X0, double X1, double X2, double s, int c,
+                                        double out[3]) {
+  MonoEval m;
+  m.x = prt[0] * X0 + prt[1] * X1 + prt[2] * X2 + prt[9];
+  m.y = prt[3] * X0 + prt[4] * X1 + prt[5] * X2 + prt[10];
+  m.z = prt[6] * X0 + prt[7] * X1 + prt[8] * X2 + prt[11];
+  m.s = s;
+  double jl[6], jp[12];
+  mono_jac(prt, m, jl, jp);
+  double p0 = jp[0], p1 = jp[6];
+#pragma unroll
+  for (int k = 1; k < 6; ++k) {
+    p0 = c == k ? jp[k] : p0;
+    p1 = c == k ? jp[6 + k] : p1;
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) out[a] = jl[a] * p0 + jl[3 + a] * p1;
+}
+
 // Workgroup barrier that orders LDS only: global loads issued before it stay in
 // flight (a __syncthreads() fence would wait vmcnt(0) and drain the prefetch).
 __device__ __forceinline__ void lds_barrier() {
@@ -217,6 +239,7 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
         MonoEval m;
         mono_error(prt, X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
         store2(d.obs_err + 2 * e, m.e0, m.e1);
+        d.obs_s[e] = m.s;
         chi += m.chi_rob;
         double jl[6], jp[12];
         mono_jac(prt, m, jl, jp);
@@ -229,8 +252,8 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
         g2 += jl[2] * jl[2] + jl[5] * jl[5];
         givens_add_row(R, jl[0], jl[1], jl[2]);
         givens_add_row(R, jl[3], jl[4], jl[5]);
-        if (d.obs_camh[e] >= 0) {
-          // H_lp block jl^T jp (3x6), structure of arrays: entry (a,c) at P[(6a+c) nE + e]
+        if (d.obs_P && d.obs_camh[e] >= 0) {
+          // row-kernel fallback only: H_lp block jl^T jp (3x6), SoA, entry (a,c) at P[(6a+c) nE + e]
           double *P = d.obs_P + e;
 #pragma unroll
           for (int a = 0; a < 3; ++a)
@@ -566,7 +589,9 @@ __device__ long long g_tile_prof[kTileProfTiles][kTileProfSlots];
 // A batch of kTileBL landmarks fills 3 kTileBL rows of the staged block
 // (landmark li in rows 3li..3li+2), i.e. kTileKS K-steps of 4 rows.
 constexpr int kTileBL = 4, kTileKS = (3 * kTileBL + 3) / 4, kTileRows = 4 * kTileKS;
-constexpr int kTileIPT = 512 / kTileThreads;  // fast path: k <= 512 / (6 * 4) = 21
+// fast path: one thread per observation of a batch, so tracks up to
+// kTileThreads / kTileBL = 64 observations and no camera seen twice by a landmark
+constexpr int kTileFastK = kTileThreads / kTileBL;
 
 // MFMA phase of one batch for the accumulator tiles q = P (mod kTileWaves):
 // acc[q/W] += sum_ks Y[4ks..4ks+3][ti-tile]^T Y[4ks..4ks+3][tj-tile].
@@ -605,13 +630,15 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
   // wave w owns the accumulator tiles q with q % kTileWaves == w
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
   constexpr int NC = NT * 16, NG = (NC + TH - 1) / TH;
-  constexpr int BL = kTileBL, IPT = kTileIPT;
+  constexpr int BL = kTileBL;
   __shared__ double Ys[2][kTileRows][NC];
   // per-landmark data of the whole tile, loaded once: offsets, camera span, w, R'^-1
   __shared__ int Lb[kTileMaxLm + 1];
   __shared__ int2 Lu[kTileMaxLm];
   __shared__ double Lw[kTileMaxLm][3];
   __shared__ double Lr[kTileMaxLm][6];
+  __shared__ double Lx[kTileMaxLm][3];            // landmarks at the linearization point
+  __shared__ double Lc[kTileMaxCams][16];         // window cameras: R t fx fy cx cy
   const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
   const int ncol = 6 * cp, nt = (ncol + 15) >> 4, ld = nt * 16;
@@ -625,7 +652,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
   for (int k = tid; k < 2 * kTileRows * NC; k += TH) (&Ys[0][0][0])[k] = 0.0;
   const int l0 = d.tile_lm_ptr[t], l1 = d.tile_lm_ptr[t + 1], ntl = l1 - l0;
   const int nbatch = (ntl + BL - 1) / BL;
-  const bool slow = d.tile_dups || d.tile_maxk > 21;
+  const bool slow = d.tile_dups || d.tile_maxk > kTileFastK;
   for (int k = tid; k <= ntl; k += TH) Lb[k] = d.lm_begin[l0 + k];
   for (int k = tid; k < ntl; k += TH) Lu[k] = d.lm_urange[l0 + k];
   for (int k = tid; k < 9 * ntl; k += TH) {
@@ -633,55 +660,67 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
     const double v = d.lm_Rp[12 * (l0 + li) + c];
     if (c < 6) Lr[li][c] = v; else Lw[li][c - 6] = v;
   }
+  for (int k = tid; k < 3 * ntl; k += TH) {
+    const int li = k / 3, c = k - 3 * li;
+    Lx[li][c] = d.X[0][4 * (l0 + li) + c];
+  }
+  {
+    const int cb = d.tile_cam_ptr[t];
+    for (int k = tid; k < 16 * cp; k += TH) {
+      const int u = k >> 4, c = k & 15;
+      Lc[u][c] = d.pose_rt[0][16 * d.hidx_pose[d.tile_cams[cb + u]] + c];
+    }
+  }
   __syncthreads();
-  // prefetched raw inputs of one batch (fast path)
-  double pp[IPT][3];
-  int pu[IPT], pli[IPT], pc[IPT];
+  // prefetched raw inputs of one batch (fast path): thread tid owns observation b0 + tid
+  double ps = 0.0;
+  int pu = -1, pli = 0;
   auto fetch = [&](int bt) {
     const int lb = BL * bt, nl = min(BL, ntl - lb);
     const int b0 = Lb[lb], bn = Lb[lb + nl];
     const int e1 = nl > 1 ? Lb[lb + 1] : bn, e2 = nl > 2 ? Lb[lb + 2] : bn, e3 = nl > 3 ? Lb[lb + 3] : bn;
-#pragma unroll
-    for (int m = 0; m < IPT; ++m) {
-      const int it = tid + TH * m, o = b0 + it / 6;
-      pu[m] = -1;
-      if (!slow && o < bn) {
-        pli[m] = lb + (o >= e1) + (o >= e2) + (o >= e3);  // tile-local landmark
-        pc[m] = it % 6;
-        pu[m] = d.obs_local[o];
-        const double *P = d.obs_P + o;
-        pp[m][0] = P[pc[m] * d.nE]; pp[m][1] = P[(6 + pc[m]) * d.nE]; pp[m][2] = P[(12 + pc[m]) * d.nE];
-      }
+    const int o = b0 + tid;
+    pu = -1;
+    if (!slow && o < bn) {
+      pli = lb + (o >= e1) + (o >= e2) + (o >= e3);  // tile-local landmark
+      pu = d.obs_local[o];
+      ps = d.obs_s[o];
     }
   };
   if (nbatch > 0) fetch(0);
   int2 prev = int2{-1, -1};
-  int wrote[IPT];  // fast path: offset in Ys[buf] of this thread's staged entries (row 4li), -1 none
-#pragma unroll
-  for (int m = 0; m < IPT; ++m) wrote[m] = -1;
+  int wrote = -1;  // fast path: offset in Ys[buf] of this thread's staged 3 x 6 block, -1 none
   lds_barrier();
-  int wrote_prev[IPT];
+  int wrote_prev;
   TP_DECL
   for (int bt = 0; bt < nbatch; ++bt) {
     const int buf = bt & 1, lb = BL * bt, nl = min(BL, ntl - lb);
-#pragma unroll
-    for (int m = 0; m < IPT; ++m) wrote_prev[m] = wrote[m];
+    wrote_prev = wrote;
     double (*Y)[NC] = Ys[buf];
     // ---- stage Y rows 4li..4li+2 = R'^-T P for every landmark li of the batch
     if (!slow) {
+      if (pu >= 0) {  // Y block of the observation: (R'^-1)^T jl^T jp, Jacobians recomputed once
+        const double *pr = Lc[pu], *xl = Lx[pli], *r = Lr[pli];
+        MonoEval m;
+        m.x = pr[0] * xl[0] + pr[1] * xl[1] + pr[2] * xl[2] + pr[9];
+        m.y = pr[3] * xl[0] + pr[4] * xl[1] + pr[5] * xl[2] + pr[10];
+        m.z = pr[6] * xl[0] + pr[7] * xl[1] + pr[8] * xl[2] + pr[11];
+        m.s = ps;
+        double jl[6], jp[12];
+        mono_jac(pr, m, jl, jp);
+        const int row = 3 * (pli - lb), col = 6 * pu;
 #pragma unroll
-      for (int m = 0; m < IPT; ++m) {
-        if (pu[m] >= 0) {  // y = (R'^-1)^T p
-          const double *r = Lr[pli[m]];
-          const double y0 = r[0] * pp[m][0];
-          const double y1 = r[1] * pp[m][0] + r[3] * pp[m][1];
-          const double y2 = r[2] * pp[m][0] + r[4] * pp[m][1] + r[5] * pp[m][2];
-          const int col = 6 * pu[m] + pc[m], row = 3 * (pli[m] - lb);
-          Y[row][col] = y0; Y[row + 1][col] = y1; Y[row + 2][col] = y2;
-          wrote[m] = row * NC + col;
-        } else {
-          wrote[m] = -1;
+        for (int c = 0; c < 6; ++c) {
+          const double p0 = jl[0] * jp[c] + jl[3] * jp[6 + c];
+          const double p1 = jl[1] * jp[c] + jl[4] * jp[6 + c];
+          const double p2 = jl[2] * jp[c] + jl[5] * jp[6 + c];
+          Y[row][col + c] = r[0] * p0;
+          Y[row + 1][col + c] = r[1] * p0 + r[3] * p1;
+          Y[row + 2][col + c] = r[2] * p0 + r[4] * p1 + r[5] * p2;
         }
+        wrote = row * NC + col;
+      } else {
+        wrote = -1;
       }
     } else if (tid < 6) {  // repeated cameras / long tracks: serial, observation order
       for (int li = 0; li < nl; ++li) {
@@ -689,8 +728,10 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
         for (int o = Lb[lb + li]; o < Lb[lb + li + 1]; ++o) {
           const int u = d.obs_local[o];
           if (u < 0) continue;
-          const double *P = d.obs_P + o;
-          const double p0 = P[tid * d.nE], p1 = P[(6 + tid) * d.nE], p2 = P[(12 + tid) * d.nE];
+          double pcol[3];
+          const double *xl = Lx[lb + li];
+          hlp_col(Lc[u], xl[0], xl[1], xl[2], d.obs_s[o], tid, pcol);
+          const double p0 = pcol[0], p1 = pcol[1], p2 = pcol[2];
           const double y0 = Rp[0] * p0;
           const double y1 = Rp[1] * p0 + Rp[3] * p1;
           const double y2 = Rp[2] * p0 + Rp[4] * p1 + Rp[5] * p2;
@@ -705,11 +746,12 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
     TP(2);
     if (!slow) {  // zero exactly the entries this thread staged into the other buffer last batch
       double *Yo = &Ys[buf ^ 1][0][0];
+      if (bt > 0 && wrote_prev >= 0) {
 #pragma unroll
-      for (int m = 0; m < IPT; ++m)
-        if (bt > 0 && wrote_prev[m] >= 0) {
-          Yo[wrote_prev[m]] = 0.0; Yo[wrote_prev[m] + NC] = 0.0; Yo[wrote_prev[m] + 2 * NC] = 0.0;
+        for (int c = 0; c < 6; ++c) {
+          Yo[wrote_prev + c] = 0.0; Yo[wrote_prev + NC + c] = 0.0; Yo[wrote_prev + 2 * NC + c] = 0.0;
         }
+      }
     } else if (prev.x >= 0) {  // clear the previous batch's columns in the other buffer
 #pragma unroll
       for (int row = 0; row < kTileRows; ++row)
@@ -961,19 +1003,28 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
     int beg = 0, end = 0;
     if (valid) {
       beg = d.lm_begin[slot]; end = d.lm_begin[slot + 1];
+      // H_lp dx_cam = jl^T (jp dx_cam), Jacobians recomputed at the linearization point
+      const double L0 = d.X[0][4 * slot], L1 = d.X[0][4 * slot + 1], L2 = d.X[0][4 * slot + 2];
+      const double *prt_lin = d.pose_rt[0];
       for (int e = beg + lane; e < end; e += W) {
         const int h = d.obs_camh[e];
         if (h < 0) continue;
-        const double *P = d.obs_P + e, *dx = d.dx + 6 * h;
-        const int64_t nE = d.nE;
-        double x[6], p[18];
+        const double *prt = prt_lin + 16 * d.obs_cam[e], *dx = d.dx + 6 * h;
+        double x[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k) x[k] = dx[k];
-#pragma unroll
-        for (int k = 0; k < 18; ++k) p[k] = P[k * nE];
-        a0 += p[0] * x[0] + p[1] * x[1] + p[2] * x[2] + p[3] * x[3] + p[4] * x[4] + p[5] * x[5];
-        a1 += p[6] * x[0] + p[7] * x[1] + p[8] * x[2] + p[9] * x[3] + p[10] * x[4] + p[11] * x[5];
-        a2 += p[12] * x[0] + p[13] * x[1] + p[14] * x[2] + p[15] * x[3] + p[16] * x[4] + p[17] * x[5];
+        MonoEval m;
+        m.x = prt[0] * L0 + prt[1] * L1 + prt[2] * L2 + prt[9];
+        m.y = prt[3] * L0 + prt[4] * L1 + prt[5] * L2 + prt[10];
+        m.z = prt[6] * L0 + prt[7] * L1 + prt[8] * L2 + prt[11];
+        m.s = d.obs_s[e];
+        double jl[6], jp[12];
+        mono_jac(prt, m, jl, jp);
+        const double t0 = jp[0] * x[0] + jp[1] * x[1] + jp[2] * x[2] + jp[3] * x[3] + jp[5] * x[5];
+        const double t1 = jp[6] * x[0] + jp[7] * x[1] + jp[8] * x[2] + jp[10] * x[4] + jp[11] * x[5];
+        a0 += jl[0] * t0 + jl[3] * t1;
+        a1 += jl[1] * t0 + jl[4] * t1;
+        a2 += jl[2] * t0 + jl[5] * t1;
       }
     }
 #pragma unroll
