@@ -65,19 +65,27 @@ __device__ double block_max(double v, double *red) {
 }
 
 // Givens-rotate row a = (a0,a1,a2) into upper-triangular R (r00 r01 r02 r11 r12 r22).
-// Diagonal of R stays >= 0, so the factor is canonical.
+// Diagonal of R stays >= 0, so the factor is canonical. Each rotation uses
+// one reciprocal square root (v_rsq_f64 + a Newton step): r = h y, c = R y,
+// s = a y with y = 1/sqrt(h), h = R^2 + a^2 -- no divides.
+__device__ __forceinline__ double rsqrt_nr(double h) {
+  double y = __builtin_amdgcn_rsq(h);
+  const double t = 0.5 * h * y;
+  return fma(y, fma(-t, y, 0.5), y);
+}
+
 __device__ __forceinline__ void givens_add_row(double R[6], double a0, double a1, double a2) {
   if (a0 != 0.0) {
-    const double r = sqrt(R[0] * R[0] + a0 * a0);
-    const double c = R[0] / r, s = a0 / r;
-    R[0] = r;
+    const double h = R[0] * R[0] + a0 * a0, y = rsqrt_nr(h);
+    const double c = R[0] * y, s = a0 * y;
+    R[0] = h * y;
     const double t1 = c * R[1] + s * a1; a1 = c * a1 - s * R[1]; R[1] = t1;
     const double t2 = c * R[2] + s * a2; a2 = c * a2 - s * R[2]; R[2] = t2;
   }
   if (a1 != 0.0) {
-    const double r = sqrt(R[3] * R[3] + a1 * a1);
-    const double c = R[3] / r, s = a1 / r;
-    R[3] = r;
+    const double h = R[3] * R[3] + a1 * a1, y = rsqrt_nr(h);
+    const double c = R[3] * y, s = a1 * y;
+    R[3] = h * y;
     const double t2 = c * R[4] + s * a2; a2 = c * a2 - s * R[4]; R[4] = t2;
   }
   if (a2 != 0.0) R[5] = sqrt(R[5] * R[5] + a2 * a2);
