@@ -115,7 +115,7 @@ int upload(sqlm_ctx *c, int idx, const std::vector<T> &v, T **out) {
 
 enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
-  B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS,
+  B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS, B_CAMSLOT, B_CAMUV,
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE
@@ -479,6 +479,20 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_OBSERR, 2 * (size_t)nE, d.obs_err);
   UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
   UP(B_CAMOBS, cam_obs, d.cam_obs);
+  {  // camera-ordered copies of the camera pass inputs (one coalesced stream + the X gather)
+    std::vector<int> cslot(cam_obs.size());
+    std::vector<double> cuv(4 * cam_obs.size());
+    for (size_t t = 0; t < cam_obs.size(); ++t) {
+      const int o = cam_obs[t];
+      cslot[t] = obs_lm[o];
+      cuv[4 * t] = obs_uv[2 * o];
+      cuv[4 * t + 1] = obs_uv[2 * o + 1];
+      cuv[4 * t + 2] = obs_info[o];
+      cuv[4 * t + 3] = obs_delta[o];
+    }
+    UP(B_CAMSLOT, cslot, d.cam_slot);
+    UP(B_CAMUV, cuv, d.cam_uv);
+  }
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
   UP(B_LIDPTR, lid_ptr, d.lid_cam_ptr);

@@ -45,6 +45,8 @@ struct DevProblem {
   // cameras
   int *cam_obs_ptr = nullptr;               // [nP+1]
   int *cam_obs = nullptr;                   // device obs ids per camera, landmark order
+  int *cam_slot = nullptr;                  // [cam_obs] landmark slot, camera order (camera pass)
+  double *cam_uv = nullptr;                 // [cam_obs][4] u v info delta, camera order
   double *Hpp = nullptr;                    // [nP][36]
   double *bp = nullptr;                     // [nP][8]
   // lidar unary edges (grouped by camera)

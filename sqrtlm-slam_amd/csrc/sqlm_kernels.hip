@@ -335,11 +335,11 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
   if (i < d.nP) {
     const double *prt = d.pose_rt[0] + 16 * d.hidx_pose[i];
     for (int t = d.cam_obs_ptr[i] + lane; t < d.cam_obs_ptr[i + 1]; t += 64) {
-      const int e = d.cam_obs[t];
-      const double *X = d.X[0] + 4 * d.obs_lm[e];
-      const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
+      const double *X = d.X[0] + 4 * d.cam_slot[t];
+      const double2 uv = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t);
+      const double2 id = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t + 2);
       MonoEval m;
-      mono_error(prt, X[0], X[1], X[2], uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
+      mono_error(prt, X[0], X[1], X[2], uv.x, uv.y, id.x, id.y, m);
       double jl[6], j[14];
       mono_jac(prt, m, jl, j);
       j[12] = m.s * m.e0;
