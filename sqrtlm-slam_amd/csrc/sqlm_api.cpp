@@ -115,7 +115,7 @@ int upload(sqlm_ctx *c, int idx, const std::vector<T> &v, T **out) {
 
 enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
-  B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS, B_CAMSLOT, B_CAMUV,
+  B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS, B_CAMSLOT, B_CAMUV, B_SROWIDX,
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE
@@ -414,6 +414,11 @@ int prepare(sqlm_ctx *c, int level) {
   d.nE = nE;
   d.nLid = (int64_t)lid_act.size();
   d.nnzb = s_row[nP];
+  // single-GPU tiled path: k_rcs_reduce writes the CR superblocks directly
+  d.cr_direct = (c->cr.enabled && c->use_tiles && !c->comm.enabled()) ? 1 : 0;
+  d.cr_B = c->cr.B;
+  d.cr_n = c->cr.n;
+  d.cr_p = c->cr.p;
   std::vector<double> qt(8 * (size_t)c->n_pose, 0.0), X(4 * (size_t)nL, 0.0);
   for (int p = 0; p < c->n_pose; ++p) {
     for (int k = 0; k < 4; ++k) qt[8 * p + k] = c->pose_q[4 * p + k];
@@ -501,6 +506,12 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_LIDERR, (size_t)d.nLid, d.lid_err);
   UP(B_SROW, s_row, d.s_row_ptr);
   UP(B_SCOL, s_col, d.s_col);
+  {
+    std::vector<int> srow(s_col.size());
+    for (int i = 0; i < nP; ++i)
+      for (int k = s_row[i]; k < s_row[i + 1]; ++k) srow[k] = i;
+    UP(B_SROWIDX, srow, d.s_row);
+  }
   AL(B_S, 36 * (size_t)d.nnzb, d.S);
   AL(B_G, 6 * (size_t)nP, d.g);
   AL(B_DX, 6 * (size_t)nP, d.dx);
@@ -610,7 +621,14 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   else launch_rcs(d, lambda, c->max_row_blocks, c->stream);
   tmark(c, 3, true);
   tmark(c, 8, false);
-  if (c->use_tiles) launch_rcs_reduce(d, lambda, c->stream);
+  if (c->use_tiles) {
+    if (d.cr_direct) {  // the reduce assembles the CR superblocks itself
+      const size_t blkbytes = (size_t)c->cr.p * c->cr.n * c->cr.n * sizeof(double);
+      HIP_OK(hipMemsetAsync(d.cr_D, 0, blkbytes, c->stream));
+      HIP_OK(hipMemsetAsync(d.cr_E, 0, blkbytes, c->stream));
+    }
+    launch_rcs_reduce(d, lambda, c->stream);
+  }
   tmark(c, 8, true);
   int s = comm_allreduce_rcs(c->comm, d, c->stream);
   if (s) return s;

@@ -59,6 +59,7 @@ struct DevProblem {
   int64_t nnzb = 0;
   int *s_row_ptr = nullptr;                 // [nP+1]
   int *s_col = nullptr;                     // [nnzb]
+  int *s_row = nullptr;                     // [nnzb] block row (direct CR assembly)
   double *S = nullptr;                      // [nnzb][36]
   double *g = nullptr;                      // [6 nP]
   double *dx = nullptr;                     // [6 nP]
@@ -85,6 +86,8 @@ struct DevProblem {
   double *cr_D = nullptr, *cr_E = nullptr;  // [p][n][n]
   double *cr_A = nullptr, *cr_C = nullptr;  // [p][n][n]
   double *cr_g = nullptr, *cr_x = nullptr;  // [p][n]
+  int cr_direct = 0;                        // k_rcs_reduce writes D/E/g in CR layout (no BSR S)
+  int cr_B = 0, cr_n = 0, cr_p = 0;
   // reductions
   double *partials = nullptr;               // [kMaxPartials]
   double *scalars = nullptr;                // [8] see Scalar
@@ -135,7 +138,7 @@ int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase co
 #endif
 constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);  // zeroes + scatters unless cr_direct
 // CR levels + top + back substitution on blocks already in CR layout (microbench / tests)
 void launch_cr_core(double *D, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
                     hipStream_t st);

@@ -823,7 +823,10 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
 
 // S block s = sum of its tile partials (tile order) + H_pp + lambda I on the
 // diagonal; g row i likewise. Partials are symmetric: entries that fall in a
-// lower 16x16 tile are read from their transpose.
+// lower 16x16 tile are read from their transpose. With cr_direct the sums go
+// straight into the block-tridiagonal superblocks of the CR solver (D_I and
+// its mirror, E_I = S(I, I+1), g_I, identity on padded rows), replacing the
+// BSR copy and its scatter.
 __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool own = !d.sharded || d.rank == 0;
@@ -843,7 +846,15 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
       v += d.Hpp[36 * j + e];
       if (r == c) v += lambda;
     }
-    d.S[gid] = v;
+    if (!d.cr_direct) {
+      d.S[gid] = v;
+    } else {
+      const int i = d.s_row[s], n = d.cr_n, B = d.cr_B;
+      const int I = i / B, li = i - I * B, J = j / B, lj = j - J * B;
+      double *base = (J == I ? d.cr_D : d.cr_E) + (size_t)I * n * n;
+      base[(6 * li + r) * n + 6 * lj + c] = v;
+      if (J == I && j != i) base[(6 * lj + c) * n + 6 * li + r] = v;
+    }
   }
   const int64_t g2 = gid - d.nnzb * 36;
   if (g2 >= 0 && g2 < (int64_t)d.nP * 6) {
@@ -853,7 +864,24 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
       const int2 ct = d.gred_idx[k];
       v += d.gpart[d.tile_gpart_ptr[ct.x] + 6 * ct.y + r];
     }
-    d.g[6 * i + r] = (own ? d.bp[8 * i + r] : 0.0) + v;
+    v += own ? d.bp[8 * i + r] : 0.0;
+    d.g[6 * i + r] = v;
+    if (d.cr_direct) {
+      const int I = i / d.cr_B, li = i - I * d.cr_B;
+      d.cr_g[(size_t)I * d.cr_n + 6 * li + r] = v;
+    }
+  }
+  if (d.cr_direct) {  // identity on the padded rows of every superblock; solve flag
+    const int64_t g3 = g2 - (int64_t)d.nP * 6;
+    if (g3 >= 0 && g3 < (int64_t)d.cr_p * d.cr_n) {
+      const int I = (int)(g3 / d.cr_n), rr = (int)(g3 % d.cr_n);
+      const int used = min(d.cr_B, d.nP - I * d.cr_B);
+      if (rr >= 6 * used) {
+        d.cr_D[((size_t)I * d.cr_n + rr) * d.cr_n + rr] = 1.0;
+        d.cr_g[(size_t)I * d.cr_n + rr] = 0.0;
+      }
+    }
+    if (gid == 0) d.flags[0] = 1;
   }
 }
 
@@ -877,7 +905,7 @@ int tile_profile_read(long long *out) {
 
 void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st) {
   if (d.nP == 0) return;
-  const int64_t items = d.nnzb * 36 + (int64_t)d.nP * 6;
+  const int64_t items = d.nnzb * 36 + (int64_t)d.nP * 6 + (d.cr_direct ? (int64_t)d.cr_p * d.cr_n : 0);
   hipLaunchKernelGGL(k_rcs_reduce, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, d, lambda);
 }
 
@@ -1112,24 +1140,34 @@ void launch_lidar_chi2(const DevProblem &d, hipStream_t st) {
 
 // ---------------------------------------------------------------- reductions
 
-__device__ double region_sum(const double *p, int n, double *red) {
-  double v = 0.0;
-  for (int k = threadIdx.x; k < n; k += 256) v += p[k];
-  return block_sum(v, red);
-}
-
-__global__ __launch_bounds__(256) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam, int n_lid) {
-  __shared__ double red[4];
-  const double c0 = region_sum(d.partials + kPartChiCurLm, n_lm_cur, red);
-  const double c1 = region_sum(d.partials + kPartChiCurLid, d.nP, red);
-  const double n0 = region_sum(d.partials + kPartChiNewLm, n_lm_new, red);
-  const double n1 = region_sum(d.partials + kPartChiNewLid, n_lid, red);
-  const double s0 = region_sum(d.partials + kPartScaleCam, n_cam, red);
-  const double s1 = region_sum(d.partials + kPartScaleLm, n_lm_new, red);
+// The six partial regions, one wavefront each (fixed order: bitwise deterministic).
+__global__ __launch_bounds__(384) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam, int n_lid) {
+  __shared__ double part[6];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const double *p = d.partials;
+  int n = 0;
+  switch (wave) {
+    case 0: p += kPartChiCurLm; n = n_lm_cur; break;
+    case 1: p += kPartChiCurLid; n = d.nP; break;
+    case 2: p += kPartChiNewLm; n = n_lm_new; break;
+    case 3: p += kPartChiNewLid; n = n_lid; break;
+    case 4: p += kPartScaleCam; n = n_cam; break;
+    default: p += kPartScaleLm; n = n_lm_new; break;
+  }
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  for (int k = lane; k < n; k += 256) {
+    a0 += p[k];
+    if (k + 64 < n) a1 += p[k + 64];
+    if (k + 128 < n) a2 += p[k + 128];
+    if (k + 192 < n) a3 += p[k + 192];
+  }
+  const double v = wave_sum((a0 + a1) + (a2 + a3));
+  if (lane == 0) part[wave] = v;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    d.scalars[kChiCur] = c0 + c1;
-    d.scalars[kChiNew] = n0 + n1;
-    d.scalars[kScale] = s0 + s1;
+    d.scalars[kChiCur] = part[0] + part[1];
+    d.scalars[kChiNew] = part[2] + part[3];
+    d.scalars[kScale] = part[4] + part[5];
     d.scalars[kMaxDiag] = __longlong_as_double((long long)*d.maxdiag);
     d.scalars[kSolveOk] = (double)d.flags[0];
   }
@@ -1137,7 +1175,7 @@ __global__ __launch_bounds__(256) void k_reduce(DevProblem d, int n_lm_cur, int 
 
 void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts, int n_lid_parts,
                    hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, st, d, n_lm_parts_cur, n_lm_parts_new, n_cam_parts,
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(384), 0, st, d, n_lm_parts_cur, n_lm_parts_new, n_cam_parts,
                      n_lid_parts);
 }
 

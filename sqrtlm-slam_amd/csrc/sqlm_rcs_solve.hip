@@ -501,6 +501,11 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
   const int ar = 16 * wave + r16;
   const bool right = I + h < v.p;
+  // every global load of the kernel is issued before the first use (one memory round trip)
+  const double *Li = blk(v.D, I, n);
+  double li[kCRMaxN / 4];
+#pragma unroll
+  for (int u = 0; u < kCRMaxN / 4; ++u) li[u] = Li[kclamp(4 * u + k4, n) * n + ar];
   {
     const double *A = blk(v.A, I, n) + ar * n, *xl = v.x + (size_t)(I - h) * n;
     const double *C = blk(v.C, I, n) + ar * n, *xr = v.x + (size_t)(I + h) * n;
@@ -521,12 +526,11 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
     if (k4 == 0) t[ar] = v.g[(size_t)I * n + ar] - s;
   }
   __syncthreads();
-  const double *Li = blk(v.D, I, n);
   double s = 0.0;  // Linv is lower triangular: k >= 16 wave
 #pragma unroll
   for (int u = 0; u < kCRMaxN / 4; ++u) {
     const int k = kclamp(4 * u + k4, n);
-    s += Li[k * n + ar] * ((4 * u >= 16 * wave && 4 * u < n) ? t[k] : 0.0);
+    s += li[u] * ((4 * u >= 16 * wave && 4 * u < n) ? t[k] : 0.0);
   }
   s = k4_sum(s);
   if (k4 == 0) v.x[(size_t)I * n + ar] = s;
@@ -562,10 +566,12 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
 
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
   CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags};
-  const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
-  if (hipMemsetAsync(d.cr_D, 0, blkbytes, st) != hipSuccess) return -2;
-  if (hipMemsetAsync(d.cr_E, 0, blkbytes, st) != hipSuccess) return -2;
-  hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
+  if (!d.cr_direct) {  // BSR S (sharded runs / row-kernel RCS): zero the superblocks and scatter
+    const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
+    if (hipMemsetAsync(d.cr_D, 0, blkbytes, st) != hipSuccess) return -2;
+    if (hipMemsetAsync(d.cr_E, 0, blkbytes, st) != hipSuccess) return -2;
+    hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
+  }
   launch_cr_core(d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
   hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
