@@ -123,32 +123,33 @@ __device__ __forceinline__ void mono_error(const double *__restrict__ prt, doubl
   m.s = sqrt(rho1 * info);
 }
 
-// Weighted Jacobians: jl (2x3, row-major) d e / d X, jp (2x6) d e / d [omega; upsilon].
+// Weighted Jacobians: jl (2x3, row-major) d e / d X, jp (2x6) d e / d [omega; upsilon]
+// (types_six_dof_expmap.cpp:103-139), written with one reciprocal iz = 1/z:
+// g2o's x/z, 1/z, x/z^2 ... become products of xz = x iz, yz = y iz and iz.
 __device__ __forceinline__ void mono_jac(const double *__restrict__ prt, const MonoEval &m, double jl[6],
                                          double jp[12]) {
-  const double x = m.x, y = m.y, z = m.z, z_2 = z * z;
+  const double iz = 1.0 / m.z, xz = m.x * iz, yz = m.y * iz;
   const double fx = prt[12], fy = prt[13];
-  const double iz = -1. / z;
-  const double t00 = iz * fx, t02 = iz * (-x / z * fx);
-  const double t11 = iz * fy, t12 = iz * (-y / z * fy);
+  const double t00 = -iz * fx, t02 = (xz * iz) * fx;
+  const double t11 = -iz * fy, t12 = (yz * iz) * fy;
   const double s = m.s;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
     jl[c] = s * (t00 * prt[c] + t02 * prt[6 + c]);
     jl[3 + c] = s * (t11 * prt[3 + c] + t12 * prt[6 + c]);
   }
-  jp[0] = s * (x * y / z_2 * fx);
-  jp[1] = s * (-(1 + (x * x / z_2)) * fx);
-  jp[2] = s * (y / z * fx);
-  jp[3] = s * (-1. / z * fx);
+  jp[0] = s * ((xz * yz) * fx);
+  jp[1] = s * (-(1 + xz * xz) * fx);
+  jp[2] = s * (yz * fx);
+  jp[3] = s * (-iz * fx);
   jp[4] = 0.0;
-  jp[5] = s * (x / z_2 * fx);
-  jp[6] = s * ((1 + y * y / z_2) * fy);
-  jp[7] = s * (-x * y / z_2 * fy);
-  jp[8] = s * (-x / z * fy);
+  jp[5] = s * ((xz * iz) * fx);
+  jp[6] = s * ((1 + yz * yz) * fy);
+  jp[7] = s * (-(xz * yz) * fy);
+  jp[8] = s * (-xz * fy);
   jp[9] = 0.0;
-  jp[10] = s * (-1. / z * fy);
-  jp[11] = s * (y / z_2 * fy);
+  jp[10] = s * (-iz * fy);
+  jp[11] = s * ((yz * iz) * fy);
 }
 
 // Column c of an observation's H_lp block P = jl^T jp (3 values), recomputed
