@@ -105,8 +105,9 @@ __device__ __forceinline__ void mono_error(const double *__restrict__ prt, doubl
   m.x = prt[0] * X0 + prt[1] * X1 + prt[2] * X2 + prt[9];
   m.y = prt[3] * X0 + prt[4] * X1 + prt[5] * X2 + prt[10];
   m.z = prt[6] * X0 + prt[7] * X1 + prt[8] * X2 + prt[11];
-  const double pu = (m.x / m.z) * prt[12] + prt[14];
-  const double pv = (m.y / m.z) * prt[13] + prt[15];
+  const double iz = 1.0 / m.z;
+  const double pu = (m.x * iz) * prt[12] + prt[14];
+  const double pv = (m.y * iz) * prt[13] + prt[15];
   m.e0 = u - pu;
   m.e1 = v - pv;
   const double chi2 = m.e0 * (info * m.e0) + m.e1 * (info * m.e1);
