@@ -440,8 +440,10 @@ __global__ void k_damp(DevProblem d, double lambda) {
   const double m11 = i11 * i11 + i12 * i12;
   const double m12 = i12 * i22;
   const double m22 = i22 * i22;
-  double *M = d.lm_M + 8 * l;
-  store2(M, m00, m01); store2(M + 2, m02, m11); store2(M + 4, m12, m22);
+  if (d.obs_P) {  // row-kernel RCS fallback only: M = (R'^T R')^-1 and M b_l
+    double *M = d.lm_M + 8 * l;
+    store2(M, m00, m01); store2(M + 2, m02, m11); store2(M + 4, m12, m22);
+  }
   const double *bl = d.lm_b + 4 * l;
   // R'^-1 (upper) and w = R'^-T b_l; the RCS tiles stage Y = R'^-T P as (R'^-1)^T P
   const double w0 = i00 * bl[0];
@@ -450,11 +452,13 @@ __global__ void k_damp(DevProblem d, double lambda) {
   double *Rp = d.lm_Rp + 12 * l;
   store2(Rp, i00, i01); store2(Rp + 2, i02, i11); store2(Rp + 4, i12, i22);
   store2(Rp + 6, w0, w1); store2(Rp + 8, w2, 0.0);
-  const double v0 = m00 * bl[0] + m01 * bl[1] + m02 * bl[2];
-  const double v1 = m01 * bl[0] + m11 * bl[1] + m12 * bl[2];
-  const double v2 = m02 * bl[0] + m12 * bl[1] + m22 * bl[2];
-  double *v = d.lm_v + 4 * l;
-  store2(v, v0, v1); store2(v + 2, v2, 0.0);
+  if (d.obs_P) {
+    const double v0 = m00 * bl[0] + m01 * bl[1] + m02 * bl[2];
+    const double v1 = m01 * bl[0] + m11 * bl[1] + m12 * bl[2];
+    const double v2 = m02 * bl[0] + m12 * bl[1] + m22 * bl[2];
+    double *v = d.lm_v + 4 * l;
+    store2(v, v0, v1); store2(v + 2, v2, 0.0);
+  }
 }
 
 void launch_damp(const DevProblem &d, double lambda, hipStream_t st) {
@@ -1071,11 +1075,13 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
     }
     double chi = 0.0;
     if (valid) {
-      const double *M = d.lm_M + 8 * slot, *bl = d.lm_b + 4 * slot;
+      // dl = (H_ll + lambda I)^-1 c = R'^-1 (R'^-T c), R'^-1 upper (i00 i01 i02 i11 i12 i22)
+      const double *Ri = d.lm_Rp + 12 * slot, *bl = d.lm_b + 4 * slot;
       const double c0 = bl[0] - a0, c1 = bl[1] - a1, c2 = bl[2] - a2;
-      const double dl0 = M[0] * c0 + M[1] * c1 + M[2] * c2;
-      const double dl1 = M[1] * c0 + M[3] * c1 + M[4] * c2;
-      const double dl2 = M[2] * c0 + M[4] * c1 + M[5] * c2;
+      const double y0 = Ri[0] * c0, y1 = Ri[1] * c0 + Ri[3] * c1, y2 = Ri[2] * c0 + Ri[4] * c1 + Ri[5] * c2;
+      const double dl0 = Ri[0] * y0 + Ri[1] * y1 + Ri[2] * y2;
+      const double dl1 = Ri[3] * y1 + Ri[4] * y2;
+      const double dl2 = Ri[5] * y2;
       const double *X = d.X[0] + 4 * slot;
       const double X0 = X[0] + dl0, X1 = X[1] + dl1, X2 = X[2] + dl2;
       if (lane == 0) {
