@@ -73,6 +73,9 @@ inline unsigned xcd_grid(int total) { return (unsigned)((total + 7) & ~7); }
 
 // ---- dense block factorization in LDS --------------------------------------
 
+constexpr int kT = 17;  // row stride of the 16x16 LDS scratch tiles (odd: conflict free)
+constexpr int kTile = 16 * kT;
+
 // Panel factorization of block column kb (columns c0 .. c0+15, rows c0 .. n-1):
 // right-looking Cholesky of the 16x16 diagonal block fused with the solve of
 // the rows below it. Wave w holds the 16 diagonal rows in lanes 0..15
@@ -126,14 +129,15 @@ __device__ __forceinline__ int panel_waves(int n, int c0) {
   return below <= 48 ? 1 : (below + 47) / 48;
 }
 
-// X = inverse of the lower-triangular 16x16 block at (c0, c0) of L; lane c
-// owns column c of X (forward substitution, L rows read as LDS broadcasts).
-constexpr int kT = 17;  // row stride of the 16x16 LDS scratch tiles (odd: conflict free)
-constexpr int kTile = 16 * kT;
-
-__device__ __forceinline__ void diag_trtri16(const double *L, int ld, int c0, const double *invd,
-                                             double *X /*16 x kT*/) {
-  const int lane = threadIdx.x & 63, c = lane & 15;
+// Inverses of the lower-triangular 16x16 diagonal blocks of L into Dinv, four
+// blocks per wave: lane quarter q takes block 4 wave + q and lane c of it owns
+// column c of X (forward substitution, rows of L read from LDS). Quarters of
+// one wave read different blocks, so no lane fetches a duplicate broadcast.
+__device__ __forceinline__ void diag_trtri16x4(const double *L, int ld, int nt, const double *invd, double *Dinv,
+                                               int wave) {
+  const int lane = threadIdx.x & 63, c = lane & 15, kb = 4 * wave + (lane >> 4);
+  if (kb >= nt) return;
+  const int c0 = 16 * kb;
   double x[16];
 #pragma unroll
   for (int rr = 0; rr < 16; ++rr) {
@@ -144,10 +148,9 @@ __device__ __forceinline__ void diag_trtri16(const double *L, int ld, int c0, co
     const double inv = invd[c0 + rr];
     x[rr] = rr == c ? inv : (rr > c ? -s * inv : 0.0);
   }
-  if (lane < 16) {
+  double *X = Dinv + kb * kTile;
 #pragma unroll
-    for (int rr = 0; rr < 16; ++rr) X[rr * kT + c] = x[rr];
-  }
+  for (int rr = 0; rr < 16; ++rr) X[rr * kT + c] = x[rr];
 }
 
 // One 16x16 trailing-update tile: L[I][J] -= L[I][kb] L[J][kb]^T (one wavefront).
@@ -211,68 +214,67 @@ __device__ __forceinline__ bool wg_potrf_trtri(double *L, int ld, int n, double 
     CR_PROF(4 + 2 * kb);
   }
   // diagonal inverses, one wave per block
-  for (int kb = wave; kb < nt; kb += nw) diag_trtri16(L, ld, 16 * kb, invd, Dinv + kb * kTile);
+  if (wave < (nt + 3) / 4) diag_trtri16x4(L, ld, nt, invd, Dinv, wave);
   __syncthreads();
   CR_PROF(31);
-  // inverse: for jb from last to first, Linv[ib][jb] = -(sum_{kb=jb+1..ib} Linv[ib][kb] L[kb][jb]) Dinv_jb
-  for (int jb = nt - 2; jb >= 0; --jb) {
-    const int c0 = 16 * jb;
-    for (int ib = jb + 1 + wave; ib < nt; ib += nw) {
+  // Linv by columns: L X = I gives X[ib][jb] = -Dinv_ib sum_{k=jb}^{ib-1} L[ib][k] X[k][jb]. Each
+  // wave owns one block column (no barriers between columns; heavy columns on
+  // distinct SIMDs) and parks X[ib][jb] in the unused upper block (jb, ib), since
+  // the other waves keep reading the lower L.
+  {
+    const int jb = wave < 4 ? wave : wave == 4 ? 5 : wave == 5 ? 4 : wave;
+    double *Wi = W + kTile * wave;
+    for (int ib = jb + 1; ib < nt; ++ib) {
       double a[4 * (kCRMaxN / 16)], b[4 * (kCRMaxN / 16)];
 #pragma unroll
       for (int t = 0; t < kCRMaxN / 16; ++t) {
-        const int kb = jb + 1 + t;
-        if (kb <= ib) {
+        const int kb = jb + t;
+        if (kb < ib) {
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
-            a[4 * t + s] = kb == ib ? Dinv[ib * kTile + r16 * kT + 4 * s + k4]
-                                    : L[(16 * kb + r16) * ld + 16 * ib + 4 * s + k4];  // Linv[ib][kb] parked at (kb, ib)
-            b[4 * t + s] = L[(16 * kb + 4 * s + k4) * ld + c0 + r16];
+            a[4 * t + s] = L[(16 * ib + r16) * ld + 16 * kb + 4 * s + k4];
+            b[4 * t + s] = kb == jb ? Dinv[jb * kTile + (4 * s + k4) * kT + r16]
+                                    : L[(16 * jb + 4 * s + k4) * ld + 16 * kb + r16];  // X[kb][jb] parked
           }
         }
       }
       d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int t = 0; t < kCRMaxN / 16; ++t)
-        if (jb + 1 + t <= ib) {
+        if (jb + t < ib) {
 #pragma unroll
           for (int s = 0; s < 4; ++s)
             acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[4 * t + s], b[4 * t + s], acc, 0, 0, 0);
         }
-      double *Wi = W + kTile * ib;  // wave-private (one ib per wave)
 #pragma unroll
       for (int j = 0; j < 4; ++j) Wi[(k4 + 4 * j) * kT + r16] = acc[j];
       wave_sync();
       double a2[4], b2[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        a2[s] = -Wi[r16 * kT + 4 * s + k4];
-        b2[s] = Dinv[jb * kTile + (4 * s + k4) * kT + r16];
+        a2[s] = -Dinv[ib * kTile + r16 * kT + 4 * s + k4];
+        b2[s] = Wi[(4 * s + k4) * kT + r16];
       }
       d4 acc2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
       for (int s = 0; s < 4; ++s) acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[s], b2[s], acc2, 0, 0, 0);
-      // park Linv[ib][jb] in the unused upper block (jb, ib): other waves still read L[ib][jb]
 #pragma unroll
-      for (int j = 0; j < 4; ++j) L[(c0 + k4 + 4 * j) * ld + 16 * ib + r16] = acc2[j];
-    }
-    __syncthreads();
-  }
-  CR_PROF(32);
-  // move the parked blocks down, diagonal blocks <- Dinv
-  for (int t = wave; t < nt * (nt + 1) / 2; t += nw) {  // lower tiles (ib >= jb), one wave each
-    int ib = 0, jb = t;
-    while (jb > ib) { jb -= ib + 1; ++ib; }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int q = lane + 64 * u, r = q >> 4, c = q & 15;
-      L[(16 * ib + r) * ld + 16 * jb + c] =
-          ib > jb ? L[(16 * jb + r) * ld + 16 * ib + c] : Dinv[ib * kTile + r * kT + c];
+      for (int j = 0; j < 4; ++j) L[(16 * jb + k4 + 4 * j) * ld + 16 * ib + r16] = acc2[j];
+      wave_sync();
     }
   }
   __syncthreads();
-  CR_PROF(33);
+  CR_PROF(32);
   return *fail == 0;
+}
+
+// Linv[r][c] of the factored LDS block: diagonal 16x16 blocks in Dinv, the
+// block (ib, jb), ib > jb, parked untransposed at block position (jb, ib).
+__device__ __forceinline__ double linv_at(const double *L, int ld, const double *Dinv, int r, int c) {
+  const int ib = r >> 4, jb = c >> 4;
+  if (ib > jb) return L[(16 * jb + (r & 15)) * ld + 16 * ib + (c & 15)];
+  if (ib == jb) return Dinv[ib * kTile + (r & 15) * kT + (c & 15)];
+  return 0.0;
 }
 
 struct CRView {
@@ -317,7 +319,7 @@ __global__ __launch_bounds__(256) void k_cr_scatter(DevProblem d, CRView v) {
 }
 
 // Factor superblock I into LDS: L <- chol(D_I)^-1; z = L g_I kept in LDS (tmp).
-// Every wave returns; afterwards L holds Linv (lower) and tmp[0:n] = g_I.
+// Every wave returns; afterwards Linv is readable through linv_at() and tmp[0:n] = g_I.
 __device__ __forceinline__ void cr_factor_block(const CRView &v, int I, double *lds, int *fail) {
   const int n = v.n, ld = n + 1, nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n, *W = Dinv + 17 * n, *invd = W + 17 * n;
@@ -351,14 +353,14 @@ __global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
   const int I = h + 2 * h * blockIdx.x, n = v.n, ld = n + 1, nt = n >> 4;
   const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
   cr_factor_block(v, I, lds, &fail);
-  const double *L = lds, *tmp = lds + n * ld;
+  const double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n;
   double *Dg = blk(v.D, I, n);
   for (int r = wave; r < n; r += nw)
-    for (int c = lane; c < n; c += 64) Dg[r * n + c] = c <= (r | 15) ? L[r * ld + c] : 0.0;
+    for (int c = lane; c < n; c += 64) Dg[r * n + c] = linv_at(L, ld, Dinv, r, c);
   if (wave < nt) {  // z = Linv g, rows 16 wave .. +16
     const int ar = 16 * wave + r16;
     double s = 0.0;
-    for (int k = k4; k < 16 * (wave + 1); k += 4) s += L[ar * ld + k] * tmp[k];
+    for (int k = k4; k < 16 * (wave + 1); k += 4) s += linv_at(L, ld, Dinv, ar, k) * tmp[k];
     s = k4_sum(s);
     if (k4 == 0) v.g[(size_t)I * n + ar] = s;
   }
@@ -476,17 +478,18 @@ __global__ __launch_bounds__(512) void k_cr_top(CRView v) {
   cr_factor_block(v, 0, lds, &fail);
   const double *L = lds;
   double *tmp = lds + n * ld, *z = tmp + n;
+  const double *Dinv = tmp + 2 * n;
   const int ar = 16 * wave + r16;
   if (wave < nt) {
     double s = 0.0;
-    for (int k = k4; k < 16 * (wave + 1); k += 4) s += L[ar * ld + k] * tmp[k];
+    for (int k = k4; k < 16 * (wave + 1); k += 4) s += linv_at(L, ld, Dinv, ar, k) * tmp[k];
     s = k4_sum(s);
     if (k4 == 0) z[ar] = s;
   }
   __syncthreads();
   if (wave < nt) {
     double s = 0.0;
-    for (int k = 16 * wave + k4; k < n; k += 4) s += L[k * ld + ar] * z[k];
+    for (int k = 16 * wave + k4; k < n; k += 4) s += linv_at(L, ld, Dinv, k, ar) * z[k];
     s = k4_sum(s);
     if (k4 == 0) v.x[ar] = s;
   }
