@@ -277,6 +277,56 @@ __device__ __forceinline__ double linv_at(const double *L, int ld, const double 
   return 0.0;
 }
 
+// (Linv g) for the 16 rows of block ib (one wavefront; entry per lane r16 after
+// the k-quarter sum). All loads are issued before the FMAs.
+__device__ __forceinline__ double linv_gemv(const double *L, int ld, const double *Dinv, const double *g, int ib) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  double a[kCRMaxN / 4], b[kCRMaxN / 4];
+#pragma unroll
+  for (int t = 0; t < kCRMaxN / 16; ++t)
+    if (t <= ib) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 4 * s + k4;
+        a[4 * t + s] = t < ib ? L[(16 * t + r16) * ld + 16 * ib + k] : Dinv[ib * kTile + r16 * kT + k];
+        b[4 * t + s] = g[16 * t + k];
+      }
+    }
+  double acc = 0.0;
+#pragma unroll
+  for (int t = 0; t < kCRMaxN / 16; ++t)
+    if (t <= ib) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = fma(a[4 * t + s], b[4 * t + s], acc);
+    }
+  return k4_sum(acc);
+}
+
+// (Linv^T z) for the 16 rows of block jb.
+__device__ __forceinline__ double linv_gemv_t(const double *L, int ld, const double *Dinv, const double *z, int jb,
+                                              int nt) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  double a[kCRMaxN / 4], b[kCRMaxN / 4];
+#pragma unroll
+  for (int t = 0; t < kCRMaxN / 16; ++t)
+    if (t >= jb && t < nt) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int k = 4 * s + k4;
+        a[4 * t + s] = t > jb ? L[(16 * jb + k) * ld + 16 * t + r16] : Dinv[jb * kTile + k * kT + r16];
+        b[4 * t + s] = z[16 * t + k];
+      }
+    }
+  double acc = 0.0;
+#pragma unroll
+  for (int t = 0; t < kCRMaxN / 16; ++t)
+    if (t >= jb && t < nt) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = fma(a[4 * t + s], b[4 * t + s], acc);
+    }
+  return k4_sum(acc);
+}
+
 struct CRView {
   int p, n, B, nP;
   double *D, *E, *A, *C, *g, *x;  // [p][n][n] x4, [p][n] x2
@@ -355,14 +405,22 @@ __global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
   cr_factor_block(v, I, lds, &fail);
   const double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n;
   double *Dg = blk(v.D, I, n);
-  for (int r = wave; r < n; r += nw)
-    for (int c = lane; c < n; c += 64) Dg[r * n + c] = linv_at(L, ld, Dinv, r, c);
+  {  // dense Linv, one 16x16 tile per wave step; lane: row lane/4, 4 columns
+    const int r = lane >> 2, c = 4 * (lane & 3);
+    for (int q = wave; q < nt * nt; q += nw) {
+      const int ib = q / nt, jb = q - ib * nt;
+      double o[4];
+      const double *src = ib > jb ? L + (16 * jb + r) * ld + 16 * ib + c : Dinv + ib * kTile + r * kT + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = ib >= jb ? src[e] : 0.0;
+      double *dst = Dg + (16 * ib + r) * n + 16 * jb + c;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[e] = o[e];
+    }
+  }
   if (wave < nt) {  // z = Linv g, rows 16 wave .. +16
-    const int ar = 16 * wave + r16;
-    double s = 0.0;
-    for (int k = k4; k < 16 * (wave + 1); k += 4) s += linv_at(L, ld, Dinv, ar, k) * tmp[k];
-    s = k4_sum(s);
-    if (k4 == 0) v.g[(size_t)I * n + ar] = s;
+    const double s = linv_gemv(L, ld, Dinv, tmp, wave);
+    if (k4 == 0) v.g[(size_t)I * n + 16 * wave + r16] = s;
   }
 }
 
@@ -481,16 +539,12 @@ __global__ __launch_bounds__(512) void k_cr_top(CRView v) {
   const double *Dinv = tmp + 2 * n;
   const int ar = 16 * wave + r16;
   if (wave < nt) {
-    double s = 0.0;
-    for (int k = k4; k < 16 * (wave + 1); k += 4) s += linv_at(L, ld, Dinv, ar, k) * tmp[k];
-    s = k4_sum(s);
+    const double s = linv_gemv(L, ld, Dinv, tmp, wave);
     if (k4 == 0) z[ar] = s;
   }
   __syncthreads();
   if (wave < nt) {
-    double s = 0.0;
-    for (int k = 16 * wave + k4; k < n; k += 4) s += linv_at(L, ld, Dinv, k, ar) * z[k];
-    s = k4_sum(s);
+    const double s = linv_gemv_t(L, ld, Dinv, z, wave, nt);
     if (k4 == 0) v.x[ar] = s;
   }
   CR_PROF(34);
