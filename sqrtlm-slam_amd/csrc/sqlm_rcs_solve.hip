@@ -555,42 +555,79 @@ __global__ __launch_bounds__(512) void k_cr_top(CRView v) {
 __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
   extern __shared__ __attribute__((aligned(16))) double t[];
   const int I = h + 2 * h * blockIdx.x, n = v.n;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
-  const int ar = 16 * wave + r16;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lo = lane & 7, hi = lane >> 3;
   const bool right = I + h < v.p;
-  // every global load of the kernel is issued before the first use (one memory round trip)
-  const double *Li = blk(v.D, I, n);
-  double li[kCRMaxN / 4];
+  // 16-byte loads, eight lanes per 128-byte line; every global load is issued
+  // before the first use (one memory round trip, 56 loads in flight).
+  // y = z - A x_{I-h} - C x_{I+h}: lane (hi, lo) takes rows 16 wave + hi (+8),
+  // columns 16 u + 2 lo (+1); partial sums close over the eight lo lanes.
+  // x_I = Linv^T y: lane takes columns 16 wave + 2 lo (+1), rows k = 16 wave + 8 u + hi
+  // (Linv is lower triangular, rows below 16 wave are zero); sums close over hi.
+  using d2 = HIP_vector_type<double, 2>;
+  const int ca = 2 * lo;
+  const d2 *A = reinterpret_cast<const d2 *>(blk(v.A, I, n)), *C = reinterpret_cast<const d2 *>(blk(v.C, I, n));
+  const d2 *xl = reinterpret_cast<const d2 *>(v.x + (size_t)(I - h) * n);
+  const d2 *xr = reinterpret_cast<const d2 *>(v.x + (size_t)(I + (right ? h : 0)) * n);
+  const d2 *Li = reinterpret_cast<const d2 *>(blk(v.D, I, n));
+  const int r0 = 16 * wave + hi, hn = n >> 1;
+  d2 a0[kCRMaxN / 16], a1[kCRMaxN / 16], c0[kCRMaxN / 16], c1[kCRMaxN / 16], vl[kCRMaxN / 16], vr[kCRMaxN / 16];
+  d2 li[kCRMaxN / 8];
 #pragma unroll
-  for (int u = 0; u < kCRMaxN / 4; ++u) li[u] = Li[kclamp(4 * u + k4, n) * n + ar];
-  {
-    const double *A = blk(v.A, I, n) + ar * n, *xl = v.x + (size_t)(I - h) * n;
-    const double *C = blk(v.C, I, n) + ar * n, *xr = v.x + (size_t)(I + h) * n;
-    double s = 0.0;
+  for (int u = 0; u < kCRMaxN / 16; ++u) {
+    const int c = kclamp(16 * u + ca, n) >> 1;
+    a0[u] = A[r0 * hn + c];
+    a1[u] = A[(r0 + 8) * hn + c];
+    vl[u] = xl[c];
+  }
 #pragma unroll
-    for (int u = 0; u < kCRMaxN / 4; ++u) {
-      const int k = kclamp(4 * u + k4, n);
-      s += A[k] * (4 * u < n ? xl[k] : 0.0);
+  for (int u = 0; u < kCRMaxN / 8; ++u) li[u] = Li[kclamp(16 * wave + 8 * u + hi, n) * hn + 8 * wave + lo];
+  if (right) {
+#pragma unroll
+    for (int u = 0; u < kCRMaxN / 16; ++u) {
+      const int c = kclamp(16 * u + ca, n) >> 1;
+      c0[u] = C[r0 * hn + c];
+      c1[u] = C[(r0 + 8) * hn + c];
+      vr[u] = xr[c];
     }
-    if (right) {
+  }
+  double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-      for (int u = 0; u < kCRMaxN / 4; ++u) {
-        const int k = kclamp(4 * u + k4, n);
-        s += C[k] * (4 * u < n ? xr[k] : 0.0);
+  for (int u = 0; u < kCRMaxN / 16; ++u)
+    if (16 * u < n) {
+      s0 += a0[u].x * vl[u].x + a0[u].y * vl[u].y;
+      s1 += a1[u].x * vl[u].x + a1[u].y * vl[u].y;
+      if (right) {
+        s0 += c0[u].x * vr[u].x + c0[u].y * vr[u].y;
+        s1 += c1[u].x * vr[u].x + c1[u].y * vr[u].y;
       }
     }
-    s = k4_sum(s);
-    if (k4 == 0) t[ar] = v.g[(size_t)I * n + ar] - s;
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    s0 += __shfl_xor(s0, m, 64);
+    s1 += __shfl_xor(s1, m, 64);
+  }
+  if (lo == 0) {
+    t[r0] = v.g[(size_t)I * n + r0] - s0;
+    t[r0 + 8] = v.g[(size_t)I * n + r0 + 8] - s1;
   }
   __syncthreads();
-  double s = 0.0;  // Linv is lower triangular: k >= 16 wave
+  double x0 = 0.0, x1 = 0.0;
 #pragma unroll
-  for (int u = 0; u < kCRMaxN / 4; ++u) {
-    const int k = kclamp(4 * u + k4, n);
-    s += li[u] * ((4 * u >= 16 * wave && 4 * u < n) ? t[k] : 0.0);
+  for (int u = 0; u < kCRMaxN / 8; ++u) {
+    const int k = 16 * wave + 8 * u + hi;
+    const double tk = k < n ? t[kclamp(k, n)] : 0.0;
+    x0 += li[u].x * tk;
+    x1 += li[u].y * tk;
   }
-  s = k4_sum(s);
-  if (k4 == 0) v.x[(size_t)I * n + ar] = s;
+#pragma unroll
+  for (int m = 8; m < 64; m <<= 1) {
+    x0 += __shfl_xor(x0, m, 64);
+    x1 += __shfl_xor(x1, m, 64);
+  }
+  if (hi == 0) {
+    v.x[(size_t)I * n + 16 * wave + ca] = x0;
+    v.x[(size_t)I * n + 16 * wave + ca + 1] = x1;
+  }
 }
 
 __global__ void k_cr_gather(DevProblem d, CRView v) {
