@@ -428,22 +428,39 @@ __global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
 // skipping K blocks that are zero because A is lower triangular (LA).
 template <bool TA, bool TB, bool LA>
 __device__ __forceinline__ d4 tile_gemm(const double *A, const double *B, int n, int ti, int tj) {
+  // K order within each pair of MFMA steps m: lane k4 feeds k = 8m + 2 k4 to the
+  // first and k + 1 to the second, so row-contiguous operands (A untransposed,
+  // B transposed) come in as one 16-byte load per lane and step pair.
+  using d2 = HIP_vector_type<double, 2>;
   const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
   const int ar = ti * 16 + r16, bc = tj * 16 + r16;
   const int kend = LA ? 16 * (ti + 1) : n;
-  double av[kCRMaxN / 4], bv[kCRMaxN / 4];
+  d2 av[kCRMaxN / 8], bv[kCRMaxN / 8];
 #pragma unroll
-  for (int s = 0; s < kCRMaxN / 4; ++s) {
-    const int k = 4 * s + k4;
-    if (4 * s < kend) {
-      av[s] = TA ? A[k * n + ar] : A[ar * n + k];
-      bv[s] = TB ? B[bc * n + k] : B[k * n + bc];
+  for (int m = 0; m < kCRMaxN / 8; ++m) {
+    const int k = 8 * m + 2 * k4;
+    if (8 * m < kend) {
+      if (TA) {
+        av[m].x = A[k * n + ar];
+        av[m].y = A[(k + 1) * n + ar];
+      } else {
+        av[m] = *reinterpret_cast<const d2 *>(A + ar * n + k);
+      }
+      if (TB) {
+        bv[m] = *reinterpret_cast<const d2 *>(B + bc * n + k);
+      } else {
+        bv[m].x = B[k * n + bc];
+        bv[m].y = B[(k + 1) * n + bc];
+      }
     }
   }
   d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int s = 0; s < kCRMaxN / 4; ++s)
-    if (4 * s < kend) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+  for (int m = 0; m < kCRMaxN / 8; ++m)
+    if (8 * m < kend) {
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv[m].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv[m].y, acc, 0, 0, 0);
+    }
   return acc;
 }
 
