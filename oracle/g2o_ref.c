@@ -66,6 +66,79 @@ void orc_mono_jacobians(const double q[4], const double t[3], const double in[4]
   Jp[11] = y / z_2 * fy;
 }
 
+/* EdgeStereoSE3ProjectXYZ::cam_project (types_six_dof_expmap.cpp:150-157):
+ * invz is a float (1/z rounded to single), bf arrives through a float
+ * parameter and bf*invz is a single-precision product. */
+void orc_stereo_project(const double q[4], const double t[3], const double in[4], double bf, const double X[3],
+                        double proj[3]) {
+  double xc[3];
+  se3_map(q, t, X, xc);
+  const float invz = (float)(1.0f / xc[2]);
+  const float bff = (float)bf;
+  proj[0] = xc[0] * invz * in[0] + in[2];
+  proj[1] = xc[1] * invz * in[1] + in[3];
+  const float bz = bff * invz;
+  proj[2] = proj[0] - bz;
+}
+
+/* EdgeStereoSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:188-234). */
+void orc_stereo_jacobians(const double q[4], const double t[3], const double in[4], double bf, const double X[3],
+                          double Jl[9], double Jp[18]) {
+  double xc[3], R[9];
+  se3_map(q, t, X, xc);
+  oq_to_mat(q, R);
+  const double x = xc[0], y = xc[1], z = xc[2], z_2 = z * z, fx = in[0], fy = in[1];
+  for (int c = 0; c < 3; ++c) {
+    Jl[c] = -fx * R[c] / z + fx * x * R[6 + c] / z_2;
+    Jl[3 + c] = -fy * R[3 + c] / z + fy * y * R[6 + c] / z_2;
+    Jl[6 + c] = Jl[c] - bf * R[6 + c] / z_2;
+  }
+  Jp[0] = x * y / z_2 * fx;
+  Jp[1] = -(1 + (x * x / z_2)) * fx;
+  Jp[2] = y / z * fx;
+  Jp[3] = -1. / z * fx;
+  Jp[4] = 0;
+  Jp[5] = x / z_2 * fx;
+  Jp[6] = (1 + y * y / z_2) * fy;
+  Jp[7] = -x * y / z_2 * fy;
+  Jp[8] = -x / z * fy;
+  Jp[9] = 0;
+  Jp[10] = -1. / z * fy;
+  Jp[11] = y / z_2 * fy;
+  Jp[12] = Jp[0] - bf * y / z_2;
+  Jp[13] = Jp[1] + bf * x / z_2;
+  Jp[14] = Jp[2];
+  Jp[15] = Jp[3];
+  Jp[16] = 0;
+  Jp[17] = Jp[5] - bf / z_2;
+}
+
+static inline int is_stereo(const orc_graph *g, int64_t e) { return g->obs_ur && g->obs_ur[e] >= 0.0; }
+
+/* EdgeStereoSE3ProjectXYZ::computeError (types_six_dof_expmap.h:122-127). */
+static void stereo_error(const orc_graph *g, int64_t e, double err[3]) {
+  const int p = g->obs_pose[e];
+  double proj[3];
+  orc_stereo_project(g->pose_q + 4 * p, g->pose_t + 3 * p, g->intr + 4 * p, g->pose_bf[p], g->pt + 3 * g->obs_pt[e],
+                     proj);
+  err[0] = g->obs_uv[2 * e + 0] - proj[0];
+  err[1] = g->obs_uv[2 * e + 1] - proj[1];
+  err[2] = g->obs_ur[e] - proj[2];
+}
+
+/* computeError of edge e (mono or stereo) into obs_err / obs_err3. */
+static void edge_error(orc_graph *g, int64_t e) {
+  if (is_stereo(g, e)) {
+    double er[3];
+    stereo_error(g, e, er);
+    g->obs_err[2 * e] = er[0];
+    g->obs_err[2 * e + 1] = er[1];
+    g->obs_err3[e] = er[2];
+  } else {
+    mono_error(g, e, g->obs_err + 2 * e);
+  }
+}
+
 /* EdgeLidarFlatPoint::computeError (types_six_dof_expmap.h:217-229). The
  * reference forms T_wc = (T_cw)^-1 through a 4x4 inverse and then applies
  * R_wc^-1 (p_w - t_wc); algebraically that is T_cw.map(p_w), which is what is
@@ -116,13 +189,21 @@ static inline void huber(double delta, double e, double rho[2]) {
   }
 }
 
+/* BaseEdge::chi2 = e^T (I info) e, 2-D or 3-D. */
 static inline double mono_chi2(const orc_graph *g, int64_t e) {
   const double *er = g->obs_err + 2 * e, w = g->obs_info[e];
-  return er[0] * (w * er[0]) + er[1] * (w * er[1]);
+  double c = er[0] * (w * er[0]) + er[1] * (w * er[1]);
+  if (is_stereo(g, e)) c += g->obs_err3[e] * (w * g->obs_err3[e]);
+  return c;
 }
 
+/* Outlier threshold of the LBA tags: chi2(0.95) with 2 DoF for mono edges
+ * (g2oOptimizer.cc:956,1123). The reference's LBA never adds stereo edges
+ * (:914-916 is empty); 3 DoF, 7.815, is the ORB-SLAM2 value for them. */
+static inline double tag_threshold(const orc_graph *g, int64_t e) { return is_stereo(g, e) ? 7.815 : 5.991; }
+
 void orc_compute_mono_errors(orc_graph *g) {
-  for (int64_t e = 0; e < g->n_obs; ++e) mono_error(g, e, g->obs_err + 2 * e);
+  for (int64_t e = 0; e < g->n_obs; ++e) edge_error(g, e);
 }
 
 void orc_edge_chi2(const orc_graph *g, double *out) {
@@ -341,7 +422,7 @@ static void ws_free(lm_ws *w) {
 /* SparseOptimizer::computeActiveErrors (sparse_optimizer.cpp:61-88). */
 static void compute_active_errors(lm_ws *w) {
   orc_graph *g = w->g;
-  for (int64_t i = 0; i < w->n_ae; ++i) mono_error(g, w->ae[i], g->obs_err + 2 * w->ae[i]);
+  for (int64_t i = 0; i < w->n_ae; ++i) edge_error(g, w->ae[i]);
   for (int64_t i = 0; i < w->n_al; ++i) lidar_error(g, w->al[i], g->lid_err + w->al[i]);
 }
 
@@ -376,38 +457,57 @@ static void build_system(lm_ws *w) {
     const int64_t e = w->ae[i];
     const int p = g->obs_pose[e], l = g->obs_pt[e];
     const int ph = w->phid[p], lh = w->lhid[l];
-    double A[6], B[12];
-    orc_mono_jacobians(g->pose_q + 4 * p, g->pose_t + 3 * p, g->intr + 4 * p, g->pt + 3 * l, A, B);
-    const double *er = g->obs_err + 2 * e;
+    double A[9], B[18], er[3];
+    const int nr = is_stereo(g, e) ? 3 : 2;
+    if (nr == 3)
+      orc_stereo_jacobians(g->pose_q + 4 * p, g->pose_t + 3 * p, g->intr + 4 * p, g->pose_bf[p], g->pt + 3 * l, A, B);
+    else
+      orc_mono_jacobians(g->pose_q + 4 * p, g->pose_t + 3 * p, g->intr + 4 * p, g->pt + 3 * l, A, B);
+    er[0] = g->obs_err[2 * e];
+    er[1] = g->obs_err[2 * e + 1];
+    er[2] = nr == 3 ? g->obs_err3[e] : 0.0;
     const double info = g->obs_info[e];
-    double omega_r[2] = {-(info * er[0] + 0.0 * er[1]), -(0.0 * er[0] + info * er[1])};
+    double omega_r[3];
+    for (int r = 0; r < nr; ++r) omega_r[r] = -(info * er[r]); /* -(I info) e, off-diagonal zeros exact */
     double wgt = info; /* diagonal of (robust) information */
     if (g->obs_delta[e] > 0.0) {
       double rho[2];
       huber(g->obs_delta[e], mono_chi2(g, e), rho);
       wgt = rho[1] * info;
-      omega_r[0] *= rho[1];
-      omega_r[1] *= rho[1];
+      for (int r = 0; r < nr; ++r) omega_r[r] *= rho[1];
     }
     /* from = point (vertex 0, never fixed) */
     double *bl = w->b + np6 + 3 * lh;
     double *H = w->Hll + 9 * lh;
     for (int r = 0; r < 3; ++r) {
-      bl[r] += A[0 * 3 + r] * omega_r[0] + A[1 * 3 + r] * omega_r[1];
-      for (int c = 0; c < 3; ++c)
-        H[r * 3 + c] += (A[0 * 3 + r] * wgt) * A[0 * 3 + c] + (A[1 * 3 + r] * wgt) * A[1 * 3 + c];
+      double sb = 0.0;
+      for (int k = 0; k < nr; ++k) sb += A[k * 3 + r] * omega_r[k];
+      bl[r] += sb;
+      for (int c = 0; c < 3; ++c) {
+        double sh = 0.0;
+        for (int k = 0; k < nr; ++k) sh += (A[k * 3 + r] * wgt) * A[k * 3 + c];
+        H[r * 3 + c] += sh;
+      }
     }
     if (ph >= 0) {
       double *Bl = w->blk + 18 * w->edge_blk[e]; /* H_pl(pose, point) = B^T W A */
       for (int r = 0; r < 6; ++r)
-        for (int c = 0; c < 3; ++c)
-          Bl[r * 3 + c] += (B[0 * 6 + r] * wgt) * A[0 * 3 + c] + (B[1 * 6 + r] * wgt) * A[1 * 3 + c];
+        for (int c = 0; c < 3; ++c) {
+          double sh = 0.0;
+          for (int k = 0; k < nr; ++k) sh += (B[k * 6 + r] * wgt) * A[k * 3 + c];
+          Bl[r * 3 + c] += sh;
+        }
       double *bp = w->b + 6 * ph;
       double *Hp = w->Hpp + 36 * ph;
       for (int r = 0; r < 6; ++r) {
-        bp[r] += B[0 * 6 + r] * omega_r[0] + B[1 * 6 + r] * omega_r[1];
-        for (int c = 0; c < 6; ++c)
-          Hp[r * 6 + c] += (B[0 * 6 + r] * wgt) * B[0 * 6 + c] + (B[1 * 6 + r] * wgt) * B[1 * 6 + c];
+        double sb = 0.0;
+        for (int k = 0; k < nr; ++k) sb += B[k * 6 + r] * omega_r[k];
+        bp[r] += sb;
+        for (int c = 0; c < 6; ++c) {
+          double sh = 0.0;
+          for (int k = 0; k < nr; ++k) sh += (B[k * 6 + r] * wgt) * B[k * 6 + c];
+          Hp[r * 6 + c] += sh;
+        }
       }
     }
   }
@@ -632,7 +732,7 @@ int orc_local_ba(orc_graph *g, const volatile uint8_t *stop, uint8_t *outlier, o
     uint8_t *dp = malloc(g->n_obs ? g->n_obs : 1);
     orc_depth_positive(g, dp);
     for (int64_t e = 0; e < g->n_obs; ++e) {
-      if (mono_chi2(g, e) > 5.991 || !dp[e]) g->obs_level[e] = 1;
+      if (mono_chi2(g, e) > tag_threshold(g, e) || !dp[e]) g->obs_level[e] = 1;
       g->obs_delta[e] = 0.0;
     }
     free(dp);
@@ -645,7 +745,7 @@ int orc_local_ba(orc_graph *g, const volatile uint8_t *stop, uint8_t *outlier, o
   if (outlier) {
     uint8_t *dp = malloc(g->n_obs ? g->n_obs : 1);
     orc_depth_positive(g, dp);
-    for (int64_t e = 0; e < g->n_obs; ++e) outlier[e] = (mono_chi2(g, e) > 5.991 || !dp[e]);
+    for (int64_t e = 0; e < g->n_obs; ++e) outlier[e] = (mono_chi2(g, e) > tag_threshold(g, e) || !dp[e]);
     free(dp);
   }
   return 1;

@@ -19,6 +19,7 @@
  *   set/restore diag  block_solver.hpp:564-604
  *   linear solve      Thirdparty/g2o/g2o/solvers/linear_solver_eigen.h:94-124
  *   mono edge         Thirdparty/g2o/g2o/types/types_six_dof_expmap.h:90-101, .cpp:103-147
+ *   stereo edge       types_six_dof_expmap.h:112-145, .cpp:150-157 (float invz), :188-234
  *   binary quad form  Thirdparty/g2o/g2o/core/base_binary_edge.hpp:55-120
  *   LiDAR flat edge   types_six_dof_expmap.h:206-234; base_unary_edge.hpp:43-122
  *   Huber             Thirdparty/g2o/g2o/core/robust_kernel_impl.cpp:78-90
@@ -61,6 +62,11 @@ typedef struct orc_graph {
   const double *lid_info;    /* [n_lid] information (1x1)                   */
   uint8_t *lid_level;        /* [n_lid] (in/out)                            */
   double *lid_err;           /* [n_lid] last computed _error                */
+  /* EdgeStereoSE3ProjectXYZ: an edge with obs_ur[e] >= 0 is a stereo edge
+   * (3-D error u, v, u_r; information = I3*info), else mono. */
+  const double *obs_ur;      /* [n_obs] right-image u, NULL = all mono      */
+  const double *pose_bf;     /* [n_pose] bf (mbf) of the edge's keyframe     */
+  double *obs_err3;          /* [n_obs] third error component (stereo), may be NULL if no stereo */
 } orc_graph;
 
 typedef struct orc_stats {
@@ -109,6 +115,11 @@ void orc_se3_oplus(double q[4], double t[3], const double d[6]);
 void orc_quat_rotate(const double q[4], const double v[3], double o[3]);
 void orc_mono_jacobians(const double q[4], const double t[3], const double intr[4],
                         const double X[3], double Jl[6], double Jp[12]);
+/* EdgeStereoSE3ProjectXYZ::cam_project / linearizeOplus: proj[3], Jl 3x3, Jp 3x6. */
+void orc_stereo_project(const double q[4], const double t[3], const double intr[4], double bf,
+                        const double X[3], double proj[3]);
+void orc_stereo_jacobians(const double q[4], const double t[3], const double intr[4], double bf,
+                          const double X[3], double Jl[9], double Jp[18]);
 double orc_lidar_error(const double q[4], const double t[3], const double pc[3],
                        const double pw[3], const double n[3]);
 void orc_lidar_jacobian(const double q[4], const double t[3], const double pc[3],

@@ -25,6 +25,7 @@ class OrcGraph(C.Structure):
         ("obs_delta", C.c_void_p), ("obs_level", C.c_void_p), ("obs_err", C.c_void_p), ("n_lid", C.c_int64),
         ("lid_pose", C.c_void_p), ("lid_pc", C.c_void_p), ("lid_pw", C.c_void_p), ("lid_n", C.c_void_p),
         ("lid_info", C.c_void_p), ("lid_level", C.c_void_p), ("lid_err", C.c_void_p),
+        ("obs_ur", C.c_void_p), ("pose_bf", C.c_void_p), ("obs_err3", C.c_void_p),
     ]
 
 
@@ -93,11 +94,14 @@ class OracleGraph:
         self.lid_info = prob.lid_info.copy()
         self.lid_level = np.zeros(prob.n_lid, np.uint8)
         self.lid_err = np.zeros(prob.n_lid)
+        self.obs_ur = prob.obs_ur.copy() if prob.obs_ur is not None else None
+        self.pose_bf = prob.pose_bf.copy() if prob.pose_bf is not None else None
+        self.obs_err3 = np.zeros(prob.n_obs) if prob.obs_ur is not None else None
         g = OrcGraph()
         g.n_pose, g.n_pt, g.n_obs, g.n_lid = prob.n_pose, prob.n_pt, prob.n_obs, prob.n_lid
         for name in ("pose_q", "pose_t", "pose_fixed", "intr", "pt", "obs_pose", "obs_pt", "obs_uv",
                      "obs_info", "obs_delta", "obs_level", "obs_err", "lid_pose", "lid_pc", "lid_pw",
-                     "lid_n", "lid_info", "lid_level", "lid_err"):
+                     "lid_n", "lid_info", "lid_level", "lid_err", "obs_ur", "pose_bf", "obs_err3"):
             setattr(g, name, _p(getattr(self, name)))
         self.g = g
 
@@ -150,6 +154,27 @@ def mono_jacobians(q, t, intr, X):
     f = lambda a: _p(np.ascontiguousarray(a, np.float64))
     lib().orc_mono_jacobians(f(q), f(t), f(intr), f(X), _p(Jl), _p(Jp))
     return Jl.reshape(2, 3), Jp.reshape(2, 6)
+
+
+def quat_rotate(q, v):
+    o = np.zeros(3)
+    f = lambda a: _p(np.ascontiguousarray(a, np.float64))
+    lib().orc_quat_rotate(f(q), f(v), _p(o))
+    return o
+
+
+def stereo_project(q, t, intr, bf, X):
+    out = np.zeros(3)
+    f = lambda a: _p(np.ascontiguousarray(a, np.float64))
+    lib().orc_stereo_project(f(q), f(t), f(intr), C.c_double(bf), f(X), _p(out))
+    return out
+
+
+def stereo_jacobians(q, t, intr, bf, X):
+    Jl, Jp = np.zeros(9), np.zeros(18)
+    f = lambda a: _p(np.ascontiguousarray(a, np.float64))
+    lib().orc_stereo_jacobians(f(q), f(t), f(intr), C.c_double(bf), f(X), _p(Jl), _p(Jp))
+    return Jl.reshape(3, 3), Jp.reshape(3, 6)
 
 
 def lidar_error(q, t, pc, pw, n):

@@ -9,7 +9,10 @@ assemble (src/backend/g2oOptimizer.cc:805-912, :142-296):
 * points  -> ``VertexSBAPointXYZ`` (always marginalised);
 * obs     -> ``EdgeSE3ProjectXYZ`` in insertion order (pose, point, uv,
   ``invSigma2`` information, Huber delta or 0 for "no kernel", level);
-* lidar   -> ``EdgeLidarFlatPoint`` unary pose edges (g2oOptimizer.cc:1062-1070).
+* lidar   -> ``EdgeLidarFlatPoint`` unary pose edges (g2oOptimizer.cc:1062-1070);
+* stereo  -> an observation with ``obs_ur >= 0`` is an ``EdgeStereoSE3ProjectXYZ``
+  (u, v, u_right; ``bf`` of its keyframe), the GBA stereo branch
+  (g2oOptimizer.cc:247-281); ``obs_ur = None`` means every edge is mono.
 """
 from __future__ import annotations
 
@@ -22,6 +25,7 @@ import numpy as np
 # stores in a float before setDelta (g2oOptimizer.cc:850,902 / :163,236).
 HUBER_MONO_LBA = float(np.float32(np.sqrt(5.991)))
 HUBER_MONO_GBA = float(np.float32(np.sqrt(5.99)))
+HUBER_STEREO = float(np.float32(np.sqrt(7.815)))  # thHuber3D (g2oOptimizer.cc:164)
 CHI2_MONO = 5.991
 
 
@@ -43,6 +47,8 @@ class BAProblem:
     lid_pw: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
     lid_n: np.ndarray = field(default_factory=lambda: np.zeros((0, 3)))
     lid_info: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    obs_ur: np.ndarray | None = None    # (E,) float64, < 0 = mono edge
+    pose_bf: np.ndarray | None = None   # (P,) float64 mbf (stereo edges)
     meta: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -62,6 +68,12 @@ class BAProblem:
         self.lid_pw = np.ascontiguousarray(self.lid_pw, np.float64).reshape(-1, 3)
         self.lid_n = np.ascontiguousarray(self.lid_n, np.float64).reshape(-1, 3)
         self.lid_info = np.ascontiguousarray(self.lid_info, np.float64).reshape(-1)
+        if self.obs_ur is not None:
+            self.obs_ur = np.ascontiguousarray(self.obs_ur, np.float64).reshape(-1)
+            if self.pose_bf is None:
+                raise ValueError("stereo observations need pose_bf")
+        if self.pose_bf is not None:
+            self.pose_bf = np.ascontiguousarray(self.pose_bf, np.float64).reshape(-1)
         self.validate()
 
     @property
@@ -96,6 +108,14 @@ class BAProblem:
                 raise ValueError(f"{name} has wrong length")
         if K and (self.lid_pose.min() < 0 or self.lid_pose.max() >= P):
             raise ValueError("lid_pose out of range")
+        if self.obs_ur is not None and self.obs_ur.shape[0] != E:
+            raise ValueError("obs_ur has wrong length")
+        if self.pose_bf is not None and self.pose_bf.shape[0] != P:
+            raise ValueError("pose_bf has wrong length")
+
+    @property
+    def has_stereo(self) -> bool:
+        return self.obs_ur is not None and bool(np.any(self.obs_ur >= 0))
 
     def copy(self) -> "BAProblem":
         return copy.deepcopy(self)

@@ -302,3 +302,33 @@ def add_lidar_flat(prob: BAProblem, pose: int, n: int, *, seed: int = 0, noise: 
     prob.lid_info = np.full(n, weight)
     prob.validate()
     return prob
+
+
+KITTI_BF = 386.1448  # Camera.bf, cfg/KITTI00-02.yaml
+
+
+def add_stereo(prob: BAProblem, frac: float = 0.5, *, bf: float = KITTI_BF, seed: int = 0,
+               robust_delta: float | None = None, noise: bool = True) -> BAProblem:
+    """Turn a fraction of the observations into EdgeStereoSE3ProjectXYZ edges
+    (GBA stereo branch, g2oOptimizer.cc:247-281): u_right = u - bf / z at the
+    ground truth plus the observation's pixel noise, rounded through float32
+    like ``mvuRight``; every keyframe gets ``mbf = bf``. ``robust_delta``
+    replaces the Huber delta of the stereo edges (the reference uses
+    thHuber3D = sqrt(7.815) when bRobust)."""
+    rng = SplitMix64(seed ^ 0x57E0)
+    E = prob.n_obs
+    sel = rng.uniform(E) < frac
+    gq, gt, gX = prob.meta["gt_q"], prob.meta["gt_t"], prob.meta["gt_pt"]
+    R = quat_to_mat(gq[prob.obs_pose])
+    Xc = np.einsum("eij,ej->ei", R, gX[prob.obs_pt]) + gt[prob.obs_pose]
+    z = Xc[:, 2]
+    oct_ = prob.meta.get("octave")
+    sigma = np.ones(E) if oct_ is None else np.sqrt(1.0 / orb_inv_level_sigma2()[oct_].astype(np.float64))
+    ur = prob.obs_uv[:, 0] - bf / z + (sigma * rng.normal(E) if noise else 0.0)
+    ur = np.where(sel & (z > 0), ur, -1.0).astype(np.float32).astype(np.float64)
+    prob.obs_ur = ur
+    prob.pose_bf = np.full(prob.n_pose, float(np.float32(bf)))
+    if robust_delta is not None:
+        prob.obs_delta = np.where(ur >= 0, robust_delta, prob.obs_delta)
+    prob.validate()
+    return prob
