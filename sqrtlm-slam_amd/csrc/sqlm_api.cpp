@@ -534,6 +534,7 @@ int prepare(sqlm_ctx *c, int level) {
 #undef UP
 #undef AL
   HIP_OK(hipMemsetAsync(d.partials, 0, sizeof(double) * kMaxPartials, c->stream));
+  HIP_OK(hipMemsetAsync(d.maxdiag, 0, sizeof(unsigned long long), c->stream));
   HIP_OK(hipMemsetAsync(d.obs_err, 0, sizeof(double) * 2 * std::max<int64_t>(nE, 1), c->stream));
   launch_pose_prep(d, 0, c->stream);
   return SQLM_OK;
@@ -576,8 +577,7 @@ void acc_events(sqlm_ctx *c, int i0, int i1) {
 // computeActiveErrors + buildSystem for the current state.
 int linearize(sqlm_ctx *c) {
   DevProblem &d = c->d;
-  HIP_OK(hipMemsetAsync(d.maxdiag, 0, sizeof(unsigned long long), c->stream));
-  tmark(c, 0, false);
+  tmark(c, 0, false);  // maxdiag was zeroed by the last k_reduce (or prepare)
   for (size_t b = 0; b < c->buckets.size(); ++b) launch_linearize(d, c->buckets[b], c->bucket_part_off[b], c->stream);
   tmark(c, 0, true);
   tmark(c, 1, false);
@@ -816,7 +816,9 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
     delete c;
     return SQLM_ERR_HIP;
   }
-  for (auto &e : c->ev) (void)hipEventCreate(&e);
+  // timing-only events: no system-scope fence, which would flush caches and
+  // leave a ~10 us bubble between the kernels they separate
+  for (auto &e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   *out = c;
   return SQLM_OK;
 }

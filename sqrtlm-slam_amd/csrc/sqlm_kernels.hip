@@ -1177,6 +1177,7 @@ __global__ __launch_bounds__(384) void k_reduce(DevProblem d, int n_lm_cur, int 
     d.scalars[kChiNew] = part[2] + part[3];
     d.scalars[kScale] = part[4] + part[5];
     d.scalars[kMaxDiag] = __longlong_as_double((long long)*d.maxdiag);
+    *d.maxdiag = 0ull;  // ready for the next linearization's atomicMax
     d.scalars[kSolveOk] = (double)d.flags[0];
   }
 }
