@@ -86,6 +86,14 @@ int sqlm_set_problem(sqlm_ctx *ctx, int n_pose, const double *pose_q, const doub
                      int64_t n_obs, const int32_t *obs_pose, const int32_t *obs_pt, const double *obs_uv,
                      const double *obs_info, const double *obs_delta, const uint8_t *obs_level);
 
+/* EdgeStereoSE3ProjectXYZ (types_six_dof_expmap.h:112-145): edges with
+ * obs_ur[e] >= 0 become stereo edges, error (u, v, u_right) - cam_project
+ * (float invz, float bf*invz, .cpp:150-157), information info*I3; the Huber
+ * delta set for the edge applies to its 3-D chi2. pose_bf [n_pose] = mbf.
+ * obs_ur = NULL (or all < 0) makes every edge mono again. Call after
+ * sqlm_set_problem (which resets it). GBA stereo branch: g2oOptimizer.cc:247-281. */
+int sqlm_set_stereo(sqlm_ctx *ctx, const double *obs_ur, const double *pose_bf);
+
 /* EdgeLidarFlatPoint unary pose edges (types_six_dof_expmap.h:206-234), added
  * after the mono edges (g2oOptimizer.cc:1062-1070). Level 0, no kernel. */
 int sqlm_set_lidar(sqlm_ctx *ctx, int64_t n, const int32_t *pose, const double *p_cam,

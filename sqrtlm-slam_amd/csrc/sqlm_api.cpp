@@ -53,6 +53,8 @@ struct sqlm_ctx {
   std::vector<int32_t> obs_pose, obs_pt;
   std::vector<double> obs_uv, obs_info, obs_delta, obs_err;
   std::vector<uint8_t> obs_level;
+  bool has_stereo = false;           // some edge is an EdgeStereoSE3ProjectXYZ
+  std::vector<double> obs_ur, pose_bf, obs_err3;
   std::vector<int32_t> lid_pose;
   std::vector<double> lid_pc, lid_pw, lid_n, lid_info, lid_err;
   std::vector<uint8_t> lid_level;
@@ -118,7 +120,8 @@ enum BufId {
   B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS, B_CAMSLOT, B_CAMUV, B_SROWIDX,
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
-  B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE
+  B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
+  B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -301,7 +304,7 @@ int prepare(sqlm_ctx *c, int level) {
   std::vector<int> fill(lm_begin.begin(), lm_begin.end() - 1);
   c->dev_edge.assign(nE, 0);
   std::vector<int> obs_lm(nE), obs_cam(nE), obs_camh(nE);
-  std::vector<double> obs_uv(2 * nE), obs_info(nE), obs_delta(nE);
+  std::vector<double> obs_uv(2 * nE), obs_info(nE), obs_delta(nE), obs_ur(c->has_stereo ? nE : 0);
   for (int64_t e = 0; e < c->n_obs; ++e) {
     if (c->obs_level[e] != level) continue;
     const int s = pt_slot[c->obs_pt[e]];
@@ -314,6 +317,7 @@ int prepare(sqlm_ctx *c, int level) {
     obs_uv[2 * o + 1] = c->obs_uv[2 * e + 1];
     obs_info[o] = c->obs_info[e];
     obs_delta[o] = c->obs_delta[e];
+    if (c->has_stereo) obs_ur[o] = c->obs_ur[e];
   }
   // camera CSR (device obs in slot order)
   std::vector<int> cam_ptr(nP + 1, 0), cam_obs;
@@ -497,6 +501,19 @@ int prepare(sqlm_ctx *c, int level) {
     }
     UP(B_CAMSLOT, cslot, d.cam_slot);
     UP(B_CAMUV, cuv, d.cam_uv);
+    if (c->has_stereo) {
+      std::vector<double> cur(cam_obs.size());
+      for (size_t t = 0; t < cam_obs.size(); ++t) cur[t] = obs_ur[cam_obs[t]];
+      UP(B_CAMUR, cur, d.cam_ur);
+    }
+  }
+  d.has_stereo = c->has_stereo ? 1 : 0;
+  if (c->has_stereo) {
+    UP(B_OBSUR, obs_ur, d.obs_ur);
+    UP(B_POSEBF, c->pose_bf, d.pose_bf);
+    AL(B_OBSERR3, (size_t)nE, d.obs_err3);
+  } else {
+    d.obs_ur = d.obs_err3 = d.pose_bf = d.cam_ur = nullptr;
   }
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
@@ -536,6 +553,7 @@ int prepare(sqlm_ctx *c, int level) {
   HIP_OK(hipMemsetAsync(d.partials, 0, sizeof(double) * kMaxPartials, c->stream));
   HIP_OK(hipMemsetAsync(d.maxdiag, 0, sizeof(unsigned long long), c->stream));
   HIP_OK(hipMemsetAsync(d.obs_err, 0, sizeof(double) * 2 * std::max<int64_t>(nE, 1), c->stream));
+  if (d.obs_err3) HIP_OK(hipMemsetAsync(d.obs_err3, 0, sizeof(double) * std::max<int64_t>(nE, 1), c->stream));
   launch_pose_prep(d, 0, c->stream);
   return SQLM_OK;
 }
@@ -543,6 +561,9 @@ int prepare(sqlm_ctx *c, int level) {
 void finish(sqlm_ctx *c) {
   DevProblem &d = c->d;
   std::vector<double> qt(8 * (size_t)c->n_pose), X(4 * (size_t)d.nL), err(2 * (size_t)d.nE), lerr(d.nLid);
+  std::vector<double> err3(d.obs_err3 ? d.nE : 0);
+  if (!err3.empty())
+    (void)hipMemcpyAsync(err3.data(), d.obs_err3, err3.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
   (void)hipMemcpyAsync(qt.data(), d.pose_qt[0], qt.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
   if (d.nL) (void)hipMemcpyAsync(X.data(), d.X[0], X.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
   if (d.nE) (void)hipMemcpyAsync(err.data(), d.obs_err, err.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
@@ -557,6 +578,7 @@ void finish(sqlm_ctx *c) {
   for (int64_t o = 0; o < d.nE; ++o) {
     c->obs_err[2 * c->dev_edge[o]] = err[2 * o];
     c->obs_err[2 * c->dev_edge[o] + 1] = err[2 * o + 1];
+    if (!err3.empty()) c->obs_err3[c->dev_edge[o]] = err3[o];
   }
   for (int64_t t = 0; t < d.nLid; ++t) c->lid_err[c->dev_lid_edge[t]] = lerr[t];
 }
@@ -771,7 +793,18 @@ void depth_positive_host(const sqlm_ctx *c, std::vector<uint8_t> &out) {
 
 inline double edge_chi2(const sqlm_ctx *c, int64_t e) {
   const double e0 = c->obs_err[2 * e], e1 = c->obs_err[2 * e + 1], w = c->obs_info[e];
+  if (c->has_stereo && c->obs_ur[e] >= 0.0) {  // BaseEdge::chi2 of the 3-D stereo error
+    const double e2 = c->obs_err3[e];
+    return e0 * (w * e0) + e1 * (w * e1) + e2 * (w * e2);
+  }
   return e0 * (w * e0) + e1 * (w * e1);
+}
+
+// LBA outlier threshold: chi2(0.95), 2 DoF for mono edges (g2oOptimizer.cc:956,
+// 1123). The reference's LBA adds no stereo edges (:914-916); 7.815 (3 DoF) is
+// the ORB-SLAM2 value for them.
+inline double tag_threshold(const sqlm_ctx *c, int64_t e) {
+  return (c->has_stereo && c->obs_ur[e] >= 0.0) ? 7.815 : 5.991;
 }
 
 }  // namespace
@@ -865,10 +898,31 @@ int sqlm_set_problem(sqlm_ctx *c, int n_pose, const double *pose_q, const double
   if (obs_level) c->obs_level.assign(obs_level, obs_level + n_obs);
   else c->obs_level.assign(n_obs, 0);
   c->obs_err.assign(2 * n_obs, 0.0);
+  c->has_stereo = false;
+  c->obs_ur.clear(); c->pose_bf.clear(); c->obs_err3.clear();
   c->n_lid = 0;
   c->lid_pose.clear(); c->lid_pc.clear(); c->lid_pw.clear(); c->lid_n.clear(); c->lid_info.clear();
   c->lid_level.clear(); c->lid_err.clear();
   c->has_problem = true;
+  return SQLM_OK;
+}
+
+int sqlm_set_stereo(sqlm_ctx *c, const double *obs_ur, const double *pose_bf) {
+  if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  c->has_stereo = false;
+  c->obs_ur.clear(); c->pose_bf.clear(); c->obs_err3.clear();
+  if (!obs_ur) return SQLM_OK;  // back to all-mono
+  if (!pose_bf && c->n_pose) return SQLM_ERR_INVALID_ARG;
+  bool any = false;
+  for (int64_t e = 0; e < c->n_obs; ++e) {
+    if (!std::isfinite(obs_ur[e])) return SQLM_ERR_INVALID_ARG;
+    any |= obs_ur[e] >= 0.0;
+  }
+  if (!any) return SQLM_OK;
+  c->obs_ur.assign(obs_ur, obs_ur + c->n_obs);
+  c->pose_bf.assign(pose_bf, pose_bf + c->n_pose);
+  c->obs_err3.assign(c->n_obs, 0.0);
+  c->has_stereo = true;
   return SQLM_OK;
 }
 
@@ -930,7 +984,7 @@ int sqlm_local_ba(sqlm_ctx *c, const volatile uint8_t *stop, uint8_t *outlier, s
     std::vector<uint8_t> dp;
     depth_positive_host(c, dp);
     for (int64_t e = 0; e < c->n_obs; ++e) {
-      if (edge_chi2(c, e) > 5.991 || !dp[e]) c->obs_level[e] = 1;
+      if (edge_chi2(c, e) > tag_threshold(c, e) || !dp[e]) c->obs_level[e] = 1;
       c->obs_delta[e] = 0.0;
     }
     s = optimize_impl(c, 0, 10, 0.0, stop, &st[1], &n);
@@ -942,7 +996,7 @@ int sqlm_local_ba(sqlm_ctx *c, const volatile uint8_t *stop, uint8_t *outlier, s
   if (outlier) {  // :1119-1136
     std::vector<uint8_t> dp;
     depth_positive_host(c, dp);
-    for (int64_t e = 0; e < c->n_obs; ++e) outlier[e] = (edge_chi2(c, e) > 5.991 || !dp[e]);
+    for (int64_t e = 0; e < c->n_obs; ++e) outlier[e] = (edge_chi2(c, e) > tag_threshold(c, e) || !dp[e]);
   }
   if (ran) *ran = 1;
   return SQLM_OK;

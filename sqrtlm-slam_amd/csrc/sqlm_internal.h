@@ -42,6 +42,12 @@ struct DevProblem {
   double *obs_s = nullptr;                  // [nE] sqrt(rho' info) at the linearization point
   double *obs_P = nullptr;                  // [18][nE] H_lp blocks, SoA: row-kernel fallback only (else null)
   double *obs_err = nullptr;                // [nE][2] last computed error (g2o _error)
+  // stereo edges (EdgeStereoSE3ProjectXYZ): has_stereo selects the ST kernels
+  int has_stereo = 0;
+  double *obs_ur = nullptr;                 // [nE] right-image u, < 0 = mono edge
+  double *obs_err3 = nullptr;               // [nE] third error component (0 for mono)
+  double *pose_bf = nullptr;                // [n_pose] bf
+  double *cam_ur = nullptr;                 // [cam_obs] obs_ur in camera order
   // cameras
   int *cam_obs_ptr = nullptr;               // [nP+1]
   int *cam_obs = nullptr;                   // device obs ids per camera, landmark order

@@ -95,6 +95,7 @@ __device__ __forceinline__ void givens_add_row(double R[6], double a0, double a1
 // with the Huber weight folded in as sqrt(rho' * info) (robust_kernel_impl.cpp:78-90).
 struct MonoEval {
   double e0, e1;      // raw error obs - proj
+  double e2;          // stereo edges: right-image error
   double chi_rob;     // rho(chi2) (robust) or chi2
   double s;           // sqrt(rho' * info)
   double x, y, z;     // camera-frame point
@@ -111,6 +112,38 @@ __device__ __forceinline__ void mono_error(const double *__restrict__ prt, doubl
   m.e0 = u - pu;
   m.e1 = v - pv;
   const double chi2 = m.e0 * (info * m.e0) + m.e1 * (info * m.e1);
+  double rho1 = 1.0;
+  m.chi_rob = chi2;
+  if (delta > 0.0) {
+    const double dsqr = delta * delta;
+    if (chi2 > dsqr) {
+      const double sq = sqrt(chi2);
+      m.chi_rob = 2 * sq * delta - dsqr;
+      rho1 = delta / sq;
+    }
+  }
+  m.s = sqrt(rho1 * info);
+}
+
+// EdgeStereoSE3ProjectXYZ (types_six_dof_expmap.h:122-127, .cpp:150-157): the
+// projection uses invz = (float)(1/z) and the single-precision product
+// bf*invz, as the reference's `const float invz` / `const float &bf` do; chi2
+// adds the right-image component (information = info I3).
+__device__ __forceinline__ void stereo_error(const double *__restrict__ prt, double X0, double X1, double X2,
+                                             double u, double v, double ur, double bf, double info, double delta,
+                                             MonoEval &m) {
+  m.x = prt[0] * X0 + prt[1] * X1 + prt[2] * X2 + prt[9];
+  m.y = prt[3] * X0 + prt[4] * X1 + prt[5] * X2 + prt[10];
+  m.z = prt[6] * X0 + prt[7] * X1 + prt[8] * X2 + prt[11];
+  const float izf = (float)(1.0 / m.z);
+  const double iz = (double)izf;
+  const double pu = (m.x * iz) * prt[12] + prt[14];
+  const double pv = (m.y * iz) * prt[13] + prt[15];
+  const float bz = (float)bf * izf;
+  m.e0 = u - pu;
+  m.e1 = v - pv;
+  m.e2 = ur - (pu - (double)bz);
+  const double chi2 = m.e0 * (info * m.e0) + m.e1 * (info * m.e1) + m.e2 * (info * m.e2);
   double rho1 = 1.0;
   m.chi_rob = chi2;
   if (delta > 0.0) {
@@ -153,11 +186,28 @@ __device__ __forceinline__ void mono_jac(const double *__restrict__ prt, const M
   jp[11] = s * ((yz * iz) * fy);
 }
 
+// Third (right-image) row of a stereo edge, weighted: d e2 / d X = row 0 -
+// bf R(2,:) / z^2, d e2 / d xi = row 0 + bf (-y, x, 0, 0, 0, -1) / z^2
+// (types_six_dof_expmap.cpp:206-233).
+__device__ __forceinline__ void stereo_row(const double *__restrict__ prt, const MonoEval &m, double bf,
+                                           const double jl[6], const double jp[12], double jl3[3], double jp3[6]) {
+  const double iz = 1.0 / m.z, k = m.s * (bf * (iz * iz));
+#pragma unroll
+  for (int c = 0; c < 3; ++c) jl3[c] = jl[c] - k * prt[6 + c];
+  jp3[0] = jp[0] - k * m.y;
+  jp3[1] = jp[1] + k * m.x;
+  jp3[2] = jp[2];
+  jp3[3] = jp[3];
+  jp3[4] = 0.0;
+  jp3[5] = jp[5] - k;
+}
+
 // Column c of an observation's H_lp block P = jl^T jp (3 values), recomputed
 // from the linearization point (pose prt, landmark X, stored weight s) by the
 // same device code k_linearize used, so the consumers need not store P.
+template <bool ST = false>
 __device__ __forceinline__ void hlp_col(const double *prt, double X0, double X1, double X2, double s, int c,
-                                        double out[3]) {
+                                        double out[3], bool stereo = false, double bf = 0.0) {
   MonoEval m;
   m.x = prt[0] * X0 + prt[1] * X1 + prt[2] * X2 + prt[9];
   m.y = prt[3] * X0 + prt[4] * X1 + prt[5] * X2 + prt[10];
@@ -173,6 +223,15 @@ __device__ __forceinline__ void hlp_col(const double *prt, double X0, double X1,
   }
 #pragma unroll
   for (int a = 0; a < 3; ++a) out[a] = jl[a] * p0 + jl[3 + a] * p1;
+  if (ST && stereo) {
+    double jl3[3], jp3[6];
+    stereo_row(prt, m, bf, jl, jp, jl3, jp3);
+    double p2 = jp3[0];
+#pragma unroll
+    for (int k = 1; k < 6; ++k) p2 = c == k ? jp3[k] : p2;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) out[a] += jl3[a] * p2;
+  }
 }
 
 // Workgroup barrier that orders LDS only: global loads issued before it stay in
@@ -224,7 +283,8 @@ int linearize_blocks(const Bucket &b) {
 // weighted Jacobian rows into a private 3x3 R by Givens rotations; a butterfly
 // over the segment merges the R's (TSQR), so every lane ends with the QR
 // factor of the landmark's stacked 2k x 3 Jacobian without forming J^T J.
-template <int W>
+// ST: some edges are stereo (obs_ur >= 0) and add a third row.
+template <int W, bool ST>
 __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin, int slot_end, int part_off) {
   __shared__ double red[4];
   constexpr int SPB = kBlock / W;
@@ -247,11 +307,16 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
         const double *prt = prt_all + 16 * cam;
         const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
         MonoEval m;
-        mono_error(prt, X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
+        double ur = -1.0, bf = 0.0;
+        if (ST) { ur = d.obs_ur[e]; bf = d.pose_bf[cam]; }
+        const bool st = ST && ur >= 0.0;
+        if (st) stereo_error(prt, X0, X1, X2, uv.x, uv.y, ur, bf, d.obs_info[e], d.obs_delta[e], m);
+        else mono_error(prt, X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
         store2(d.obs_err + 2 * e, m.e0, m.e1);
+        if (ST) d.obs_err3[e] = st ? m.e2 : 0.0;
         d.obs_s[e] = m.s;
         chi += m.chi_rob;
-        double jl[6], jp[12];
+        double jl[6], jp[12], jl3[3] = {0, 0, 0}, jp3[6] = {0, 0, 0, 0, 0, 0};
         mono_jac(prt, m, jl, jp);
         const double r0 = m.s * m.e0, r1 = m.s * m.e1;
         b0 -= jl[0] * r0 + jl[3] * r1;
@@ -262,13 +327,21 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
         g2 += jl[2] * jl[2] + jl[5] * jl[5];
         givens_add_row(R, jl[0], jl[1], jl[2]);
         givens_add_row(R, jl[3], jl[4], jl[5]);
+        if (st) {
+          stereo_row(prt, m, bf, jl, jp, jl3, jp3);
+          const double r2 = m.s * m.e2;
+          b0 -= jl3[0] * r2; b1 -= jl3[1] * r2; b2 -= jl3[2] * r2;
+          g0 += jl3[0] * jl3[0]; g1 += jl3[1] * jl3[1]; g2 += jl3[2] * jl3[2];
+          givens_add_row(R, jl3[0], jl3[1], jl3[2]);
+        }
         if (d.obs_P && d.obs_camh[e] >= 0) {
           // row-kernel fallback only: H_lp block jl^T jp (3x6), SoA, entry (a,c) at P[(6a+c) nE + e]
           double *P = d.obs_P + e;
 #pragma unroll
           for (int a = 0; a < 3; ++a)
 #pragma unroll
-            for (int c = 0; c < 6; ++c) P[(6 * a + c) * d.nE] = jl[a] * jp[c] + jl[3 + a] * jp[6 + c];
+            for (int c = 0; c < 6; ++c)
+              P[(6 * a + c) * d.nE] = jl[a] * jp[c] + jl[3 + a] * jp[6 + c] + (st ? jl3[a] * jp3[c] : 0.0);
         }
       }
     }
@@ -312,8 +385,15 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
   const int nb = linearize_blocks(b);
   if (nb <= 0) return;
   switch (b.W) {
-#define SQLM_CASE(WW) \
-  case WW: hipLaunchKernelGGL(k_linearize<WW>, dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, part_off); break;
+#define SQLM_CASE(WW)                                                                                          \
+  case WW:                                                                                                     \
+    if (d.has_stereo)                                                                                          \
+      hipLaunchKernelGGL((k_linearize<WW, true>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end,  \
+                         part_off);                                                                            \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_linearize<WW, false>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, \
+                         part_off);                                                                            \
+    break;
     SQLM_CASE(2) SQLM_CASE(4) SQLM_CASE(8) SQLM_CASE(16) SQLM_CASE(32) SQLM_CASE(64)
 #undef SQLM_CASE
     default: break;
@@ -326,6 +406,7 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
 // weighted pose Jacobian recomputed from the inputs (the same device code as
 // k_linearize, so bit-identical), plus the camera's LiDAR unary edges
 // (numeric Jacobian, base_unary_edge.hpp:82-122).
+template <bool ST>
 __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + wave;
@@ -336,12 +417,16 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
   for (int k = 0; k < 6; ++k) b[k] = 0.0;
   if (i < d.nP) {
     const double *prt = d.pose_rt[0] + 16 * d.hidx_pose[i];
+    const double bf = ST ? d.pose_bf[d.hidx_pose[i]] : 0.0;
     for (int t = d.cam_obs_ptr[i] + lane; t < d.cam_obs_ptr[i + 1]; t += 64) {
       const double *X = d.X[0] + 4 * d.cam_slot[t];
       const double2 uv = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t);
       const double2 id = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t + 2);
+      const double ur = ST ? d.cam_ur[t] : -1.0;
+      const bool st = ST && ur >= 0.0;
       MonoEval m;
-      mono_error(prt, X[0], X[1], X[2], uv.x, uv.y, id.x, id.y, m);
+      if (st) stereo_error(prt, X[0], X[1], X[2], uv.x, uv.y, ur, bf, id.x, id.y, m);
+      else mono_error(prt, X[0], X[1], X[2], uv.x, uv.y, id.x, id.y, m);
       double jl[6], j[14];
       mono_jac(prt, m, jl, j);
       j[12] = m.s * m.e0;
@@ -352,6 +437,18 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
         b[r] -= j[r] * j[12] + j[6 + r] * j[13];
 #pragma unroll
         for (int c = r; c < 6; ++c) H[k++] += j[r] * j[c] + j[6 + r] * j[6 + c];
+      }
+      if (st) {
+        double jl3[3], jp3[6];
+        stereo_row(prt, m, bf, jl, j, jl3, jp3);
+        const double r2 = m.s * m.e2;
+        k = 0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          b[r] -= jp3[r] * r2;
+#pragma unroll
+          for (int c = r; c < 6; ++c) H[k++] += jp3[r] * jp3[c];
+        }
       }
     }
     if (d.nLid > 0) {
@@ -400,7 +497,8 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
 
 void launch_camera_pass(const DevProblem &d, hipStream_t st) {
   if (d.nP == 0) return;
-  hipLaunchKernelGGL(k_camera_pass, dim3((d.nP + 3) / 4), dim3(256), 0, st, d);
+  if (d.has_stereo) hipLaunchKernelGGL(k_camera_pass<true>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d);
+  else hipLaunchKernelGGL(k_camera_pass<false>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d);
 }
 
 // Sharded runs: max |diag(H_pp)| after the cross-rank sum of H_pp.
@@ -639,7 +737,7 @@ __device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int t
   }
 }
 
-template <int NT>
+template <int NT, bool ST>
 __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
   // wave w owns the accumulator tiles q with q % kTileWaves == w
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
@@ -653,6 +751,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
   __shared__ double Lr[kTileMaxLm][6];
   __shared__ double Lx[kTileMaxLm][3];            // landmarks at the linearization point
   __shared__ double Lc[kTileMaxCams][16];         // window cameras: R t fx fy cx cy
+  __shared__ double Lbf[ST ? kTileMaxCams : 1];   // window cameras: bf (stereo edges)
   const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
   const int ncol = 6 * cp, nt = (ncol + 15) >> 4, ld = nt * 16;
@@ -684,10 +783,12 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
       const int u = k >> 4, c = k & 15;
       Lc[u][c] = d.pose_rt[0][16 * d.hidx_pose[d.tile_cams[cb + u]] + c];
     }
+    if (ST)
+      for (int u = tid; u < cp; u += TH) Lbf[u] = d.pose_bf[d.hidx_pose[d.tile_cams[cb + u]]];
   }
   __syncthreads();
   // prefetched raw inputs of one batch (fast path): thread tid owns observation b0 + tid
-  double ps = 0.0;
+  double ps = 0.0, pur = -1.0;
   int pu = -1, pli = 0;
   auto fetch = [&](int bt) {
     const int lb = BL * bt, nl = min(BL, ntl - lb);
@@ -699,6 +800,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
       pli = lb + (o >= e1) + (o >= e2) + (o >= e3);  // tile-local landmark
       pu = d.obs_local[o];
       ps = d.obs_s[o];
+      if (ST) pur = d.obs_ur[o];
     }
   };
   if (nbatch > 0) fetch(0);
@@ -720,14 +822,17 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
         m.y = pr[3] * xl[0] + pr[4] * xl[1] + pr[5] * xl[2] + pr[10];
         m.z = pr[6] * xl[0] + pr[7] * xl[1] + pr[8] * xl[2] + pr[11];
         m.s = ps;
-        double jl[6], jp[12];
+        double jl[6], jp[12], jl3[3] = {0, 0, 0}, jp3[6] = {0, 0, 0, 0, 0, 0};
         mono_jac(pr, m, jl, jp);
+        const bool st = ST && pur >= 0.0;
+        if (st) stereo_row(pr, m, Lbf[pu], jl, jp, jl3, jp3);
         const int row = 3 * (pli - lb), col = 6 * pu;
 #pragma unroll
         for (int c = 0; c < 6; ++c) {
-          const double p0 = jl[0] * jp[c] + jl[3] * jp[6 + c];
-          const double p1 = jl[1] * jp[c] + jl[4] * jp[6 + c];
-          const double p2 = jl[2] * jp[c] + jl[5] * jp[6 + c];
+          double p0 = jl[0] * jp[c] + jl[3] * jp[6 + c];
+          double p1 = jl[1] * jp[c] + jl[4] * jp[6 + c];
+          double p2 = jl[2] * jp[c] + jl[5] * jp[6 + c];
+          if (st) { p0 += jl3[0] * jp3[c]; p1 += jl3[1] * jp3[c]; p2 += jl3[2] * jp3[c]; }
           Y[row][col + c] = r[0] * p0;
           Y[row + 1][col + c] = r[1] * p0 + r[3] * p1;
           Y[row + 2][col + c] = r[2] * p0 + r[4] * p1 + r[5] * p2;
@@ -744,7 +849,8 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
           if (u < 0) continue;
           double pcol[3];
           const double *xl = Lx[lb + li];
-          hlp_col(Lc[u], xl[0], xl[1], xl[2], d.obs_s[o], tid, pcol);
+          const double our = ST ? d.obs_ur[o] : -1.0;
+          hlp_col<ST>(Lc[u], xl[0], xl[1], xl[2], d.obs_s[o], tid, pcol, our >= 0.0, ST ? Lbf[u] : 0.0);
           const double p0 = pcol[0], p1 = pcol[1], p2 = pcol[2];
           const double y0 = Rp[0] * p0;
           const double y1 = Rp[1] * p0 + Rp[3] * p1;
@@ -896,10 +1002,16 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
   (void)max_k;
   const int nt = (6 * max_cp + 15) / 16;
   if (d.n_tiles > 0) {
-    if (nt <= 3) hipLaunchKernelGGL(k_rcs_tile<3>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
-    else if (nt <= 5) hipLaunchKernelGGL(k_rcs_tile<5>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
-    else if (nt <= 7) hipLaunchKernelGGL(k_rcs_tile<7>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
-    else hipLaunchKernelGGL(k_rcs_tile<9>, dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);
+#define SQLM_TILE(NTT)                                                                            \
+  do {                                                                                            \
+    if (d.has_stereo) hipLaunchKernelGGL((k_rcs_tile<NTT, true>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d); \
+    else hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);            \
+  } while (0)
+    if (nt <= 3) SQLM_TILE(3);
+    else if (nt <= 5) SQLM_TILE(5);
+    else if (nt <= 7) SQLM_TILE(7);
+    else SQLM_TILE(9);
+#undef SQLM_TILE
   }
 }
 
@@ -1028,7 +1140,7 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st) {
 
 // Back-substitution dl = M (b_l - sum_i H_lp,i dx_i), X' = X + dl, then the
 // residuals of the landmark's edges at the trial state (computeActiveErrors).
-template <int W>
+template <int W, bool ST>
 __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
                                                          double lambda, int part_off) {
   __shared__ double red[4];
@@ -1067,6 +1179,14 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
         a0 += jl[0] * t0 + jl[3] * t1;
         a1 += jl[1] * t0 + jl[4] * t1;
         a2 += jl[2] * t0 + jl[5] * t1;
+        if (ST && d.obs_ur[e] >= 0.0) {
+          double jl3[3], jp3[6];
+          stereo_row(prt, m, d.pose_bf[d.obs_cam[e]], jl, jp, jl3, jp3);
+          const double t2 = jp3[0] * x[0] + jp3[1] * x[1] + jp3[2] * x[2] + jp3[3] * x[3] + jp3[5] * x[5];
+          a0 += jl3[0] * t2;
+          a1 += jl3[1] * t2;
+          a2 += jl3[2] * t2;
+        }
       }
     }
 #pragma unroll
@@ -1092,9 +1212,16 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
       const double *prt_all = d.pose_rt[1];
       for (int e = beg + lane; e < end; e += W) {
         const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
+        const int cam = d.obs_cam[e];
         MonoEval m;
-        mono_error(prt_all + 16 * d.obs_cam[e], X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
+        const double ur = ST ? d.obs_ur[e] : -1.0;
+        if (ST && ur >= 0.0)
+          stereo_error(prt_all + 16 * cam, X0, X1, X2, uv.x, uv.y, ur, d.pose_bf[cam], d.obs_info[e], d.obs_delta[e],
+                       m);
+        else
+          mono_error(prt_all + 16 * cam, X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
         store2(d.obs_err + 2 * e, m.e0, m.e1);
+        if (ST) d.obs_err3[e] = ur >= 0.0 ? m.e2 : 0.0;
         chi += m.chi_rob;
       }
     }
@@ -1114,10 +1241,14 @@ void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda,
   const int nb = linearize_blocks(b);
   if (nb <= 0) return;
   switch (b.W) {
-#define SQLM_CASE(WW)                                                                                      \
-  case WW:                                                                                                 \
-    hipLaunchKernelGGL(k_landmark_update<WW>, dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, \
-                       lambda, part_off);                                                                  \
+#define SQLM_CASE(WW)                                                                                    \
+  case WW:                                                                                               \
+    if (d.has_stereo)                                                                                    \
+      hipLaunchKernelGGL((k_landmark_update<WW, true>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin,  \
+                         b.slot_end, lambda, part_off);                                                  \
+    else                                                                                                 \
+      hipLaunchKernelGGL((k_landmark_update<WW, false>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, \
+                         b.slot_end, lambda, part_off);                                                  \
     break;
     SQLM_CASE(2) SQLM_CASE(4) SQLM_CASE(8) SQLM_CASE(16) SQLM_CASE(32) SQLM_CASE(64)
 #undef SQLM_CASE

@@ -29,8 +29,10 @@ EXPORTS = [
     "sqlm_get_edge_depth_positive", "sqlm_get_edge_level", "sqlm_pose_from_Tcw_f32", "sqlm_pose_to_Tcw_f32",
     "sqlm_comm_id_size", "sqlm_comm_get_unique_id", "sqlm_ctx_set_comm", "sqlm_ctx_set_host_comm",
     "sqlm_bench_iterations",
-    "sqlm_kernel_timer_name",
+    "sqlm_kernel_timer_name", "sqlm_set_stereo",
 ]
+# every symbol include/sqrtlm_capture.h declares
+CAPTURE_EXPORTS = ["sqlm_capture_write", "sqlm_capture_read", "sqlm_capture_free", "sqlm_capture_replay"]
 
 
 class SqlmError(RuntimeError):

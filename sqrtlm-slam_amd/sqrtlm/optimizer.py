@@ -59,6 +59,8 @@ class Context:
         if p.n_lid:
             check(lib().sqlm_set_lidar(self._h, C.c_int64(p.n_lid), ptr(p.lid_pose), ptr(p.lid_pc), ptr(p.lid_pw),
                                        ptr(p.lid_n), ptr(p.lid_info)), "sqlm_set_lidar")
+        if p.obs_ur is not None:
+            check(lib().sqlm_set_stereo(self._h, ptr(p.obs_ur), ptr(p.pose_bf)), "sqlm_set_stereo")
         self.problem = p
 
     def set_edge_level(self, level: np.ndarray) -> None:

@@ -38,7 +38,10 @@ def shard(prob: BAProblem, rank: int, world: int) -> BAProblem:
     if rank == 0 and prob.n_lid:
         lid = dict(lid_pose=prob.lid_pose, lid_pc=prob.lid_pc, lid_pw=prob.lid_pw, lid_n=prob.lid_n,
                    lid_info=prob.lid_info)
+    stereo = {}
+    if prob.obs_ur is not None:
+        stereo = dict(obs_ur=prob.obs_ur[sel], pose_bf=prob.pose_bf)
     return BAProblem(pose_q=prob.pose_q, pose_t=prob.pose_t, pose_fixed=prob.pose_fixed, intr=prob.intr,
                      pt=prob.pt[lo:hi], obs_pose=prob.obs_pose[sel], obs_pt=prob.obs_pt[sel] - lo,
                      obs_uv=prob.obs_uv[sel], obs_info=prob.obs_info[sel], obs_delta=prob.obs_delta[sel],
-                     obs_level=prob.obs_level[sel], **lid)
+                     obs_level=prob.obs_level[sel], **lid, **stereo)
