@@ -143,3 +143,19 @@ def test_stereo_local_ba_tags(gpu_ctx, oracle):
         assert a["iterations"] == b["iterations"] and a["trace_trials"] == b["trace_trials"]
     q, t = gpu_ctx.poses()
     assert np.abs(q - ref.pose_q).max() < TOL and _rel(gpu_ctx.points(), ref.pt) < TOL
+
+
+@pytest.mark.gpu
+def test_replay_cli_reports_parity():
+    import json
+    import subprocess
+    root = os.path.dirname(HERE)
+    exe = os.path.join(root, "tools", "sqlm_replay")
+    assert os.path.exists(exe), "build tools/ first (__graft_entry__.build())"
+    files = [os.path.join(HERE, "golden", f) for f in FIXTURES]
+    r = subprocess.run([exe] + files, capture_output=True, text=True, timeout=300)
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert len(lines) == 2 and all(x["parity"] for x in lines)
+    assert lines[0]["kind"] == "lba" and lines[0]["n_lid"] > 0 and len(lines[0]["passes"]) == 3
+    assert lines[1]["kind"] == "gba" and lines[1]["passes"][0]["iterations"] == 10
