@@ -25,6 +25,7 @@
  *   Huber             Thirdparty/g2o/g2o/core/robust_kernel_impl.cpp:78-90
  *   local BA schedule src/backend/g2oOptimizer.cc:704-1191
  *   global BA         src/backend/g2oOptimizer.cc:80-362
+ *   essential graph   g2oOptimizer.cc:1212-1534; types_seven_dof_expmap.h:48-122; sim3.h (eg_ref.c)
  */
 #ifndef SQLM_ORACLE_H
 #define SQLM_ORACLE_H
@@ -108,6 +109,34 @@ int orc_global_ba(orc_graph *g, int iterations, const volatile uint8_t *stop, or
 void orc_se3_from_Tcw_f32(const float T[16], double q[4], double t[3]);
 /* Converter::toCvMat(SE3Quat) (Converter.cc:73-79,98-109): q,t -> float 4x4. */
 void orc_se3_to_Tcw_f32(const double q[4], const double t[3], float T[16]);
+
+/* ---- essential graph (eg_ref.c) ------------------------------------------
+ * VertexSim3Expmap per keyframe, S = [qx qy qz qw tx ty tz s] (Sim3 S_iw),
+ * EdgeSim3 e: vertex 0 = ei[e], vertex 1 = ej[e], measurement S_ji,
+ * error log(S_ji * S_i * S_j^-1), information Omega (NULL = identity). */
+typedef struct orc_eg_graph {
+  int n_kf;
+  double *Siw;               /* [n_kf][8] (in/out)                          */
+  const uint8_t *fixed;      /* [n_kf] setFixed (the loop keyframe)         */
+  int fix_scale;             /* VertexSim3Expmap::_fix_scale (bFixScale)    */
+  int64_t n_edge;
+  const int32_t *ei, *ej;    /* [n_edge]                                    */
+  const double *Sji;         /* [n_edge][8]                                 */
+  const double *info;        /* [n_edge][49] row-major or NULL = identity   */
+  double *err;               /* [n_edge][7] last computed _error            */
+} orc_eg_graph;
+
+/* optimizer.optimize(iterations) with setUserLambdaInit(user_lambda) (the
+ * reference uses 1e-16, g2oOptimizer.cc:1226). Returns iterations done. */
+int orc_eg_optimize(orc_eg_graph *g, int iterations, double user_lambda, const volatile uint8_t *stop,
+                    orc_stats *st);
+void orc_sim3_from_update(const double u[7], double S[8]);
+void orc_sim3_log(const double S[8], double out[7]);
+void orc_sim3_mul(const double a[8], const double b[8], double out[8]);
+void orc_sim3_inverse(const double a[8], double out[8]);
+void orc_eg_edge_error(const double Si[8], const double Sj[8], const double C[8], double e[7]);
+void orc_eg_edge_jacobians(const double Si[8], const double Sj[8], const double C[8], int fix_scale, int free_i,
+                           int free_j, double Ji[49], double Jj[49]);
 
 /* Building blocks exposed for the known-answer tests. */
 void orc_se3_exp(const double upd[6], double q[4], double t[3]);

@@ -200,3 +200,79 @@ def se3_to_Tcw_f32(q, t):
     f = lambda a: _p(np.ascontiguousarray(a, np.float64))
     lib().orc_se3_to_Tcw_f32(f(q), f(t), _p(T))
     return T.reshape(4, 4)
+
+
+# ---------------------------------------------------------------- essential graph (eg_ref.c)
+
+class OrcEgGraph(C.Structure):
+    _fields_ = [("n_kf", C.c_int), ("Siw", C.c_void_p), ("fixed", C.c_void_p), ("fix_scale", C.c_int),
+                ("n_edge", C.c_int64), ("ei", C.c_void_p), ("ej", C.c_void_p), ("Sji", C.c_void_p),
+                ("info", C.c_void_p), ("err", C.c_void_p)]
+
+
+class OracleEG:
+    """Owns numpy copies of a synth.PoseGraph and the orc_eg_graph view."""
+
+    def __init__(self, pg):
+        self.Siw = pg.Siw.copy()
+        self.fixed = pg.fixed.copy()
+        self.ei, self.ej, self.Sji = pg.ei.copy(), pg.ej.copy(), pg.Sji.copy()
+        self.info = None if pg.info is None else np.ascontiguousarray(pg.info.reshape(-1, 49))
+        self.err = np.zeros((pg.n_edge, 7))
+        g = OrcEgGraph()
+        g.n_kf, g.n_edge, g.fix_scale = pg.n_kf, pg.n_edge, pg.fix_scale
+        for name in ("Siw", "fixed", "ei", "ej", "Sji", "info", "err"):
+            setattr(g, name, _p(getattr(self, name)))
+        self.g = g
+
+    def optimize(self, iterations=20, user_lambda=1e-16, stop=None):
+        st = OrcStats()
+        lib().orc_eg_optimize.restype = C.c_int
+        n = lib().orc_eg_optimize(C.byref(self.g), iterations, C.c_double(user_lambda), _p(stop), C.byref(st))
+        return n, st.as_dict()
+
+    def edge_chi2(self):
+        if self.info is None:
+            return np.einsum("ei,ei->e", self.err, self.err)
+        I = self.info.reshape(-1, 7, 7)
+        return np.einsum("ei,eij,ej->e", self.err, I, self.err)
+
+
+def _f(a):
+    return _p(np.ascontiguousarray(a, np.float64))
+
+
+def sim3_from_update(u):
+    S = np.zeros(8)
+    lib().orc_sim3_from_update(_f(u), _p(S))
+    return S
+
+
+def sim3_log(S):
+    o = np.zeros(7)
+    lib().orc_sim3_log(_f(S), _p(o))
+    return o
+
+
+def sim3_mul(a, b):
+    o = np.zeros(8)
+    lib().orc_sim3_mul(_f(a), _f(b), _p(o))
+    return o
+
+
+def sim3_inverse(a):
+    o = np.zeros(8)
+    lib().orc_sim3_inverse(_f(a), _p(o))
+    return o
+
+
+def eg_edge_error(Si, Sj, Cm):
+    e = np.zeros(7)
+    lib().orc_eg_edge_error(_f(Si), _f(Sj), _f(Cm), _p(e))
+    return e
+
+
+def eg_edge_jacobians(Si, Sj, Cm, fix_scale=0, free_i=1, free_j=1):
+    Ji, Jj = np.zeros(49), np.zeros(49)
+    lib().orc_eg_edge_jacobians(_f(Si), _f(Sj), _f(Cm), int(fix_scale), int(free_i), int(free_j), _p(Ji), _p(Jj))
+    return Ji.reshape(7, 7), Jj.reshape(7, 7)

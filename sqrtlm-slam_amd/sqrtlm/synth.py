@@ -18,6 +18,9 @@ double as ``Converter::toSE3Quat`` / ``toVector3d`` do (src/utils/Converter.cc:5
 """
 from __future__ import annotations
 
+import copy
+from dataclasses import dataclass, field
+
 import numpy as np
 
 from .problem import HUBER_MONO_GBA, HUBER_MONO_LBA, BAProblem
@@ -332,3 +335,106 @@ def add_stereo(prob: BAProblem, frac: float = 0.5, *, bf: float = KITTI_BF, seed
         prob.obs_delta = np.where(ur >= 0, robust_delta, prob.obs_delta)
     prob.validate()
     return prob
+
+
+# ---------------------------------------------------------------- essential graph
+
+@dataclass
+class PoseGraph:
+    """Essential graph of g2oOptimizer::OptimizeEssentialGraph (g2oOptimizer.cc:1212-1534):
+    Sim3 S_iw per keyframe [qx qy qz qw tx ty tz s], EdgeSim3 (i = vertex 0,
+    j = vertex 1, measurement S_ji), identity information unless ``info``."""
+    Siw: np.ndarray                 # (K,8)
+    fixed: np.ndarray               # (K,) uint8, the loop keyframe
+    fix_scale: int
+    ei: np.ndarray                  # (E,) int32
+    ej: np.ndarray                  # (E,) int32
+    Sji: np.ndarray                 # (E,8)
+    info: np.ndarray | None = None  # (E,7,7)
+    meta: dict = field(default_factory=dict)
+
+    def __post_init__(self):
+        self.Siw = np.ascontiguousarray(self.Siw, np.float64).reshape(-1, 8)
+        self.fixed = np.ascontiguousarray(self.fixed, np.uint8).reshape(-1)
+        self.ei = np.ascontiguousarray(self.ei, np.int32).reshape(-1)
+        self.ej = np.ascontiguousarray(self.ej, np.int32).reshape(-1)
+        self.Sji = np.ascontiguousarray(self.Sji, np.float64).reshape(-1, 8)
+        if self.info is not None:
+            self.info = np.ascontiguousarray(self.info, np.float64).reshape(-1, 7, 7)
+        K, E = self.Siw.shape[0], self.ei.shape[0]
+        if self.fixed.shape[0] != K or self.ej.shape[0] != E or self.Sji.shape[0] != E:
+            raise ValueError("pose graph arrays disagree in length")
+        if E and (min(self.ei.min(), self.ej.min()) < 0 or max(self.ei.max(), self.ej.max()) >= K):
+            raise ValueError("edge vertex out of range")
+
+    @property
+    def n_kf(self) -> int:
+        return self.Siw.shape[0]
+
+    @property
+    def n_edge(self) -> int:
+        return self.ei.shape[0]
+
+    def copy(self) -> "PoseGraph":
+        return copy.deepcopy(self)
+
+
+def _sim3_np(R, t, s):
+    q = quat_from_mat(R)
+    return np.concatenate([q, t, np.atleast_1d(s)[:, None] if np.ndim(s) else np.full((q.shape[0], 1), s)], axis=1)
+
+
+def _sim3_compose(a, b):
+    """a*b for arrays of [q t s] (numpy restatement for data generation only)."""
+    Ra, Rb = quat_to_mat(a[:, :4]), quat_to_mat(b[:, :4])
+    R = Ra @ Rb
+    t = a[:, 7:8] * np.einsum("nij,nj->ni", Ra, b[:, 4:7]) + a[:, 4:7]
+    return np.concatenate([quat_from_mat(R), t, (a[:, 7] * b[:, 7])[:, None]], axis=1)
+
+
+def _sim3_inv(a):
+    R = quat_to_mat(a[:, :4])
+    Rt = np.transpose(R, (0, 2, 1))
+    t = np.einsum("nij,nj->ni", Rt, -a[:, 4:7] / a[:, 7:8])
+    return np.concatenate([quat_from_mat(Rt), t, (1.0 / a[:, 7])[:, None]], axis=1)
+
+
+def make_pose_graph(n_kf: int = 200, *, window: int = 4, n_loops: int = 3, seed: int = 0, noise: bool = True,
+                    drift: float = 0.01, fix_scale: bool = False) -> PoseGraph:
+    """A loop-closing essential graph on the generator's trajectory: spanning
+    tree i -> i-1, covisibility edges to the previous ``window`` keyframes,
+    and ``n_loops`` long edges closing the trajectory onto its start. Edge
+    measurements are ground-truth relative Sim3 (plus noise); the initial
+    estimates carry an accumulated rotation / translation / scale drift, as
+    the uncorrected side of a loop does. Keyframe 0 (the loop keyframe) is fixed."""
+    rng = SplitMix64(seed ^ 0xE55E)
+    i = np.arange(n_kf)
+    yaw = 0.02 * np.sin(i / 10.0)
+    R_cw = np.transpose(_rot_y(yaw), (0, 2, 1))
+    C = np.stack([np.sin(i / 40.0) * 20.0, np.zeros(n_kf), i * 1.0], axis=1)  # camera centres
+    t_cw = -np.einsum("nij,nj->ni", R_cw, C)
+    gt = _sim3_np(R_cw, t_cw, 1.0)
+    pairs = [(k, k - 1) for k in range(1, n_kf)]
+    pairs += [(k, k - d) for k in range(n_kf) for d in range(2, window + 1) if k - d >= 0]
+    loop_src = np.linspace(n_kf - 1, n_kf - 1 - 3 * max(n_loops - 1, 0), n_loops).astype(int)
+    pairs += [(int(a), int(b)) for a, b in zip(loop_src, np.arange(n_loops) * 2)]
+    ei = np.array([p[0] for p in pairs], np.int32)
+    ej = np.array([p[1] for p in pairs], np.int32)
+    Sji = _sim3_compose(gt[ej], _sim3_inv(gt[ei]))
+    if noise:
+        E = ei.size
+        w = rng.normal(3 * E).reshape(-1, 3) * 2e-3
+        dR = _so3_exp(w)
+        Sji = _sim3_compose(np.concatenate([quat_from_mat(dR), rng.normal(3 * E).reshape(-1, 3) * 5e-3,
+                                            np.exp(rng.normal(E) * 1e-3)[:, None]], axis=1), Sji)
+    # drifted initial estimates: accumulated along the trajectory, KF 0 exact
+    acc = np.cumsum(rng.normal(3 * n_kf).reshape(-1, 3) * drift, axis=0)
+    acc[0] = 0.0
+    dS = np.concatenate([quat_from_mat(_so3_exp(acc * 0.2)), acc * 2.0,
+                         np.exp(np.cumsum(rng.normal(n_kf) * drift * (0 if fix_scale else 1)))[:, None]], axis=1)
+    dS[0] = [0, 0, 0, 1, 0, 0, 0, 1]
+    S0 = _sim3_compose(gt, dS)
+    fixed = np.zeros(n_kf, np.uint8)
+    fixed[0] = 1
+    return PoseGraph(Siw=S0, fixed=fixed, fix_scale=int(fix_scale), ei=ei, ej=ej, Sji=Sji,
+                     meta=dict(gt=gt, seed=seed))

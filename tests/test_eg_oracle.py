@@ -1,0 +1,96 @@
+"""Essential-graph oracle: Sim3 algebra of
+Thirdparty/g2o/g2o/types/sim3.h, EdgeSim3 numeric Jacobians and the LM loop,
+pinned by independent checks (parity with the reference itself is unpinned,
+oracle/oracle.h): exp/log inverse pairs on both branches, group identities,
+numeric Jacobians against wider central differences, one LM step against
+numpy-assembled dense normal equations, noise-free convergence."""
+import numpy as np
+import pytest
+
+from sqrtlm import synth
+
+pytestmark = []
+
+
+@pytest.mark.parametrize("scale", [0.0, 0.3])
+@pytest.mark.parametrize("rot", [1e-7, 0.4])
+def test_sim3_exp_log_roundtrip(oracle, scale, rot):
+    rng = np.random.default_rng(int(scale * 10 + rot * 100))
+    for _ in range(10):
+        u = np.concatenate([rng.normal(size=3) * rot, rng.normal(size=3), [rng.normal() * scale]])
+        S = oracle.sim3_from_update(u)
+        np.testing.assert_allclose(oracle.sim3_log(S), u, rtol=1e-9, atol=1e-12)
+
+
+def test_sim3_group_identities(oracle):
+    rng = np.random.default_rng(3)
+    a = oracle.sim3_from_update(rng.normal(size=7) * 0.3)
+    b = oracle.sim3_from_update(rng.normal(size=7) * 0.3)
+    c = oracle.sim3_from_update(rng.normal(size=7) * 0.3)
+    I = oracle.sim3_mul(a, oracle.sim3_inverse(a))
+    np.testing.assert_allclose(oracle.sim3_log(I), np.zeros(7), atol=1e-12)
+    ab_c = oracle.sim3_mul(oracle.sim3_mul(a, b), c)
+    a_bc = oracle.sim3_mul(a, oracle.sim3_mul(b, c))
+    np.testing.assert_allclose(ab_c, a_bc, rtol=1e-12, atol=1e-12)
+
+
+def test_eg_numeric_jacobians_vs_wide_differences(oracle):
+    rng = np.random.default_rng(5)
+    for fix_scale in (0, 1):
+        Si = oracle.sim3_from_update(rng.normal(size=7) * 0.5)
+        Sj = oracle.sim3_from_update(rng.normal(size=7) * 0.5)
+        Cm = oracle.sim3_mul(oracle.sim3_from_update(rng.normal(size=7) * 0.01), oracle.sim3_mul(Sj, oracle.sim3_inverse(Si)))
+        Ji, Jj = oracle.eg_edge_jacobians(Si, Sj, Cm, fix_scale)
+        h = 1e-5
+        for side, J in ((0, Ji), (1, Jj)):
+            for d in range(7):
+                u = np.zeros(7); u[d] = h
+                if fix_scale:
+                    u[6] = 0.0
+                P = oracle.sim3_mul(oracle.sim3_from_update(u), Si if side == 0 else Sj)
+                M = oracle.sim3_mul(oracle.sim3_from_update(-u), Si if side == 0 else Sj)
+                ep = oracle.eg_edge_error(P, Sj, Cm) if side == 0 else oracle.eg_edge_error(Si, P, Cm)
+                em = oracle.eg_edge_error(M, Sj, Cm) if side == 0 else oracle.eg_edge_error(Si, M, Cm)
+                np.testing.assert_allclose(J[:, d], (ep - em) / (2 * h), rtol=1e-4, atol=1e-5)
+            if fix_scale:
+                assert np.all(J[:, 6] == 0.0)
+
+
+def test_eg_lm_step_equals_dense_normal_equations(oracle):
+    pg = synth.make_pose_graph(12, window=3, n_loops=1, seed=2)
+    K = pg.n_kf
+    free = np.nonzero(pg.fixed == 0)[0]
+    hid = -np.ones(K, int); hid[free] = np.arange(free.size)
+    n = 7 * free.size
+    H = np.zeros((n, n)); b = np.zeros(n)
+    for e in range(pg.n_edge):
+        i, j = pg.ei[e], pg.ej[e]
+        err = oracle.eg_edge_error(pg.Siw[i], pg.Siw[j], pg.Sji[e])
+        Ji, Jj = oracle.eg_edge_jacobians(pg.Siw[i], pg.Siw[j], pg.Sji[e], 0, hid[i] >= 0, hid[j] >= 0)
+        J = np.zeros((7, n))
+        if hid[i] >= 0:
+            J[:, 7 * hid[i]:7 * hid[i] + 7] = Ji
+        if hid[j] >= 0:
+            J[:, 7 * hid[j]:7 * hid[j] + 7] = Jj
+        H += J.T @ J
+        b -= J.T @ err
+    lam = 1e-16
+    dx = np.linalg.solve(H + lam * np.eye(n), b)
+    g = oracle.OracleEG(pg)
+    _, st = g.optimize(1, lam)
+    assert st["trace_trials"][0] == 1
+    for k, p in enumerate(free):
+        S1 = oracle.sim3_mul(oracle.sim3_from_update(dx[7 * k:7 * k + 7]), pg.Siw[p])
+        np.testing.assert_allclose(g.Siw[p], S1, rtol=1e-7, atol=1e-8)
+
+
+@pytest.mark.parametrize("fix_scale", [False, True])
+def test_eg_noise_free_converges(oracle, fix_scale):
+    pg = synth.make_pose_graph(60, window=3, n_loops=2, seed=7, noise=False, fix_scale=fix_scale)
+    g = oracle.OracleEG(pg)
+    n, st = g.optimize(20, 1e-16)
+    assert st["chi2_begin"] > 1e-2 and st["chi2_end"] < 1e-16 * max(1.0, st["chi2_begin"]) + 1e-18
+    gt = pg.meta["gt"]
+    # poses relative to the fixed KF 0 recover the ground truth
+    for p in range(pg.n_kf):
+        np.testing.assert_allclose(g.Siw[p, 4:], gt[p, 4:], rtol=1e-6, atol=1e-6)
