@@ -125,6 +125,24 @@ int sqlm_local_ba(sqlm_ctx *ctx, const volatile uint8_t *stop, uint8_t *outlier,
 int sqlm_global_ba(sqlm_ctx *ctx, int iterations, const volatile uint8_t *stop, sqlm_stats *stats,
                    int *n_iter);
 
+/* Essential graph: g2oOptimizer::OptimizeEssentialGraph (g2oOptimizer.cc:1212-1534).
+ * Vertices VertexSim3Expmap (types_seven_dof_expmap.h:48-94), one per keyframe in
+ * g2o id order: Siw [n_kf][8] = qx qy qz qw tx ty tz s (Sim3 S_iw), fixed [n_kf]
+ * (the loop keyframe), fix_scale = bFixScale (VertexSim3Expmap::_fix_scale).
+ * Edges EdgeSim3 (:99-122) in insertion order: vertex 0 = edge_i, vertex 1 =
+ * edge_j, measurement Sji [n_edge][8], error log(S_ji * S_i * S_j^-1),
+ * information info [n_edge][49] row-major (NULL = identity, as the reference).
+ * Numeric Jacobians (central differences, delta 1e-9, base_binary_edge.hpp:131-205). */
+int sqlm_eg_set_problem(sqlm_ctx *ctx, int n_kf, const double *Siw, const uint8_t *fixed, int fix_scale,
+                        int64_t n_edge, const int32_t *edge_i, const int32_t *edge_j, const double *Sji,
+                        const double *info);
+/* optimizer.setUserLambdaInit(user_lambda) (the reference: 1e-16); optimize(iterations). */
+int sqlm_eg_optimize(sqlm_ctx *ctx, int iterations, double user_lambda, const volatile uint8_t *stop,
+                     sqlm_stats *stats, int *n_iter);
+int sqlm_eg_get_poses(sqlm_ctx *ctx, double *Siw);
+/* e->chi2() from the last computed error (g2o semantics). */
+int sqlm_eg_get_edge_chi2(sqlm_ctx *ctx, double *chi2);
+
 /* Results (write-back inputs, g2oOptimizer.cc:1167-1189, :306-360). */
 int sqlm_get_poses(sqlm_ctx *ctx, double *pose_q, double *pose_t);
 int sqlm_get_points(sqlm_ctx *ctx, double *pt);

@@ -76,6 +76,8 @@ struct sqlm_ctx {
   double *h_scalars = nullptr;  // pinned
   // ---- comm ----
   Comm comm;
+  // ---- essential graph (sqlm_eg.hip) ----
+  EGSolver *eg = nullptr;
   // ---- timing ----
   hipEvent_t ev[2 * SQLM_NKERNEL_TIMERS] = {};
   bool timing = false;
@@ -861,6 +863,7 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   comm_destroy(c->comm);
+  if (c->eg) eg_destroy(c->eg);
   for (auto &b : c->bufs)
     if (b.p) (void)hipFree(b.p);
   for (auto &e : c->ev)
@@ -1000,6 +1003,31 @@ int sqlm_local_ba(sqlm_ctx *c, const volatile uint8_t *stop, uint8_t *outlier, s
   }
   if (ran) *ran = 1;
   return SQLM_OK;
+}
+
+int sqlm_eg_set_problem(sqlm_ctx *c, int n_kf, const double *Siw, const uint8_t *fixed, int fix_scale, int64_t n_edge,
+                        const int32_t *ei, const int32_t *ej, const double *Sji, const double *info) {
+  if (!c) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  if (!c->eg && !(c->eg = eg_create(c->stream))) return SQLM_ERR_OOM;
+  return eg_set_problem(c->eg, n_kf, Siw, fixed, fix_scale, n_edge, ei, ej, Sji, info);
+}
+
+int sqlm_eg_optimize(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8_t *stop, sqlm_stats *st,
+                     int *n_iter) {
+  if (!c || !c->eg) return SQLM_ERR_STATE;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  return eg_optimize(c->eg, iterations, user_lambda, stop, st, n_iter);
+}
+
+int sqlm_eg_get_poses(sqlm_ctx *c, double *Siw) {
+  if (!c || !c->eg) return SQLM_ERR_STATE;
+  return eg_get_poses(c->eg, Siw);
+}
+
+int sqlm_eg_get_edge_chi2(sqlm_ctx *c, double *chi2) {
+  if (!c || !c->eg) return SQLM_ERR_STATE;
+  return eg_get_edge_chi2(c->eg, chi2);
 }
 
 int sqlm_global_ba(sqlm_ctx *c, int iterations, const volatile uint8_t *stop, sqlm_stats *st, int *n_iter) {

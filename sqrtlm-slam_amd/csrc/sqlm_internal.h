@@ -148,6 +148,11 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);  // 
 // CR levels + top + back substitution on blocks already in CR layout (microbench / tests)
 void launch_cr_core(double *D, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
                     hipStream_t st);
+// Dense SPD solve (sqlm_rcs_solve.hip): A (n x n, lower, n % kCRMaxN == 0) is
+// factored in place into L (+ diagonal block inverses Linv), r is consumed,
+// x = A^-1 r; flags[0] is cleared on a non-positive pivot.
+int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
+                           hipStream_t st);
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off,
                             hipStream_t st);
@@ -157,5 +162,16 @@ void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, 
 void launch_depth_positive(const DevProblem &d, uint8_t *out_dev, hipStream_t st);
 
 int linearize_blocks(const Bucket &b);
+
+// Essential graph (sqlm_eg.hip): one solver per context, on the context's stream.
+struct EGSolver;
+EGSolver *eg_create(hipStream_t st);
+void eg_destroy(EGSolver *s);
+int eg_set_problem(EGSolver *s, int n_kf, const double *Siw, const uint8_t *fixed, int fix_scale, int64_t n_edge,
+                   const int32_t *ei, const int32_t *ej, const double *Sji, const double *info);
+int eg_optimize(EGSolver *s, int iterations, double user_lambda, const volatile uint8_t *stop, struct sqlm_stats *st,
+                int *n_iter);
+int eg_get_poses(const EGSolver *s, double *Siw);
+int eg_get_edge_chi2(const EGSolver *s, double *chi2);
 
 }  // namespace sqlm

@@ -56,6 +56,12 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 // compiler issues them all before the first use.
 __device__ __forceinline__ int kclamp(int k, int n) { return k < n ? k : n - 1; }
 
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
 // sum over the four k4 groups of a wave (lanes r16, r16+16, r16+32, r16+48)
 __device__ __forceinline__ double k4_sum(double s) {
   s += __shfl_xor(s, 16, 64);
@@ -645,6 +651,165 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
     v.x[(size_t)I * n + 16 * wave + ca] = x0;
     v.x[(size_t)I * n + 16 * wave + ca + 1] = x1;
   }
+}
+
+// ---- dense SPD solve (essential graph) --------------------------------------
+// Blocked right-looking Cholesky of an n x n SPD matrix (n a multiple of
+// kCRMaxN, lower triangle of A row-major), block size nb = kCRMaxN:
+//   Linv_kk = chol(A_kk)^-1 (LDS factor), L_ik = A_ik Linv_kk^T,
+//   A_ij -= L_ik L_jk^T (k < j <= i, MFMA tiles),
+// then L L^T x = b by block forward / backward substitution.
+struct DenseView {
+  int n, nblk;
+  double *A, *L, *Linv;  // [n][n], [n][n], [nblk][nb][nb]
+  double *r, *x;         // [n] right-hand side (consumed), solution
+  int *flags;
+};
+
+__global__ __launch_bounds__(512) void k_dchol_diag(DenseView v, int k) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int fail;
+  constexpr int nb = kCRMaxN;
+  const int ld = nb + 1, nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double *L = lds, *tmp = lds + nb * ld, *Dinv = tmp + 2 * nb, *W = Dinv + 17 * nb, *invd = W + 17 * nb;
+  const double *Ak = v.A + (size_t)k * nb * v.n + (size_t)k * nb;
+  for (int r = wave; r < nb; r += nw)
+    for (int c = lane; c < nb; c += 64)
+      if (c <= (r | 15)) L[r * ld + c] = Ak[(size_t)r * v.n + c];
+  __syncthreads();
+  if (!wg_potrf_trtri(L, ld, nb, Dinv, W, invd, &fail) && threadIdx.x == 0) v.flags[0] = 0;
+  double *Lo = v.Linv + (size_t)k * nb * nb;
+  for (int r = wave; r < nb; r += nw)
+    for (int c = lane; c < nb; c += 64) Lo[r * nb + c] = linv_at(L, ld, Dinv, r, c);
+}
+
+// 16x16 tile of X Y^T over K = kend (X, Y row-major with their own leading dims).
+__device__ __forceinline__ d4 tile_xyt(const double *X, int ldx, const double *Y, int ldy, int kend) {
+  using d2 = HIP_vector_type<double, 2>;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  d2 av[kCRMaxN / 8], bv[kCRMaxN / 8];
+#pragma unroll
+  for (int m = 0; m < kCRMaxN / 8; ++m)
+    if (8 * m < kend) {
+      av[m] = *reinterpret_cast<const d2 *>(X + (size_t)r16 * ldx + 8 * m + 2 * k4);
+      bv[m] = *reinterpret_cast<const d2 *>(Y + (size_t)r16 * ldy + 8 * m + 2 * k4);
+    }
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int m = 0; m < kCRMaxN / 8; ++m)
+    if (8 * m < kend) {
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv[m].x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv[m].y, acc, 0, 0, 0);
+    }
+  return acc;
+}
+
+// L_ik = A_ik Linv_kk^T for every block row i > k; one wavefront per 16x16 tile.
+__global__ __launch_bounds__(64) void k_dchol_panel(DenseView v, int k, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  constexpr int nb = kCRMaxN, nt = nb / 16;
+  const int bi = k + 1 + lb / (nt * nt), t = lb % (nt * nt), ti = t / nt, tj = t % nt;
+  const double *X = v.A + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb;
+  const double *Y = v.Linv + (size_t)k * nb * nb + (size_t)(16 * tj) * nb;  // Linv rows 16 tj..: lower, K <= 16 (tj+1)
+  const d4 acc = tile_xyt(X, v.n, Y, nb, 16 * (tj + 1));
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  double *o = v.L + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb + 16 * tj;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[(size_t)(k4 + 4 * j) * v.n + r16] = acc[j];
+}
+
+// A_ij -= L_ik L_jk^T for k < j <= i (diagonal blocks: lower tiles only).
+__global__ __launch_bounds__(64) void k_dchol_update(DenseView v, int k, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  constexpr int nb = kCRMaxN, nt = nb / 16;
+  // block pair (bi, bj), bi >= bj > k, row-major over the lower block triangle; 49 tiles each
+  const int pair = lb / (nt * nt), t = lb % (nt * nt);
+  int ii = 0, rem = pair;
+  while (rem > ii) { rem -= ii + 1; ++ii; }
+  const int bi = k + 1 + ii, bj = k + 1 + rem, ti = t / nt, tj = t % nt;
+  if (bi == bj && tj > ti) return;
+  const double *X = v.L + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb;
+  const double *Y = v.L + (size_t)(bj * nb + 16 * tj) * v.n + (size_t)k * nb;
+  const d4 acc = tile_xyt(X, v.n, Y, v.n, nb);
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  double *o = v.A + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)bj * nb + 16 * tj;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[(size_t)(k4 + 4 * j) * v.n + r16] -= acc[j];
+}
+
+// forward: y_k = Linv_kk r_k (into x), then r_i -= L_ik y_k for rows below
+__global__ __launch_bounds__(128) void k_dtrsv_fwd_diag(DenseView v, int k) {
+  constexpr int nb = kCRMaxN;
+  const int r = threadIdx.x;
+  if (r >= nb) return;
+  const double *Li = v.Linv + (size_t)k * nb * nb + (size_t)r * nb, *rk = v.r + (size_t)k * nb;
+  double s = 0.0;
+  for (int m = 0; m <= r; ++m) s += Li[m] * rk[m];
+  v.x[(size_t)k * nb + r] = s;
+}
+
+// one wavefront per row below block k: r_i -= L_i,k-block . y_k
+__global__ __launch_bounds__(256) void k_dtrsv_fwd_update(DenseView v, int k) {
+  constexpr int nb = kCRMaxN;
+  const int row = (k + 1) * nb + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= v.n) return;
+  const double *Lr = v.L + (size_t)row * v.n + (size_t)k * nb, *y = v.x + (size_t)k * nb;
+  double s = 0.0;
+  for (int m = lane; m < nb; m += 64) s += Lr[m] * y[m];
+  s = wave_sum_d(s);
+  if (lane == 0) v.r[row] -= s;
+}
+
+// backward: x_k = Linv_kk^T r_k, then r_j -= L_kj^T x_k for columns left of block k
+__global__ __launch_bounds__(128) void k_dtrsv_bwd_diag(DenseView v, int k) {
+  constexpr int nb = kCRMaxN;
+  const int c = threadIdx.x;
+  if (c >= nb) return;
+  const double *Lk = v.Linv + (size_t)k * nb * nb, *rk = v.r + (size_t)k * nb;
+  double s = 0.0;
+  for (int m = c; m < nb; ++m) s += Lk[(size_t)m * nb + c] * rk[m];
+  v.x[(size_t)k * nb + c] = s;
+}
+
+__global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k) {
+  constexpr int nb = kCRMaxN;
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= k * nb) return;
+  const double *Lk = v.L + (size_t)k * nb * v.n + c, *xk = v.x + (size_t)k * nb;
+  double s = 0.0;
+  for (int m = 0; m < nb; ++m) s += Lk[(size_t)m * v.n] * xk[m];
+  v.r[c] -= s;
+}
+
+int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
+                           hipStream_t st) {
+  constexpr int nb = kCRMaxN, nt = nb / 16;
+  if (n <= 0 || n % nb) return -1;
+  const int nblk = n / nb;
+  DenseView v{n, nblk, A, L, Linv, r, x, flags};
+  const size_t lds = cr_factor_lds(nb);
+  for (int k = 0; k < nblk; ++k) {
+    hipLaunchKernelGGL(k_dchol_diag, dim3(1), dim3(512), lds, st, v, k);
+    const int m = nblk - 1 - k;
+    if (m == 0) break;
+    const int np = m * nt * nt, nu = m * (m + 1) / 2 * nt * nt;
+    hipLaunchKernelGGL(k_dchol_panel, dim3(xcd_grid(np)), dim3(64), 0, st, v, k, np);
+    hipLaunchKernelGGL(k_dchol_update, dim3(xcd_grid(nu)), dim3(64), 0, st, v, k, nu);
+  }
+  for (int k = 0; k < nblk; ++k) {
+    hipLaunchKernelGGL(k_dtrsv_fwd_diag, dim3(1), dim3(128), 0, st, v, k);
+    const int rows = n - (k + 1) * nb;
+    if (rows > 0) hipLaunchKernelGGL(k_dtrsv_fwd_update, dim3((rows + 3) / 4), dim3(256), 0, st, v, k);
+  }
+  // y (in x) becomes the right-hand side of the backward pass
+  if (hipMemcpyAsync(r, x, sizeof(double) * n, hipMemcpyDeviceToDevice, st) != hipSuccess) return -2;
+  for (int k = nblk - 1; k >= 0; --k) {
+    hipLaunchKernelGGL(k_dtrsv_bwd_diag, dim3(1), dim3(128), 0, st, v, k);
+    if (k > 0) hipLaunchKernelGGL(k_dtrsv_bwd_update, dim3((k * nb + 255) / 256), dim3(256), 0, st, v, k);
+  }
+  return 0;
 }
 
 __global__ void k_cr_gather(DevProblem d, CRView v) {

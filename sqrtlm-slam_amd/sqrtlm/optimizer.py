@@ -21,7 +21,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check, lib, ptr
-from .problem import HUBER_MONO_GBA, BAProblem
+from .problem import HUBER_STEREO, HUBER_MONO_GBA, BAProblem
 
 
 class Context:
@@ -154,6 +154,32 @@ class Context:
         check(lib().sqlm_get_edge_level(self._h, ptr(out)), "sqlm_get_edge_level")
         return out
 
+    # ------------------------------------------------------------- essential graph
+    def eg_set_problem(self, pg) -> None:
+        """A synth.PoseGraph (Sim3 vertices, EdgeSim3 edges) -> sqlm_eg_set_problem."""
+        info = None if pg.info is None else np.ascontiguousarray(pg.info.reshape(-1, 49), np.float64)
+        check(lib().sqlm_eg_set_problem(self._h, pg.n_kf, ptr(pg.Siw), ptr(pg.fixed), int(pg.fix_scale),
+                                        C.c_int64(pg.n_edge), ptr(pg.ei), ptr(pg.ej), ptr(pg.Sji), ptr(info)),
+              "sqlm_eg_set_problem")
+        self.pose_graph = pg
+
+    def eg_optimize(self, iterations: int = 20, user_lambda: float = 1e-16, stop=None):
+        st = _lib.Stats()
+        n = C.c_int(0)
+        check(lib().sqlm_eg_optimize(self._h, int(iterations), C.c_double(user_lambda), ptr(stop), C.byref(st),
+                                     C.byref(n)), "sqlm_eg_optimize")
+        return n.value, st.as_dict()
+
+    def eg_poses(self):
+        S = np.zeros((self.pose_graph.n_kf, 8))
+        check(lib().sqlm_eg_get_poses(self._h, ptr(S)), "sqlm_eg_get_poses")
+        return S
+
+    def eg_edge_chi2(self):
+        out = np.zeros(self.pose_graph.n_edge)
+        check(lib().sqlm_eg_get_edge_chi2(self._h, ptr(out)), "sqlm_eg_get_edge_chi2")
+        return out
+
 
 def comm_unique_id() -> bytes:
     n = lib().sqlm_comm_id_size()
@@ -223,7 +249,8 @@ class Optimizer:
         """g2oOptimizer::BundleAdjustment (g2oOptimizer.cc:110-362): KF 0 fixed
         (caller sets pose_fixed), Huber (float)sqrt(5.99) if bRobust."""
         c = cls._context(ctx)
-        prob.obs_delta[:] = HUBER_MONO_GBA if bRobust else 0.0
+        stereo = prob.obs_ur >= 0 if prob.obs_ur is not None else np.zeros(prob.n_obs, bool)
+        prob.obs_delta[:] = np.where(stereo, HUBER_STEREO, HUBER_MONO_GBA) if bRobust else 0.0
         c.set_problem(prob)
         n, st = c.global_ba(nIterations, stop_flag)
         cls._write_back(c, prob)
@@ -234,3 +261,14 @@ class Optimizer:
                                bRobust: bool = True, ctx: Context | None = None):
         """g2oOptimizer::GlobalBundleAdjustemnt (g2oOptimizer.cc:80-89)."""
         return cls.BundleAdjustment(prob, nIterations, stop_flag, nLoopKF, bRobust, ctx)
+
+    @classmethod
+    def OptimizeEssentialGraph(cls, pg, ctx: Context | None = None, stop_flag=None):
+        """g2oOptimizer::OptimizeEssentialGraph (g2oOptimizer.cc:1212-1534) on an
+        assembled pose graph: setUserLambdaInit(1e-16), optimize(20); the
+        corrected Sim3 estimates are written back into ``pg.Siw``."""
+        c = cls._context(ctx)
+        c.eg_set_problem(pg)
+        n, st = c.eg_optimize(20, 1e-16, stop_flag)
+        pg.Siw[:] = c.eg_poses()
+        return n, st

@@ -400,11 +400,13 @@ def _sim3_inv(a):
 
 
 def make_pose_graph(n_kf: int = 200, *, window: int = 4, n_loops: int = 3, seed: int = 0, noise: bool = True,
-                    drift: float = 0.01, fix_scale: bool = False) -> PoseGraph:
+                    drift: float = 0.01, fix_scale: bool = False, rot_noise: float = 2e-3,
+                    trans_noise: float = 5e-3, scale_noise: float = 1e-3) -> PoseGraph:
     """A loop-closing essential graph on the generator's trajectory: spanning
     tree i -> i-1, covisibility edges to the previous ``window`` keyframes,
     and ``n_loops`` long edges closing the trajectory onto its start. Edge
-    measurements are ground-truth relative Sim3 (plus noise); the initial
+    measurements are ground-truth relative Sim3 (plus noise of the given
+    standard deviations: rotation rad, translation m, log-scale); the initial
     estimates carry an accumulated rotation / translation / scale drift, as
     the uncorrected side of a loop does. Keyframe 0 (the loop keyframe) is fixed."""
     rng = SplitMix64(seed ^ 0xE55E)
@@ -423,10 +425,11 @@ def make_pose_graph(n_kf: int = 200, *, window: int = 4, n_loops: int = 3, seed:
     Sji = _sim3_compose(gt[ej], _sim3_inv(gt[ei]))
     if noise:
         E = ei.size
-        w = rng.normal(3 * E).reshape(-1, 3) * 2e-3
+        w = rng.normal(3 * E).reshape(-1, 3) * rot_noise
         dR = _so3_exp(w)
-        Sji = _sim3_compose(np.concatenate([quat_from_mat(dR), rng.normal(3 * E).reshape(-1, 3) * 5e-3,
-                                            np.exp(rng.normal(E) * 1e-3)[:, None]], axis=1), Sji)
+        Sji = _sim3_compose(np.concatenate([quat_from_mat(dR), rng.normal(3 * E).reshape(-1, 3) * trans_noise,
+                                            np.exp(rng.normal(E) * (0.0 if fix_scale else scale_noise))[:, None]],
+                                           axis=1), Sji)
     # drifted initial estimates: accumulated along the trajectory, KF 0 exact
     acc = np.cumsum(rng.normal(3 * n_kf).reshape(-1, 3) * drift, axis=0)
     acc[0] = 0.0

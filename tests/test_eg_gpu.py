@@ -1,0 +1,79 @@
+"""Essential graph on the HIP path vs the CPU oracle
+on identical seeded pose graphs.
+
+What is compared, and why (measured):
+  * one LM iteration: the whole pipeline (numeric Jacobians, assembly, dense
+    Cholesky, Sim3 update) — estimates within 1e-8 relative;
+  * to convergence, noise-free graphs: the same optimum within 1e-9;
+  * to convergence with measurement noise: final chi2 within 1e-6 relative and
+    estimates within 1e-4. The LM stops on accept/reject decisions made on
+    chi2 differences at the numeric-Jacobian noise floor (central differences
+    over 1e-9), so the last iteration can differ and the optimum is flat in
+    some directions: iteration counts are not compared.
+Problems use bFixScale = true (stereo / RGB-D, the KITTI case). With a free
+scale, g2o's Sim3(update) (sim3.h:98-104, theta < 1e-5 <= |sigma|) computes
+B = ((sigma^2/2 - sigma + 1) s) / sigma^3, which makes the update erratic; the
+restatement reproduces it, so only the first step is compared there.
+"""
+import numpy as np
+import pytest
+
+from sqrtlm import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return np.abs(a - b).max() / max(1.0, np.abs(b).max())
+
+
+def _both(gpu_ctx, oracle, pg, iters):
+    ref = oracle.OracleEG(pg)
+    nr, sr = ref.optimize(iters, 1e-16)
+    gpu_ctx.eg_set_problem(pg)
+    ng, sg = gpu_ctx.eg_optimize(iters, 1e-16)
+    return ref, sr, sg
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_eg_first_iteration_matches(gpu_ctx, oracle, seed):
+    pg = synth.make_pose_graph(300, window=4, n_loops=3, seed=seed, fix_scale=True, rot_noise=3e-4,
+                               trans_noise=5e-4)
+    ref, sr, sg = _both(gpu_ctx, oracle, pg, 1)
+    assert sg["trace_trials"] == sr["trace_trials"]
+    assert abs(sg["chi2_end"] - sr["chi2_end"]) <= 1e-8 * sr["chi2_begin"]
+    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-8
+    np.testing.assert_allclose(gpu_ctx.eg_edge_chi2(), ref.edge_chi2(), rtol=1e-6, atol=1e-12)
+
+
+def test_eg_free_scale_first_iteration(gpu_ctx, oracle):
+    pg = synth.make_pose_graph(60, window=4, n_loops=3, seed=3, noise=False, fix_scale=False)
+    ref, sr, sg = _both(gpu_ctx, oracle, pg, 1)
+    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-5
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_eg_noise_free_same_optimum(gpu_ctx, oracle, seed):
+    pg = synth.make_pose_graph(400, window=4, n_loops=3, seed=seed, noise=False, fix_scale=True)
+    ref, sr, sg = _both(gpu_ctx, oracle, pg, 20)
+    assert sg["chi2_end"] < 1e-18 and sr["chi2_end"] < 1e-18
+    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-9
+    np.testing.assert_allclose(gpu_ctx.eg_poses()[:, 4:], pg.meta["gt"][:, 4:], atol=1e-6)
+
+
+@pytest.mark.parametrize("seed", [1, 3])
+def test_eg_noisy_same_optimum(gpu_ctx, oracle, seed):
+    pg = synth.make_pose_graph(150, window=4, n_loops=3, seed=seed, fix_scale=True, rot_noise=3e-4,
+                               trans_noise=5e-4)
+    ref, sr, sg = _both(gpu_ctx, oracle, pg, 20)
+    assert abs(sg["chi2_end"] - sr["chi2_end"]) <= 1e-6 * sr["chi2_end"]
+    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-4
+
+
+def test_eg_facade_writes_back(gpu_ctx, oracle):
+    from sqrtlm.optimizer import Optimizer
+    pg = synth.make_pose_graph(60, seed=14, noise=False, fix_scale=True)
+    ref = oracle.OracleEG(pg)
+    ref.optimize(20, 1e-16)
+    n, st = Optimizer.OptimizeEssentialGraph(pg, ctx=gpu_ctx)
+    assert n > 0 and _rel(pg.Siw, ref.Siw) < 1e-9
