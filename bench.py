@@ -144,12 +144,77 @@ def cpu_baseline(prob, name: str):
                       f"single thread, {total_dt:.1f} s of optimize() time"}
 
 
+EG_N_KF = 1500  # KITTI-00 keyframe count of ORB-SLAM2-style mapping (SURVEY.md §8 sizes, config 5: EG 7*#KF)
+
+
+def bench_eg(args, world):
+    """Essential graph (g2oOptimizer.cc:1212-1534) on a
+    KITTI-00-scale loop: 1500 Sim3 keyframes, spanning tree + 8 covisibility
+    edges per keyframe + 20 loop edges, fix-scale (stereo). A step is one LM
+    iteration of optimize(20) with lambda_init 1e-16, as the reference runs it;
+    replicas only (one pose graph per GPU)."""
+    from sqrtlm import synth
+    from sqrtlm.optimizer import Context
+    pg = synth.make_pose_graph(EG_N_KF, window=8, n_loops=20, seed=5, fix_scale=True)
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+    with Context(local_rank) as ctx:
+        for _ in range(max(1, args.warmup)):
+            ctx.eg_set_problem(pg)
+            ctx.eg_optimize(20, 1e-16)
+        if world > 1:
+            dist.barrier()
+        n_it, t_tot, st = 0, 0.0, None
+        for _ in range(max(1, args.steps // 20)):
+            ctx.eg_set_problem(pg)
+            t0 = time.perf_counter()
+            n, st = ctx.eg_optimize(20, 1e-16)
+            t_tot += time.perf_counter() - t0
+            n_it += n
+        ms = 1000.0 * t_tot / max(1, n_it)
+    if world > 1:
+        import torch
+        tt = torch.tensor([ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ms = float(tt.item())
+    if rank == 0:
+        n = 7 * int((pg.fixed == 0).sum())
+        out = {"metric": "LM iterations/sec (essential graph, KITTI-00 scale)", "value": world * 1000.0 / ms,
+               "unit": "LM iterations/s", "n_gpus": world, "steps": n_it, "warmup": args.warmup,
+               "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "f64", "data": "synthetic (repo pose-graph generator, seed 5)",
+               "config": {"workload": "essential graph (Sim3, fix-scale)", "n_kf": pg.n_kf, "n_edge": pg.n_edge,
+                          "dims": n, "parallelism": f"replicas x{world}"},
+               "trials_per_step": st["trials"] / max(1, st["iterations"]) if st else None,
+               "chi2_last": st["chi2_end"] if st else None,
+               "roofline": {"bound": "mfma", "kernel": "dense Cholesky (per trial)", "algorithmic_flops": n ** 3 / 3.0,
+                            "peak": MFMA_F64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "achieved": (n ** 3 / 3.0) * (st["trials"] / max(1, st["iterations"])) / (ms * 1e-3) / 1e12,
+                            "note": "whole-iteration time, upper bound on the Cholesky's share"}}
+        out["roofline"]["frac"] = out["roofline"]["achieved"] / MFMA_F64_PEAK_TFLOPS
+        if not args.no_cpu_baseline and world == 1:
+            from oracle import oracle as O
+            O.build()
+            ref = O.OracleEG(pg)
+            t0 = time.perf_counter()
+            nr, _ = ref.optimize(3, 1e-16)
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": nr / dt, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+                                   "sample": f"{nr} LM iterations of the same graph, single thread, {dt:.1f} s"}
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["gba", "lba"], default="gba")
+    ap.add_argument("--config", choices=["gba", "lba", "eg"], default="gba")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink config 4 (parity / debugging only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -157,6 +222,8 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.config == "eg":
+        return bench_eg(args, world)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -168,7 +235,9 @@ def main():
     from sqrtlm.shard import shard
     prob, desc = make_workload(args.config, args.scale)
     local = shard(prob, rank, world)
-    ctx = Context(local_rank if args.comm == "rccl" else 0)
+    # SQLM_BENCH_ONE_GPU=1 puts every rank on GPU 0 (1-GPU rehearsal of the RCCL transport)
+    one_gpu = args.comm == "host" or os.environ.get("SQLM_BENCH_ONE_GPU") == "1"
+    ctx = Context(0 if one_gpu else local_rank)
     if world > 1 and args.comm == "rccl":
         import torch
         from sqrtlm._lib import lib
