@@ -1,0 +1,89 @@
+/*
+ * sqrtlm_orb.h — C ABI of the ORB front-end path of libsqrtlm.so (SURVEY.md
+ * §8 row f3): ORB FAST + steered-BRIEF extraction and Hamming matching on the
+ * GPU, behind the reference's ORBextractor / ORBmatcher interfaces.
+ *
+ * Seam: ORB_SLAM2::ORBextractor::operator()(image, keypoints, descriptors)
+ * (src/frontend/ORBextractor.cc:1284-1399, declared include/frontend/
+ * ORBextractor.h) and ORBmatcher::SearchForInitialization / DescriptorDistance
+ * (src/frontend/ORBmatcher.cc:573-718, :2096-2116). Frame::ExtractORB
+ * (src/data_structure/Frame.cc) calls the extractor once per image; the
+ * adapter replaces that call with sqlm_orb_extract and copies the arrays into
+ * cv::KeyPoint / cv::Mat.
+ *
+ * Contexts come from sqrtlm.h (sqlm_ctx_create); the calls run on the
+ * context's HIP stream. Status codes as in sqrtlm.h.
+ */
+#ifndef SQRTLM_ORB_H
+#define SQRTLM_ORB_H
+
+#include <stdint.h>
+
+#include "sqrtlm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cv::KeyPoint fields the reference uses: pt.x, pt.y, size, angle (degrees,
+ * [0,360)), response (FAST score), octave (pyramid level). */
+typedef struct sqlm_keypoint {
+  float x, y, size, angle, response;
+  int32_t octave;
+} sqlm_keypoint;
+
+/* ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+ * (ORBextractor.cc:474-560; cfg/KITTI00-02.yaml: 2000, 1.2, 8, 20, 7). */
+typedef struct sqlm_orb_params {
+  int32_t nfeatures;
+  float scale_factor;
+  int32_t nlevels;
+  int32_t ini_th_fast;
+  int32_t min_th_fast;
+} sqlm_orb_params;
+
+/* ORBextractor::operator()(image, keypoints, descriptors): 8-bit grey image
+ * (w x h, row stride in bytes, host memory) -> keypoints in level-0
+ * coordinates and 32-byte descriptors, level after level in the reference's
+ * order. Writes at most `cap` entries; *n_out = the full count (> cap means
+ * the arrays were too small: nothing beyond cap is written).
+ * SQLM_ERR_UNSUPPORTED: a pyramid level narrower / shorter than one 30-pixel
+ * cell (the reference divides by zero there) or wider than 4096. */
+int sqlm_orb_extract(sqlm_ctx *ctx, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                     sqlm_keypoint *kps, uint8_t *desc, int cap, int *n_out);
+
+/* The pyramid image of `level` from the last sqlm_orb_extract (ORBextractor::
+ * mvImagePyramid[level], GetImagePyramid) into out [lh][lw]; *lw / *lh its size. */
+int sqlm_orb_get_level(sqlm_ctx *ctx, int level, uint8_t *out, int cap, int *lw, int *lh);
+
+/* Brute-force Hamming matching (DescriptorDistance, ORBmatcher.cc:2096-2116,
+ * over every train descriptor): for each query, the best distance, its first
+ * train index in increasing order (strict <, the reference's tie-breaking)
+ * and the second-best distance (INT_MAX when nt < 2). */
+int sqlm_orb_match_bf(sqlm_ctx *ctx, const uint8_t *query, int nq, const uint8_t *train, int nt, int32_t *best_idx,
+                      int32_t *best_dist, int32_t *second_dist);
+
+/* Frame grid bounds of the second frame (Frame::mnMinX, mnMaxX, mnMinY, mnMaxY). */
+typedef struct sqlm_frame_bounds {
+  float min_x, max_x, min_y, max_y;
+} sqlm_frame_bounds;
+
+/* ORBmatcher(nnratio, check_ori).SearchForInitialization(F1, F2, prev,
+ * matches12, window) (ORBmatcher.cc:573-718): k1/d1 = F1.mvKeysUn /
+ * mDescriptors, k2/d2 = F2's, prev [n1][2] = vbPrevMatched (updated in place),
+ * m12 [n1] = vnMatches12; *n_matches = the return value. */
+int sqlm_orb_search_for_init(sqlm_ctx *ctx, const sqlm_keypoint *k1, const uint8_t *d1, int n1,
+                             const sqlm_keypoint *k2, const uint8_t *d2, int n2, const sqlm_frame_bounds *f2,
+                             float *prev, int32_t *m12, int window, float nnratio, int check_ori, int *n_matches);
+
+/* Bench helper: time `reps` extractions of one image (input uploaded once;
+ * timed region = the whole device pipeline incl. the host quadtree step).
+ * ms_per_frame, and per-stage device milliseconds [6]: pyramid, fast,
+ * compact, blur, describe, host quadtree (wall). */
+int sqlm_orb_bench_extract(sqlm_ctx *ctx, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                           int reps, double *ms_per_frame, double *stage_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,145 @@
+"""TEST INFRASTRUCTURE — ctypes binding of the ORB oracle (oracle/orb_ref.c).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this
+module, as the checker. Parity statement: oracle/orb_ref.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .oracle import _p, lib
+
+# cv::KeyPoint fields the reference uses (orc_kp / sqlm_keypoint layout)
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
+                     ("octave", "<i4")])
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("nfeatures", C.c_int), ("scale_factor", C.c_float), ("nlevels", C.c_int),
+                ("ini_th_fast", C.c_int), ("min_th_fast", C.c_int)]
+
+
+def params(nfeatures=2000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7) -> OrbParams:
+    """cfg/KITTI00-02.yaml ORBextractor block (nFeatures 2000, scaleFactor 1.2, nLevels 8, 20 / 7)."""
+    return OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th)
+
+
+def levels(p, w, h):
+    L = p.nlevels
+    lw, lh, nf = (np.zeros(L, np.int32) for _ in range(3))
+    sc = np.zeros(L, np.float32)
+    r = lib().orc_orb_levels(C.byref(p), w, h, _p(lw), _p(lh), _p(nf), _p(sc))
+    if r:
+        raise ValueError(f"orc_orb_levels: {r}")
+    return lw, lh, nf, sc
+
+
+def resize(src, dw, dh):
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().orc_orb_resize(_p(src), src.shape[1], src.shape[0], src.shape[1], _p(out), dw, dh, dw)
+    return out
+
+
+def blur(src):
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros_like(src)
+    lib().orc_orb_blur(_p(src), src.shape[1], src.shape[0], src.shape[1], _p(out), src.shape[1])
+    return out
+
+
+def gauss_kernel():
+    k = np.zeros(7, np.int32)
+    lib().orc_orb_gauss_kernel(_p(k))
+    return k
+
+
+def fast(img, th, cap=100000):
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros(cap, KP_DTYPE)
+    n = lib().orc_orb_fast(_p(img), img.shape[1], img.shape[1], img.shape[0], th, _p(out), cap)
+    return out[:min(n, cap)]
+
+
+def level_candidates(p, img, cap=400000):
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros(cap, KP_DTYPE)
+    n = lib().orc_orb_level_candidates(C.byref(p), _p(img), img.shape[1], img.shape[0], img.shape[1], _p(out), cap)
+    return out[:min(n, cap)]
+
+
+def distribute(keys, minX, maxX, minY, maxY, N):
+    keys = np.ascontiguousarray(keys, KP_DTYPE)
+    out = np.zeros(max(len(keys), 1), KP_DTYPE)
+    n = lib().orc_orb_distribute(_p(keys), len(keys), minX, maxX, minY, maxY, N, _p(out))
+    return out[:n]
+
+
+def ic_angle(img, x, y):
+    img = np.ascontiguousarray(img, np.uint8)
+    f = lib().orc_orb_ic_angle
+    f.restype = C.c_float
+    return f(_p(img), img.shape[1], C.c_float(x), C.c_float(y))
+
+
+def fast_atan2(y, x):
+    f = lib().orc_fast_atan2
+    f.restype = C.c_float
+    return f(C.c_float(y), C.c_float(x))
+
+
+def describe(img, kp):
+    img = np.ascontiguousarray(img, np.uint8)
+    k = np.ascontiguousarray(np.asarray(kp, KP_DTYPE).reshape(1))
+    d = np.zeros(32, np.uint8)
+    lib().orc_orb_describe(_p(img), img.shape[1], _p(k), _p(d))
+    return d
+
+
+def extract(p, img, cap=100000, with_levels=False):
+    """ORBextractor::operator(): (keypoints KP_DTYPE, descriptors uint8 [n][32][, pyramid levels])."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    lev = None
+    if with_levels:
+        lw, lh, _, _ = levels(p, w, h)
+        lev = np.zeros(int(np.sum(lw.astype(np.int64) * lh)), np.uint8)
+    n = lib().orc_orb_extract(C.byref(p), _p(img), w, h, w, _p(kps), _p(desc), cap, _p(lev))
+    if n < 0:
+        raise ValueError("orc_orb_extract failed")
+    n = min(n, cap)
+    if with_levels:
+        lw, lh, _, _ = levels(p, w, h)
+        offs = np.concatenate([[0], np.cumsum(lw.astype(np.int64) * lh)])
+        pyr = [lev[offs[i]:offs[i + 1]].reshape(lh[i], lw[i]) for i in range(len(lw))]
+        return kps[:n], desc[:n], pyr
+    return kps[:n], desc[:n]
+
+
+def hamming(a, b):
+    a = np.ascontiguousarray(a, np.uint8)
+    b = np.ascontiguousarray(b, np.uint8)
+    return lib().orc_hamming(_p(a), _p(b))
+
+
+class FrameGrid(C.Structure):
+    _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
+
+
+def search_for_init(k1, d1, k2, d2, grid, prev, window=100, nnratio=0.9, check_ori=True):
+    """ORBmatcher(nnratio, check_ori).SearchForInitialization(F1, F2, prev, m12, window)
+    -> (nmatches, m12, updated prev)."""
+    k1 = np.ascontiguousarray(k1, KP_DTYPE)
+    k2 = np.ascontiguousarray(k2, KP_DTYPE)
+    d1 = np.ascontiguousarray(d1, np.uint8)
+    d2 = np.ascontiguousarray(d2, np.uint8)
+    prev = np.ascontiguousarray(prev, np.float32).copy()
+    m12 = np.zeros(len(k1), np.int32)
+    g = FrameGrid(*grid)
+    n = lib().orc_search_for_init(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2), C.byref(g), _p(prev), _p(m12),
+                                  int(window), C.c_float(nnratio), int(bool(check_ori)))
+    return n, m12, prev

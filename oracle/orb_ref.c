@@ -1,0 +1,875 @@
+/* TEST INFRASTRUCTURE — CPU restatement of the reference's ORB front end
+ * (SURVEY.md §8 row f3). See orb_ref.h for scope and the parity statement.
+ * Built with -ffp-contract=off like the reference (-std=c++11 / c++14 is ISO
+ * mode for GCC, which disables FMA contraction; CMakeLists.txt:4,44,50). */
+#include "orb_ref.h"
+
+#include <limits.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "orb_pattern.h"
+
+#define EDGE_THRESHOLD 19 /* ORBextractor.cc:78 */
+#define PATCH_SIZE 31     /* :76 */
+#define HALF_PATCH_SIZE 15
+#define ORC_CV_PI 3.1415926535897932384626433832795 /* CV_PI */
+
+/* OpenCV cvRound / cvFloor / cvCeil on x86-64 (SSE2 cvtss2si: round half to even). */
+static int cv_round(float v) { return (int)lrintf(v); }
+static int cv_roundd(double v) { return (int)lrint(v); }
+static int cv_floor(float v) {
+  int i = (int)v;
+  return i - (i > v);
+}
+
+static int imin(int a, int b) { return a < b ? a : b; }
+static int imax(int a, int b) { return a > b ? a : b; }
+
+/* ---- level geometry (ORBextractor ctor :474-560, ComputePyramid :1224-1282) ---- */
+int orc_orb_levels(const orc_orb_params *p, int cols, int rows, int *lw, int *lh, int *nfeat, float *scale) {
+  const int L = p->nlevels;
+  if (L < 1 || L > ORC_ORB_MAX_LEVELS) return -1;
+  float sf[ORC_ORB_MAX_LEVELS];
+  sf[0] = 1.0f;
+  for (int i = 1; i < L; ++i) sf[i] = sf[i - 1] * p->scale_factor;
+  for (int i = 0; i < L; ++i) {
+    const float inv = 1.0f / sf[i];
+    lw[i] = cv_round((float)cols * inv);
+    lh[i] = cv_round((float)rows * inv);
+    scale[i] = sf[i];
+  }
+  const float factor = 1.0f / p->scale_factor;
+  float nd = p->nfeatures * (1 - factor) / (1 - (float)pow((double)factor, (double)L));
+  int sum = 0;
+  for (int l = 0; l < L - 1; ++l) {
+    nfeat[l] = cv_round(nd);
+    sum += nfeat[l];
+    nd *= factor;
+  }
+  nfeat[L - 1] = imax(p->nfeatures - sum, 0);
+  /* the cell grid needs at least one 30-pixel cell per axis on every level */
+  for (int i = 0; i < L; ++i)
+    if (lw[i] - 2 * (EDGE_THRESHOLD - 3) < 30 || lh[i] - 2 * (EDGE_THRESHOLD - 3) < 30) return -2;
+  return 0;
+}
+
+/* ---- cv::resize INTER_LINEAR, 8U (OpenCV 3.3.1 imgproc/resize.cpp) ----
+ * Coefficients: fx = (float)((dx+0.5)*scale_x - 0.5), sx = cvFloor(fx), short
+ * weights saturate_cast<short>((1-fx)*2048), (fx*2048); x clamped at the
+ * borders (xmax: pure copy S[sx]*2048), rows clipped. Horizontal pass in int.
+ * Vertical pass: SSE2 VResizeLinearVec_32s8u for x below the vector end
+ * (((S0>>4)*b0 >> 16) + ((S1>>4)*b1 >> 16) + 2) >> 2, then the scalar
+ * FixedPtCast (b0*S0 + b1*S1 + 2^21) >> 22 for the tail. */
+static short sat_short(float v) {
+  int r = cv_round(v);
+  return (short)(r < SHRT_MIN ? SHRT_MIN : r > SHRT_MAX ? SHRT_MAX : r);
+}
+static int sat16(int v) { return v < -32768 ? -32768 : v > 32767 ? 32767 : v; }
+static uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
+
+int orc_resize_vec_end(int width) {
+  int x = 0;
+  for (; x <= width - 16; x += 16) {
+  }
+  for (; x < width - 4; x += 4) {
+  }
+  return x;
+}
+
+void orc_orb_resize(const uint8_t *src, int sw, int sh, int sstride, uint8_t *dst, int dw, int dh, int dstride) {
+  const double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+  const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+  int *xofs = (int *)malloc(sizeof(int) * dw);
+  short *ialpha = (short *)malloc(sizeof(short) * 2 * dw);
+  int xmax = dw;
+  for (int dx = 0; dx < dw; ++dx) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cv_floor(fx);
+    fx -= sx;
+    if (sx < 0) fx = 0, sx = 0;
+    if (sx + 1 >= sw) {
+      xmax = imin(xmax, dx);
+      if (sx >= sw - 1) fx = 0, sx = sw - 1;
+    }
+    xofs[dx] = sx;
+    ialpha[2 * dx] = sat_short((1.f - fx) * 2048);
+    ialpha[2 * dx + 1] = sat_short(fx * 2048);
+  }
+  int *r0 = (int *)malloc(sizeof(int) * dw), *r1 = (int *)malloc(sizeof(int) * dw);
+  const int vend = orc_resize_vec_end(dw);
+  for (int dy = 0; dy < dh; ++dy) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cv_floor(fy);
+    fy -= sy;
+    const short b0 = sat_short((1.f - fy) * 2048), b1 = sat_short(fy * 2048);
+    const int y0 = imin(imax(sy, 0), sh - 1), y1 = imin(imax(sy + 1, 0), sh - 1);
+    for (int k = 0; k < 2; ++k) {
+      const uint8_t *S = src + (size_t)(k ? y1 : y0) * sstride;
+      int *D = k ? r1 : r0;
+      for (int dx = 0; dx < dw; ++dx) {
+        const int sx = xofs[dx];
+        D[dx] = dx < xmax ? S[sx] * ialpha[2 * dx] + S[sx + 1] * ialpha[2 * dx + 1] : S[sx] * 2048;
+      }
+    }
+    uint8_t *out = dst + (size_t)dy * dstride;
+    for (int x = 0; x < dw; ++x) {
+      if (x < vend) {
+        const int a = sat16(r0[x] >> 4), c = sat16(r1[x] >> 4);
+        const int m = sat16(((a * b0) >> 16) + ((c * b1) >> 16));
+        out[x] = sat_u8(sat16(m + 2) >> 2);
+      } else {
+        out[x] = sat_u8((r0[x] * b0 + r1[x] * b1 + (1 << 21)) >> 22);
+      }
+    }
+  }
+  free(xofs);
+  free(ialpha);
+  free(r0);
+  free(r1);
+}
+
+/* ---- cv::FAST, TYPE_9_16, nonmax suppression (OpenCV 3.3.1 features2d/fast.cpp) ---- */
+static const int kFastOff[16][2] = {{0, 3},  {1, 3},  {2, 2},  {3, 1},  {3, 0},   {3, -1}, {2, -2}, {1, -3},
+                                    {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+/* cornerScore<16>: the largest threshold for which the pixel stays a corner, minus one. */
+static int corner_score16(const uint8_t *ptr, const int *pixel, int threshold) {
+  const int K = 8, N = K * 3 + 1;
+  int k, v = ptr[0];
+  short d[25];
+  for (k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+  int a0 = threshold;
+  for (k = 0; k < 16; k += 2) {
+    int a = imin((int)d[k + 1], (int)d[k + 2]);
+    a = imin(a, (int)d[k + 3]);
+    if (a <= a0) continue;
+    a = imin(a, (int)d[k + 4]);
+    a = imin(a, (int)d[k + 5]);
+    a = imin(a, (int)d[k + 6]);
+    a = imin(a, (int)d[k + 7]);
+    a = imin(a, (int)d[k + 8]);
+    a0 = imax(a0, imin(a, (int)d[k]));
+    a0 = imax(a0, imin(a, (int)d[k + 9]));
+  }
+  int b0 = -a0;
+  for (k = 0; k < 16; k += 2) {
+    int b = imax((int)d[k + 1], (int)d[k + 2]);
+    b = imax(b, (int)d[k + 3]);
+    b = imax(b, (int)d[k + 4]);
+    b = imax(b, (int)d[k + 5]);
+    if (b >= b0) continue;
+    b = imax(b, (int)d[k + 6]);
+    b = imax(b, (int)d[k + 7]);
+    b = imax(b, (int)d[k + 8]);
+    b0 = imin(b0, imax(b, (int)d[k]));
+    b0 = imin(b0, imax(b, (int)d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+int orc_orb_fast(const uint8_t *img, int stride, int w, int h, int threshold, orc_kp *out, int cap) {
+  const int K = 8, N = 16 + K + 1;
+  int pixel[25];
+  for (int k = 0; k < 16; ++k) pixel[k] = kFastOff[k][0] + kFastOff[k][1] * stride;
+  for (int k = 16; k < 25; ++k) pixel[k] = pixel[k - 16];
+  threshold = imin(imax(threshold, 0), 255);
+  uint8_t tab[512];
+  for (int i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+  uint8_t *buf[3];
+  int *cpbuf[3];
+  uint8_t *bmem = (uint8_t *)calloc((size_t)3 * w + 1, 1);
+  int *cmem = (int *)calloc((size_t)3 * (w + 1), sizeof(int));
+  for (int b = 0; b < 3; ++b) {
+    buf[b] = bmem + (size_t)b * w;
+    cpbuf[b] = cmem + (size_t)b * (w + 1) + 1;
+  }
+  int n = 0;
+  for (int i = 3; i < h - 2; i++) {
+    const uint8_t *ptr = img + (size_t)i * stride + 3;
+    uint8_t *curr = buf[(i - 3) % 3];
+    int *cornerpos = cpbuf[(i - 3) % 3];
+    memset(curr, 0, w);
+    int ncorners = 0;
+    if (i < h - 3) {
+      for (int j = 3; j < w - 3; j++, ptr++) {
+        const int v = ptr[0];
+        const uint8_t *t = &tab[0] - v + 255;
+        int d = t[ptr[pixel[0]]] | t[ptr[pixel[8]]];
+        if (d == 0) continue;
+        d &= t[ptr[pixel[2]]] | t[ptr[pixel[10]]];
+        d &= t[ptr[pixel[4]]] | t[ptr[pixel[12]]];
+        d &= t[ptr[pixel[6]]] | t[ptr[pixel[14]]];
+        if (d == 0) continue;
+        d &= t[ptr[pixel[1]]] | t[ptr[pixel[9]]];
+        d &= t[ptr[pixel[3]]] | t[ptr[pixel[11]]];
+        d &= t[ptr[pixel[5]]] | t[ptr[pixel[13]]];
+        d &= t[ptr[pixel[7]]] | t[ptr[pixel[15]]];
+        if (d & 1) {
+          const int vt = v - threshold;
+          int count = 0;
+          for (int k = 0; k < N; k++) {
+            const int x = ptr[pixel[k]];
+            if (x < vt) {
+              if (++count > K) {
+                cornerpos[ncorners++] = j;
+                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                break;
+              }
+            } else
+              count = 0;
+          }
+        }
+        if (d & 2) {
+          const int vt = v + threshold;
+          int count = 0;
+          for (int k = 0; k < N; k++) {
+            const int x = ptr[pixel[k]];
+            if (x > vt) {
+              if (++count > K) {
+                cornerpos[ncorners++] = j;
+                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                break;
+              }
+            } else
+              count = 0;
+          }
+        }
+      }
+    }
+    cornerpos[-1] = ncorners;
+    if (i == 3) continue;
+    const uint8_t *prev = buf[(i - 4 + 3) % 3];
+    const uint8_t *pprev = buf[(i - 5 + 3) % 3];
+    cornerpos = cpbuf[(i - 4 + 3) % 3];
+    ncorners = cornerpos[-1];
+    for (int k = 0; k < ncorners; k++) {
+      const int j = cornerpos[k];
+      const int score = prev[j];
+      if (score > prev[j + 1] && score > prev[j - 1] && score > pprev[j - 1] && score > pprev[j] &&
+          score > pprev[j + 1] && score > curr[j - 1] && score > curr[j] && score > curr[j + 1]) {
+        if (n < cap) {
+          out[n].x = (float)j;
+          out[n].y = (float)(i - 1);
+          out[n].size = 7.f;
+          out[n].angle = -1.f;
+          out[n].response = (float)score;
+          out[n].octave = 0;
+        }
+        ++n;
+      }
+    }
+  }
+  free(bmem);
+  free(cmem);
+  return n;
+}
+
+/* ComputeKeyPointsOctTree cell loop (ORBextractor.cc:1045-1135): FAST with
+ * iniThFAST on each 30-px cell (+6 overlap), minThFAST when the cell is empty. */
+int orc_orb_level_candidates(const orc_orb_params *p, const uint8_t *img, int cols, int rows, int stride,
+                             orc_kp *out, int cap) {
+  const float W = 30;
+  const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+  const int maxBorderX = cols - EDGE_THRESHOLD + 3, maxBorderY = rows - EDGE_THRESHOLD + 3;
+  const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+  const int nCols = (int)(width / W), nRows = (int)(height / W);
+  const int wCell = (int)ceilf(width / nCols), hCell = (int)ceilf(height / nRows);
+  int n = 0;
+  orc_kp *cell = (orc_kp *)malloc(sizeof(orc_kp) * 4096);
+  for (int i = 0; i < nRows; i++) {
+    const float iniY = (float)(minBorderY + i * hCell);
+    float maxY = iniY + hCell + 6;
+    if (iniY >= maxBorderY - 3) continue;
+    if (maxY > maxBorderY) maxY = (float)maxBorderY;
+    for (int j = 0; j < nCols; j++) {
+      const float iniX = (float)(minBorderX + j * wCell);
+      float maxX = iniX + wCell + 6;
+      if (iniX >= maxBorderX - 3) continue;
+      if (maxX > maxBorderX) maxX = (float)maxBorderX;
+      const uint8_t *view = img + (size_t)(int)iniY * stride + (int)iniX;
+      const int vw = (int)maxX - (int)iniX, vh = (int)maxY - (int)iniY;
+      int c = orc_orb_fast(view, stride, vw, vh, p->ini_th_fast, cell, 4096);
+      if (c == 0) c = orc_orb_fast(view, stride, vw, vh, p->min_th_fast, cell, 4096);
+      if (c > 4096) c = 4096;
+      for (int k = 0; k < c; ++k) {
+        orc_kp kp = cell[k];
+        kp.x += j * wCell;
+        kp.y += i * hCell;
+        if (n < cap) out[n] = kp;
+        ++n;
+      }
+    }
+  }
+  free(cell);
+  return n;
+}
+
+/* ---- DistributeOctTree (ORBextractor.cc:606-1043) ---- */
+typedef struct onode {
+  int ulx, uly, urx, ury, blx, bly, brx, bry;
+  orc_kp *keys;
+  int nkeys;
+  int nomore;
+  struct onode *prev, *next;
+} onode;
+
+typedef struct olist {
+  onode *head;
+  int size;
+  onode **pool;
+  int npool, cpool;
+} olist;
+
+static onode *onode_new(olist *L, int cap) {
+  onode *n = (onode *)calloc(1, sizeof(onode));
+  n->keys = (orc_kp *)malloc(sizeof(orc_kp) * (cap > 0 ? cap : 1));
+  if (L->npool == L->cpool) {
+    L->cpool = L->cpool ? 2 * L->cpool : 64;
+    L->pool = (onode **)realloc(L->pool, sizeof(onode *) * L->cpool);
+  }
+  L->pool[L->npool++] = n;
+  return n;
+}
+static void olist_push_front(olist *L, onode *n) {
+  n->prev = NULL;
+  n->next = L->head;
+  if (L->head) L->head->prev = n;
+  L->head = n;
+  L->size++;
+}
+static onode *olist_erase(olist *L, onode *n) {
+  onode *nx = n->next;
+  if (n->prev) n->prev->next = nx;
+  else L->head = nx;
+  if (nx) nx->prev = n->prev;
+  L->size--;
+  return nx;
+}
+
+/* ExtractorNode::DivideNode (:606-690) */
+static void divide_node(olist *L, const onode *p, onode **c) {
+  const int halfX = (int)ceilf((float)(p->urx - p->ulx) / 2);
+  const int halfY = (int)ceilf((float)(p->bry - p->uly) / 2);
+  for (int k = 0; k < 4; ++k) c[k] = onode_new(L, p->nkeys);
+  c[0]->ulx = p->ulx; c[0]->uly = p->uly;
+  c[0]->urx = p->ulx + halfX; c[0]->ury = p->uly;
+  c[0]->blx = p->ulx; c[0]->bly = p->uly + halfY;
+  c[0]->brx = p->ulx + halfX; c[0]->bry = p->uly + halfY;
+  c[1]->ulx = c[0]->urx; c[1]->uly = c[0]->ury;
+  c[1]->urx = p->urx; c[1]->ury = p->ury;
+  c[1]->blx = c[0]->brx; c[1]->bly = c[0]->bry;
+  c[1]->brx = p->urx; c[1]->bry = p->uly + halfY;
+  c[2]->ulx = c[0]->blx; c[2]->uly = c[0]->bly;
+  c[2]->urx = c[0]->brx; c[2]->ury = c[0]->bry;
+  c[2]->blx = p->blx; c[2]->bly = p->bly;
+  c[2]->brx = c[0]->brx; c[2]->bry = p->bly;
+  c[3]->ulx = c[2]->urx; c[3]->uly = c[2]->ury;
+  c[3]->urx = c[1]->brx; c[3]->ury = c[1]->bry;
+  c[3]->blx = c[2]->brx; c[3]->bly = c[2]->bry;
+  c[3]->brx = p->brx; c[3]->bry = p->bry;
+  for (int i = 0; i < p->nkeys; ++i) {
+    const orc_kp *kp = &p->keys[i];
+    int t;
+    if (kp->x < c[0]->urx) t = kp->y < c[0]->bry ? 0 : 2;
+    else t = kp->y < c[0]->bry ? 1 : 3;
+    c[t]->keys[c[t]->nkeys++] = *kp;
+  }
+  for (int k = 0; k < 4; ++k)
+    if (c[k]->nkeys == 1) c[k]->nomore = 1;
+}
+
+typedef struct {
+  int size;
+  onode *node;
+} size_node;
+
+/* stable ascending sort by size (std::stable_sort in :900-906) */
+static void stable_sort_sizes(size_node *v, int n) {
+  for (int i = 1; i < n; ++i) {
+    size_node x = v[i];
+    int j = i - 1;
+    while (j >= 0 && v[j].size > x.size) {
+      v[j + 1] = v[j];
+      --j;
+    }
+    v[j + 1] = x;
+  }
+}
+
+int orc_orb_distribute(const orc_kp *keys, int n, int minX, int maxX, int minY, int maxY, int N, orc_kp *out) {
+  const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
+  const float hX = (float)(maxX - minX) / nIni;
+  olist L = {0};
+  onode **ini = (onode **)malloc(sizeof(onode *) * (nIni > 0 ? nIni : 1));
+  /* lNodes.push_back in order: build back to front with push_front */
+  for (int i = 0; i < nIni; i++) {
+    onode *ni = onode_new(&L, n);
+    ni->ulx = (int)(hX * (float)i); ni->uly = 0;
+    ni->urx = (int)(hX * (float)(i + 1)); ni->ury = 0;
+    ni->blx = ni->ulx; ni->bly = maxY - minY;
+    ni->brx = ni->urx; ni->bry = maxY - minY;
+    ini[i] = ni;
+  }
+  for (int i = nIni - 1; i >= 0; --i) olist_push_front(&L, ini[i]);
+  for (int i = 0; i < n; i++) {
+    onode *t = ini[(size_t)(keys[i].x / hX)];
+    t->keys[t->nkeys++] = keys[i];
+  }
+  for (onode *it = L.head; it;) {
+    if (it->nkeys == 1) {
+      it->nomore = 1;
+      it = it->next;
+    } else if (it->nkeys == 0) it = olist_erase(&L, it);
+    else it = it->next;
+  }
+  int cap_sz = 1024;
+  size_node *vs = (size_node *)malloc(sizeof(size_node) * cap_sz);
+  size_node *vp = (size_node *)malloc(sizeof(size_node) * cap_sz);
+  int nvs = 0;
+#define PUSH_SZ(cnt, nd)                                                     \
+  do {                                                                            \
+    if (cnt == cap_sz) {                                                          \
+      cap_sz *= 2;                                                                \
+      vs = (size_node *)realloc(vs, sizeof(size_node) * cap_sz);                  \
+      vp = (size_node *)realloc(vp, sizeof(size_node) * cap_sz);                  \
+    }                                                                             \
+    vs[cnt].size = (nd)->nkeys;                                                   \
+    vs[cnt].node = (nd);                                                          \
+    cnt++;                                                                        \
+  } while (0)
+  int bFinish = 0;
+  while (!bFinish) {
+    int prevSize = L.size;
+    int nToExpand = 0;
+    nvs = 0;
+    for (onode *it = L.head; it;) {
+      if (it->nomore) {
+        it = it->next;
+        continue;
+      }
+      onode *c[4];
+      divide_node(&L, it, c);
+      for (int k = 0; k < 4; ++k) {
+        if (c[k]->nkeys > 0) {
+          olist_push_front(&L, c[k]);
+          if (c[k]->nkeys > 1) {
+            nToExpand++;
+            PUSH_SZ(nvs, c[k]);
+          }
+        }
+      }
+      it = olist_erase(&L, it);
+    }
+    if (L.size >= N || L.size == prevSize) {
+      bFinish = 1;
+    } else if ((L.size + nToExpand * 3) > N) {
+      while (!bFinish) {
+        prevSize = L.size;
+        const int nprev = nvs;
+        memcpy(vp, vs, sizeof(size_node) * nprev);
+        nvs = 0;
+        stable_sort_sizes(vp, nprev);
+        for (int j = nprev - 1; j >= 0; j--) {
+          onode *c[4];
+          divide_node(&L, vp[j].node, c);
+          for (int k = 0; k < 4; ++k) {
+            if (c[k]->nkeys > 0) {
+              olist_push_front(&L, c[k]);
+              if (c[k]->nkeys > 1) PUSH_SZ(nvs, c[k]);
+            }
+          }
+          olist_erase(&L, vp[j].node);
+          if (L.size >= N) break;
+        }
+        if (L.size >= N || L.size == prevSize) bFinish = 1;
+      }
+    }
+  }
+#undef PUSH_SZ
+  int nout = 0;
+  for (onode *it = L.head; it; it = it->next) {
+    const orc_kp *best = &it->keys[0];
+    float maxResponse = best->response;
+    for (int k = 1; k < it->nkeys; k++)
+      if (it->keys[k].response > maxResponse) {
+        best = &it->keys[k];
+        maxResponse = it->keys[k].response;
+      }
+    out[nout++] = *best;
+  }
+  for (int i = 0; i < L.npool; ++i) {
+    free(L.pool[i]->keys);
+    free(L.pool[i]);
+  }
+  free(L.pool);
+  free(ini);
+  free(vs);
+  free(vp);
+  return nout;
+}
+
+/* ---- cv::GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101), 8U (OpenCV 3.3.1) ----
+ * getGaussianKernel(7, 2, CV_32F): t_i = exp(-0.5/4 x_i^2) rounded to float,
+ * normalised in double, rounded to float; the 8U path converts both kernels to
+ * int (x256, cvRound). Row pass: exact int sums. Column pass: SSE2
+ * SymmColumnVec_32s8u (float kernel k/65536, s = k0*R0; s += k_k*(R+k + R-k);
+ * round half even) for x below width & ~3, scalar (s + 2^15) >> 16 after. */
+void orc_orb_gauss_kernel(int ik[7]) {
+  const double scale2X = -0.5 / (2.0 * 2.0);
+  float cf[7];
+  double sum = 0;
+  for (int i = 0; i < 7; i++) {
+    const double x = i - (7 - 1) * 0.5;
+    const double t = exp(scale2X * x * x);
+    cf[i] = (float)t;
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 7; i++) {
+    cf[i] = (float)(cf[i] * sum);
+    ik[i] = cv_round(cf[i] * 256.0f);
+  }
+}
+
+static int refl101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+
+void orc_orb_blur(const uint8_t *src, int w, int h, int sstride, uint8_t *dst, int dstride) {
+  int ik[7];
+  orc_orb_gauss_kernel(ik);
+  float fk[4];
+  for (int k = 0; k < 4; ++k) fk[k] = (float)((double)ik[3 + k] / 65536.0);
+  int *R = (int *)malloc(sizeof(int) * (size_t)w * h);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      int s = 0;
+      for (int i = 0; i < 7; ++i) s += ik[i] * src[(size_t)y * sstride + refl101(x + i - 3, w)];
+      R[(size_t)y * w + x] = s;
+    }
+  const int vend = w & ~3;
+  for (int y = 0; y < h; ++y) {
+    const int *rows[7];
+    for (int k = -3; k <= 3; ++k) rows[k + 3] = R + (size_t)refl101(y + k, h) * w;
+    for (int x = 0; x < w; ++x) {
+      int v;
+      if (x < vend) {
+        float s = (float)rows[3][x] * fk[0];
+        s = s + 0.0f;
+        for (int k = 1; k <= 3; ++k) s = s + (float)(rows[3 + k][x] + rows[3 - k][x]) * fk[k];
+        v = (int)lrintf(s);
+        v = sat16(v);
+      } else {
+        int s = ik[3] * rows[3][x];
+        for (int k = 1; k <= 3; ++k) s += ik[3 + k] * (rows[3 + k][x] + rows[3 - k][x]);
+        v = (s + (1 << 15)) >> 16;
+      }
+      dst[(size_t)y * dstride + x] = sat_u8(v);
+    }
+  }
+  free(R);
+}
+
+/* ---- IC_Angle (:92-141) with OpenCV's fastAtan2 (core/mathfuncs_core) ---- */
+static void orb_umax(int umax[HALF_PATCH_SIZE + 1]) {
+  int v, v0, vmax = (int)floorf(HALF_PATCH_SIZE * sqrtf(2.f) / 2 + 1);
+  int vmin = (int)ceilf(HALF_PATCH_SIZE * sqrtf(2.f) / 2);
+  const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+  for (v = 0; v <= vmax; ++v) umax[v] = cv_roundd(sqrt(hp2 - v * v));
+  for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+    while (umax[v0] == umax[v0 + 1]) ++v0;
+    umax[v] = v0;
+    ++v0;
+  }
+}
+
+float orc_fast_atan2(float y, float x) {
+  const float p1 = 0.9997878412794807f * (float)(180 / ORC_CV_PI);
+  const float p3 = -0.3258083974640975f * (float)(180 / ORC_CV_PI);
+  const float p5 = 0.1555786518463281f * (float)(180 / ORC_CV_PI);
+  const float p7 = -0.04432655554792128f * (float)(180 / ORC_CV_PI);
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+float orc_orb_ic_angle(const uint8_t *image, int step, float px, float py) {
+  int umax[HALF_PATCH_SIZE + 1];
+  orb_umax(umax);
+  int m_01 = 0, m_10 = 0;
+  const uint8_t *center = image + (size_t)cv_round(py) * step + cv_round(px);
+  for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * center[u];
+  for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+    int v_sum = 0;
+    const int d = umax[v];
+    for (int u = -d; u <= d; ++u) {
+      const int val_plus = center[u + v * step], val_minus = center[u - v * step];
+      v_sum += (val_plus - val_minus);
+      m_10 += u * (val_plus + val_minus);
+    }
+    m_01 += v * v_sum;
+  }
+  return orc_fast_atan2((float)m_01, (float)m_10);
+}
+
+/* computeOrbDescriptor (:155-206). cos / sin: the double functions rounded to
+ * float (the correctly rounded cosf/sinf; the reference's glibc cosf agrees
+ * except where its < 1 ulp error bound is not correctly rounded). */
+void orc_orb_describe(const uint8_t *img, int step, const orc_kp *kpt, uint8_t *desc) {
+  const float factorPI = (float)(ORC_CV_PI / 180.f);
+  const float angle = (float)kpt->angle * factorPI;
+  const float a = (float)cos((double)angle), b = (float)sin((double)angle);
+  const uint8_t *center = img + (size_t)cv_round(kpt->y) * step + cv_round(kpt->x);
+  const signed char *pattern = kOrbPattern;
+#define GET_VALUE(idx)                                                                                        \
+  center[cv_round((float)pattern[2 * (idx)] * b + (float)pattern[2 * (idx) + 1] * a) * step +               \
+         cv_round((float)pattern[2 * (idx)] * a - (float)pattern[2 * (idx) + 1] * b)]
+  for (int i = 0; i < 32; ++i, pattern += 32) {
+    int val = 0;
+    for (int bit = 0; bit < 8; ++bit) {
+      const int t0 = GET_VALUE(2 * bit), t1 = GET_VALUE(2 * bit + 1);
+      val |= (t0 < t1) << bit;
+    }
+    desc[i] = (uint8_t)val;
+  }
+#undef GET_VALUE
+}
+
+/* ---- ORBextractor::operator() (:1284-1399) ---- */
+int orc_orb_extract(const orc_orb_params *p, const uint8_t *img, int w, int h, int stride, orc_kp *kps,
+                    uint8_t *desc, int cap, uint8_t *levels_out) {
+  int lw[ORC_ORB_MAX_LEVELS], lh[ORC_ORB_MAX_LEVELS], nf[ORC_ORB_MAX_LEVELS];
+  float sc[ORC_ORB_MAX_LEVELS];
+  if (orc_orb_levels(p, w, h, lw, lh, nf, sc)) return -1;
+  const int L = p->nlevels;
+  uint8_t *lev[ORC_ORB_MAX_LEVELS];
+  for (int l = 0; l < L; ++l) {
+    lev[l] = (uint8_t *)malloc((size_t)lw[l] * lh[l]);
+    if (l == 0)
+      for (int y = 0; y < h; ++y) memcpy(lev[0] + (size_t)y * w, img + (size_t)y * stride, w);
+    else
+      orc_orb_resize(lev[l - 1], lw[l - 1], lh[l - 1], lw[l - 1], lev[l], lw[l], lh[l], lw[l]);
+  }
+  int umax[HALF_PATCH_SIZE + 1];
+  orb_umax(umax);
+  (void)umax;
+  int total = 0;
+  const int border = EDGE_THRESHOLD - 3;
+  orc_kp *cand = (orc_kp *)malloc(sizeof(orc_kp) * 200000);
+  orc_kp *sel = (orc_kp *)malloc(sizeof(orc_kp) * 200000);
+  uint8_t *blur = (uint8_t *)malloc((size_t)w * h);
+  for (int l = 0; l < L; ++l) {
+    int nc = orc_orb_level_candidates(p, lev[l], lw[l], lh[l], lw[l], cand, 200000);
+    if (nc > 200000) nc = 200000;
+    const int ns = orc_orb_distribute(cand, nc, border, lw[l] - EDGE_THRESHOLD + 3, border,
+                                      lh[l] - EDGE_THRESHOLD + 3, nf[l], sel);
+    const int scaledPatchSize = (int)(PATCH_SIZE * sc[l]);
+    for (int i = 0; i < ns; ++i) {
+      sel[i].x += border;
+      sel[i].y += border;
+      sel[i].octave = l;
+      sel[i].size = (float)scaledPatchSize;
+      sel[i].angle = orc_orb_ic_angle(lev[l], lw[l], sel[i].x, sel[i].y);
+    }
+    if (ns > 0) orc_orb_blur(lev[l], lw[l], lh[l], lw[l], blur, lw[l]);
+    for (int i = 0; i < ns; ++i) {
+      if (total + i < cap) orc_orb_describe(blur, lw[l], &sel[i], desc + (size_t)32 * (total + i));
+      if (l != 0) {
+        sel[i].x *= sc[l];
+        sel[i].y *= sc[l];
+      }
+      if (total + i < cap) kps[total + i] = sel[i];
+    }
+    total += ns;
+  }
+  if (levels_out) {
+    size_t off = 0;
+    for (int l = 0; l < L; ++l) {
+      memcpy(levels_out + off, lev[l], (size_t)lw[l] * lh[l]);
+      off += (size_t)lw[l] * lh[l];
+    }
+  }
+  for (int l = 0; l < L; ++l) free(lev[l]);
+  free(cand);
+  free(sel);
+  free(blur);
+  return total;
+}
+
+/* ---- ORBmatcher ---- */
+int orc_hamming(const uint8_t *a8, const uint8_t *b8) {
+  int dist = 0;
+  for (int i = 0; i < 8; i++) {
+    uint32_t pa, pb;
+    memcpy(&pa, a8 + 4 * i, 4);
+    memcpy(&pb, b8 + 4 * i, 4);
+    unsigned int v = pa ^ pb;
+    v = v - ((v >> 1) & 0x55555555);
+    v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+    dist += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+  }
+  return dist;
+}
+
+#define GRID_COLS 64
+#define GRID_ROWS 48
+#define HISTO_LENGTH 30
+#define TH_LOW 50
+
+/* PosInGrid (Frame.cc:1554-1565): std::round of float. */
+static int pos_in_grid(const orc_frame_grid *g, const orc_kp *kp, int *px, int *py) {
+  const float wi = (float)GRID_COLS / (g->max_x - g->min_x), hi = (float)GRID_ROWS / (g->max_y - g->min_y);
+  *px = (int)roundf((kp->x - g->min_x) * wi);
+  *py = (int)roundf((kp->y - g->min_y) * hi);
+  return !(*px < 0 || *px >= GRID_COLS || *py < 0 || *py >= GRID_ROWS);
+}
+
+int orc_search_for_init(const orc_kp *k1, const uint8_t *d1, int n1, const orc_kp *k2, const uint8_t *d2, int n2,
+                        const orc_frame_grid *g2, float *prev, int *m12, int window, float nnratio, int check_ori) {
+  /* AssignFeaturesToGrid (Frame.cc:1268-1285): cell lists in keypoint order */
+  int *cnt = (int *)calloc(GRID_COLS * GRID_ROWS + 1, sizeof(int));
+  int *cell = (int *)malloc(sizeof(int) * (n2 > 0 ? n2 : 1));
+  for (int i = 0; i < n2; ++i) {
+    int px, py;
+    cell[i] = pos_in_grid(g2, &k2[i], &px, &py) ? px * GRID_ROWS + py : -1;
+    if (cell[i] >= 0) cnt[cell[i] + 1]++;
+  }
+  for (int c = 0; c < GRID_COLS * GRID_ROWS; ++c) cnt[c + 1] += cnt[c];
+  int *fill = (int *)malloc(sizeof(int) * (GRID_COLS * GRID_ROWS));
+  memcpy(fill, cnt, sizeof(int) * GRID_COLS * GRID_ROWS);
+  int *lst = (int *)malloc(sizeof(int) * (n2 > 0 ? n2 : 1));
+  for (int i = 0; i < n2; ++i)
+    if (cell[i] >= 0) lst[fill[cell[i]]++] = i;
+  const float wi = (float)GRID_COLS / (g2->max_x - g2->min_x), hi = (float)GRID_ROWS / (g2->max_y - g2->min_y);
+
+  int nmatches = 0;
+  for (int i = 0; i < n1; ++i) m12[i] = -1;
+  int *rot = (int *)malloc(sizeof(int) * (n1 > 0 ? n1 : 1));
+  int *rotbin = (int *)malloc(sizeof(int) * (n1 > 0 ? n1 : 1));
+  int hist[HISTO_LENGTH] = {0};
+  int nrot = 0;
+  const float factor = HISTO_LENGTH / 360.0f;
+  int *vMatchedDistance = (int *)malloc(sizeof(int) * (n2 > 0 ? n2 : 1));
+  int *vnMatches21 = (int *)malloc(sizeof(int) * (n2 > 0 ? n2 : 1));
+  for (int i = 0; i < n2; ++i) {
+    vMatchedDistance[i] = INT_MAX;
+    vnMatches21[i] = -1;
+  }
+  for (int i1 = 0; i1 < n1; i1++) {
+    const int level1 = k1[i1].octave;
+    if (level1 > 0) continue;
+    /* GetFeaturesInArea(prev.x, prev.y, window, level1, level1) (Frame.cc:1463-1552) */
+    const float x = prev[2 * i1], y = prev[2 * i1 + 1], r = (float)window;
+    const int nMinCellX = imax(0, (int)floorf((x - g2->min_x - r) * wi));
+    if (nMinCellX >= GRID_COLS) continue;
+    const int nMaxCellX = imin(GRID_COLS - 1, (int)ceilf((x - g2->min_x + r) * wi));
+    if (nMaxCellX < 0) continue;
+    const int nMinCellY = imax(0, (int)floorf((y - g2->min_y - r) * hi));
+    if (nMinCellY >= GRID_ROWS) continue;
+    const int nMaxCellY = imin(GRID_ROWS - 1, (int)ceilf((y - g2->min_y + r) * hi));
+    if (nMaxCellY < 0) continue;
+    const int bCheckLevels = (level1 > 0) || (level1 >= 0);
+    int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1, any = 0;
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+      for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+        const int c = ix * GRID_ROWS + iy;
+        for (int q = cnt[c]; q < cnt[c + 1]; ++q) {
+          const int i2 = lst[q];
+          const orc_kp *kpUn = &k2[i2];
+          if (bCheckLevels) {
+            if (kpUn->octave < level1) continue;
+            if (level1 >= 0 && kpUn->octave > level1) continue;
+          }
+          const float distx = kpUn->x - x, disty = kpUn->y - y;
+          if (!(fabsf(distx) < r && fabsf(disty) < r)) continue;
+          any = 1;
+          /* ORBmatcher.cc:620-641 */
+          const int dist = orc_hamming(d1 + 32 * (size_t)i1, d2 + 32 * (size_t)i2);
+          if (vMatchedDistance[i2] <= dist) continue;
+          if (dist < bestDist) {
+            bestDist2 = bestDist;
+            bestDist = dist;
+            bestIdx2 = i2;
+          } else if (dist < bestDist2) {
+            bestDist2 = dist;
+          }
+        }
+      }
+    if (!any) continue;
+    if (bestDist <= TH_LOW) {
+      if (bestDist < (float)bestDist2 * nnratio) {
+        if (vnMatches21[bestIdx2] >= 0) {
+          m12[vnMatches21[bestIdx2]] = -1;
+          nmatches--;
+        }
+        m12[i1] = bestIdx2;
+        vnMatches21[bestIdx2] = i1;
+        vMatchedDistance[bestIdx2] = bestDist;
+        nmatches++;
+        if (check_ori) {
+          float rr = k1[i1].angle - k2[bestIdx2].angle;
+          if (rr < 0.0) rr += 360.0f;
+          int bin = (int)roundf(rr * factor);
+          if (bin == HISTO_LENGTH) bin = 0;
+          rot[nrot] = i1;
+          rotbin[nrot] = bin;
+          nrot++;
+          hist[bin]++;
+        }
+      }
+    }
+  }
+  if (check_ori) {
+    /* ComputeThreeMaxima (ORBmatcher.cc:2048-2090) */
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      const int s = hist[i];
+      if (s > max1) {
+        max3 = max2; max2 = max1; max1 = s;
+        ind3 = ind2; ind2 = ind1; ind1 = i;
+      } else if (s > max2) {
+        max3 = max2; max2 = s;
+        ind3 = ind2; ind2 = i;
+      } else if (s > max3) {
+        max3 = s;
+        ind3 = i;
+      }
+    }
+    if (max2 < 0.1f * (float)max1) {
+      ind2 = -1;
+      ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+      ind3 = -1;
+    }
+    for (int q = 0; q < nrot; ++q) {
+      const int b = rotbin[q];
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      if (m12[rot[q]] >= 0) {
+        m12[rot[q]] = -1;
+        nmatches--;
+      }
+    }
+  }
+  for (int i1 = 0; i1 < n1; i1++)
+    if (m12[i1] >= 0) {
+      prev[2 * i1] = k2[m12[i1]].x;
+      prev[2 * i1 + 1] = k2[m12[i1]].y;
+    }
+  free(cnt); free(cell); free(fill); free(lst); free(rot); free(rotbin); free(vMatchedDistance); free(vnMatches21);
+  return nmatches;
+}

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/sqrtlm.h"
+#include "../../include/sqrtlm_orb.h"
 #include "se3_dev.h"
 #include "sqlm_comm.h"
 #include "sqlm_internal.h"
@@ -78,6 +79,7 @@ struct sqlm_ctx {
   Comm comm;
   // ---- essential graph (sqlm_eg.hip) ----
   EGSolver *eg = nullptr;
+  OrbEngine *orb = nullptr;
   // ---- timing ----
   hipEvent_t ev[2 * SQLM_NKERNEL_TIMERS] = {};
   bool timing = false;
@@ -864,6 +866,7 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   comm_destroy(c->comm);
   if (c->eg) eg_destroy(c->eg);
+  if (c->orb) orb_destroy(c->orb);
   for (auto &b : c->bufs)
     if (b.p) (void)hipFree(b.p);
   for (auto &e : c->ev)
@@ -1144,6 +1147,45 @@ int sqlm_debug_tile_profile(long long *out) { return sqlm::tile_profile_read(out
 
 const char *sqlm_kernel_timer_name(int i) {
   return (i >= 0 && i < SQLM_NKERNEL_TIMERS) ? kTimerNames[i] : "";
+}
+
+// ---- ORB front end (include/sqrtlm_orb.h) ----
+static int orb_engine(sqlm_ctx *c) {
+  if (!c) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  if (!c->orb && !(c->orb = orb_create(c->stream))) return SQLM_ERR_OOM;
+  return SQLM_OK;
+}
+
+int sqlm_orb_extract(sqlm_ctx *c, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                     sqlm_keypoint *kps, uint8_t *desc, int cap, int *n_out) {
+  if (int r = orb_engine(c)) return r;
+  return orb_extract(c->orb, p, image, w, h, stride, kps, desc, cap, n_out);
+}
+
+int sqlm_orb_get_level(sqlm_ctx *c, int level, uint8_t *out, int cap, int *lw, int *lh) {
+  if (!c || !c->orb) return SQLM_ERR_STATE;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  return orb_get_level(c->orb, level, out, cap, lw, lh);
+}
+
+int sqlm_orb_match_bf(sqlm_ctx *c, const uint8_t *query, int nq, const uint8_t *train, int nt, int32_t *best_idx,
+                      int32_t *best_dist, int32_t *second_dist) {
+  if (int r = orb_engine(c)) return r;
+  return orb_match_bf(c->orb, query, nq, train, nt, best_idx, best_dist, second_dist);
+}
+
+int sqlm_orb_search_for_init(sqlm_ctx *c, const sqlm_keypoint *k1, const uint8_t *d1, int n1, const sqlm_keypoint *k2,
+                             const uint8_t *d2, int n2, const sqlm_frame_bounds *f2, float *prev, int32_t *m12,
+                             int window, float nnratio, int check_ori, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_for_init(c->orb, k1, d1, n1, k2, d2, n2, f2, prev, m12, window, nnratio, check_ori, n_matches);
+}
+
+int sqlm_orb_bench_extract(sqlm_ctx *c, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                           int reps, double *ms_per_frame, double *stage_ms) {
+  if (int r = orb_engine(c)) return r;
+  return orb_bench_extract(c->orb, p, image, w, h, stride, reps, ms_per_frame, stage_ms);
 }
 
 }  // extern "C"

@@ -174,4 +174,20 @@ int eg_optimize(EGSolver *s, int iterations, double user_lambda, const volatile 
 int eg_get_poses(const EGSolver *s, double *Siw);
 int eg_get_edge_chi2(const EGSolver *s, double *chi2);
 
+// ORB front end (sqlm_orb.hip): one engine per context, on the context's stream.
+struct OrbEngine;
+OrbEngine *orb_create(hipStream_t st);
+void orb_destroy(OrbEngine *e);
+int orb_extract(OrbEngine *e, const struct sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                struct sqlm_keypoint *kps, uint8_t *desc, int cap, int *n_out);
+int orb_get_level(OrbEngine *e, int level, uint8_t *out, int cap, int *w, int *h);
+int orb_bench_extract(OrbEngine *e, const struct sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                      int reps, double *ms_per_frame, double *stage_ms);
+int orb_match_bf(OrbEngine *e, const uint8_t *query, int nq, const uint8_t *train, int nt, int32_t *best_idx,
+                 int32_t *best_dist, int32_t *second_dist);
+int orb_search_for_init(OrbEngine *e, const struct sqlm_keypoint *k1, const uint8_t *d1, int n1,
+                        const struct sqlm_keypoint *k2, const uint8_t *d2, int n2,
+                        const struct sqlm_frame_bounds *f2, float *prev, int32_t *m12, int window, float nnratio,
+                        int check_ori, int *n_matches);
+
 }  // namespace sqlm

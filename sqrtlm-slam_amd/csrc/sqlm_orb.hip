@@ -1,0 +1,1186 @@
+// sqlm_orb.hip — ORB front end on gfx950:
+// ORBextractor::operator() (src/frontend/ORBextractor.cc:1284-1399) and
+// ORBmatcher::SearchForInitialization / DescriptorDistance
+// (src/frontend/ORBmatcher.cc:573-718, :2096-2116), bit-exact with the CPU
+// restatement in oracle/orb_ref.c.
+//
+// Extraction pipeline for one image (all levels in flight on one stream):
+//   k_orb_resize    level l from level l-1, one thread per output pixel
+//                   (OpenCV INTER_LINEAR fixed point, SSE2 vertical rounding
+//                   below the vector end, scalar after — see orb_ref.c);
+//   k_orb_fast      one workgroup per 30-px cell of every level: the cell view
+//                   (<= 72x72) is staged in LDS, FAST-9/16 score per pixel,
+//                   3x3 non-max suppression, the minThFAST retry when the cell
+//                   is empty, and a ballot compaction that keeps OpenCV's
+//                   row-major emission order;
+//   k_orb_scan / k_orb_compact   cell counts -> one contiguous candidate list
+//                   per level in the reference's cell order (4 B each);
+//   host            DistributeOctTree (ORBextractor.cc:692-1043) on the
+//                   candidates: a serial list algorithm whose output order is
+//                   part of the result, so it stays a host step;
+//   k_orb_blur      GaussianBlur 7x7 sigma 2 per level, LDS tile with halo
+//                   (integer row pass, float column pass as OpenCV's SSE2);
+//   k_orb_describe  one wavefront per keypoint: intensity-centroid moments
+//                   (IC_Angle) by lane-parallel integer sums + fastAtan2, then
+//                   256 steered-BRIEF tests, 4 per lane, nibbles merged by a
+//                   lane shuffle.
+// Matching: k_orb_bf (one thread per query, train descriptors staged through
+// LDS, v_bcnt popcounts) and, for SearchForInitialization, k_sfi_list (one
+// wavefront per query enumerates the frame grid window in the reference's
+// order and emits (candidate, distance) pairs); the order-dependent
+// acceptance loop (vMatchedDistance, vnMatches21, rotation histogram) runs on
+// the host over those lists.
+//
+// Compiled with -ffp-contract=off: the reference is built in ISO C++ mode
+// (CMakeLists.txt:4), where GCC does not contract a*b+c into an FMA.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <list>
+#include <vector>
+
+#include "../../include/sqrtlm_orb.h"
+#include "orb_pattern.h"
+#include "sqlm_internal.h"
+
+namespace sqlm {
+
+namespace {
+
+constexpr int kEdge = 19;       // EDGE_THRESHOLD (ORBextractor.cc:78)
+constexpr int kPatch = 31;      // PATCH_SIZE (:76)
+constexpr int kHalf = 15;       // HALF_PATCH_SIZE
+constexpr int kCellMax = 72;    // largest FAST view side (cell <= 60 + 6 overlap)
+constexpr int kCellCap = 1024;  // candidates per cell (3x3 NMS: <= 33 x 33)
+constexpr int kMaxLevels = 16;
+constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:70-75)
+constexpr int kHistoLength = 30, kThLow = 50;  // ORBmatcher.cc:46-48
+
+struct OrbCell {
+  int img_off, pitch;  // level image in the packed pyramid
+  int x0, y0, w, h;    // FAST view
+  int offx, offy;      // j*wCell, i*hCell (coordinates relative to minBorder)
+};
+
+struct OrbDescIn {
+  float x, y, response;
+  int level;
+};
+
+struct LevelTab {
+  int off[kMaxLevels], pitch[kMaxLevels];
+  float scale[kMaxLevels], size[kMaxLevels];
+  int umax[kHalf + 1];
+};
+
+__device__ __forceinline__ int d_floor(float v) {
+  const int i = (int)v;
+  return i - (i > v);
+}
+__device__ __forceinline__ int d_round(float v) { return (int)__builtin_rintf(v); }  // cvRound: half to even
+__device__ __forceinline__ int d_sat_short(float v) {
+  const int r = d_round(v);
+  return r < -32768 ? -32768 : r > 32767 ? 32767 : r;
+}
+__device__ __forceinline__ int d_sat16(int v) { return v < -32768 ? -32768 : v > 32767 ? 32767 : v; }
+__device__ __forceinline__ int d_sat_u8(int v) { return v < 0 ? 0 : v > 255 ? 255 : v; }
+
+// ---- pyramid ------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_orb_resize(const uint8_t *__restrict__ src, int sw, int sh,
+                                                    uint8_t *__restrict__ dst, int dw, int dh, double scale_x,
+                                                    double scale_y, int vend) {
+  const int dx = blockIdx.x * blockDim.x + threadIdx.x, dy = blockIdx.y;
+  if (dx >= dw || dy >= dh) return;
+  float fx = (float)((dx + 0.5) * scale_x - 0.5);
+  int sx = d_floor(fx);
+  fx -= sx;
+  if (sx < 0) fx = 0, sx = 0;
+  const bool tail = sx + 1 >= sw;  // dx >= xmax (sx is monotone in dx)
+  if (tail && sx >= sw - 1) fx = 0, sx = sw - 1;
+  const int a0 = d_sat_short((1.f - fx) * 2048), a1 = d_sat_short(fx * 2048);
+  float fy = (float)((dy + 0.5) * scale_y - 0.5);
+  int sy = d_floor(fy);
+  fy -= sy;
+  const int b0 = d_sat_short((1.f - fy) * 2048), b1 = d_sat_short(fy * 2048);
+  const int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
+  const uint8_t *S0 = src + (size_t)y0 * sw, *S1 = src + (size_t)y1 * sw;
+  const int r0 = tail ? S0[sx] * 2048 : S0[sx] * a0 + S0[sx + 1] * a1;
+  const int r1 = tail ? S1[sx] * 2048 : S1[sx] * a0 + S1[sx + 1] * a1;
+  int v;
+  if (dx < vend) {
+    const int a = d_sat16(r0 >> 4), c = d_sat16(r1 >> 4);
+    const int m = d_sat16(((a * b0) >> 16) + ((c * b1) >> 16));
+    v = d_sat16(m + 2) >> 2;
+  } else {
+    v = (r0 * b0 + r1 * b1 + (1 << 21)) >> 22;
+  }
+  dst[(size_t)dy * dw + dx] = (uint8_t)d_sat_u8(v);
+}
+
+// ---- FAST-9/16 per cell --------------------------------------------------------
+__constant__ int c_fast_off[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1}, {2, -2}, {1, -3},
+                                      {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+
+// cornerScore<16> (OpenCV fast_score.cpp) on an LDS view with row pitch kCellMax.
+__device__ int fast_corner_score(const uint8_t *ptr, const int *pixel, int threshold) {
+  int d[25];
+  const int v = ptr[0];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) d[k] = v - ptr[pixel[k]];
+  int a0 = threshold;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(d[k + 1], d[k + 2]);
+    a = min(a, d[k + 3]);
+    if (a <= a0) continue;
+    a = min(a, d[k + 4]);
+    a = min(a, d[k + 5]);
+    a = min(a, d[k + 6]);
+    a = min(a, d[k + 7]);
+    a = min(a, d[k + 8]);
+    a0 = max(a0, min(a, d[k]));
+    a0 = max(a0, min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int b = max(d[k + 1], d[k + 2]);
+    b = max(b, d[k + 3]);
+    b = max(b, d[k + 4]);
+    b = max(b, d[k + 5]);
+    if (b >= b0) continue;
+    b = max(b, d[k + 6]);
+    b = max(b, d[k + 7]);
+    b = max(b, d[k + 8]);
+    b0 = min(b0, max(b, d[k]));
+    b0 = min(b0, max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// The FAST test of OpenCV's FAST_t<16> for one pixel: 0 if not a corner, else
+// its score (>= threshold - 1 > 0 for the thresholds used).
+__device__ int fast_pixel(const uint8_t *ptr, const int *pixel, int threshold) {
+  const int v = ptr[0];
+  auto cls = [&](int x) { const int i = x - v; return i < -threshold ? 1 : i > threshold ? 2 : 0; };
+  int d = cls(ptr[pixel[0]]) | cls(ptr[pixel[8]]);
+  if (d == 0) return 0;
+  d &= cls(ptr[pixel[2]]) | cls(ptr[pixel[10]]);
+  d &= cls(ptr[pixel[4]]) | cls(ptr[pixel[12]]);
+  d &= cls(ptr[pixel[6]]) | cls(ptr[pixel[14]]);
+  if (d == 0) return 0;
+  d &= cls(ptr[pixel[1]]) | cls(ptr[pixel[9]]);
+  d &= cls(ptr[pixel[3]]) | cls(ptr[pixel[11]]);
+  d &= cls(ptr[pixel[5]]) | cls(ptr[pixel[13]]);
+  d &= cls(ptr[pixel[7]]) | cls(ptr[pixel[15]]);
+  if (d & 1) {
+    const int vt = v - threshold;
+    int count = 0;
+    for (int k = 0; k < 25; k++) {
+      if (ptr[pixel[k]] < vt) {
+        if (++count > 8) return fast_corner_score(ptr, pixel, threshold);
+      } else
+        count = 0;
+    }
+  }
+  if (d & 2) {
+    const int vt = v + threshold;
+    int count = 0;
+    for (int k = 0; k < 25; k++) {
+      if (ptr[pixel[k]] > vt) {
+        if (++count > 8) return fast_corner_score(ptr, pixel, threshold);
+      } else
+        count = 0;
+    }
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void k_orb_fast(const uint8_t *__restrict__ pyr, const OrbCell *__restrict__ cells,
+                                                  int ini_th, int min_th, uint32_t *__restrict__ out,
+                                                  int *__restrict__ cnt) {
+  __shared__ uint8_t pix[kCellMax * kCellMax];
+  __shared__ uint8_t sc[kCellMax * kCellMax];
+  __shared__ int wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const OrbCell c = cells[blockIdx.x];
+  const int n = c.w * c.h;
+  for (int p = tid; p < n; p += 256) {
+    const int y = p / c.w, x = p - y * c.w;
+    pix[y * kCellMax + x] = pyr[c.img_off + (size_t)(c.y0 + y) * c.pitch + c.x0 + x];
+  }
+  int pixel[25];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) pixel[k] = c_fast_off[k][0] + c_fast_off[k][1] * kCellMax;
+#pragma unroll
+  for (int k = 16; k < 25; ++k) pixel[k] = pixel[k - 16];
+  auto keep = [&](int p) -> bool {
+    const int y = p / c.w, x = p - y * c.w;
+    if (y < 3 || y >= c.h - 3 || x < 3 || x >= c.w - 3) return false;
+    const uint8_t *s = &sc[y * kCellMax + x];
+    const int v = s[0];
+    return v > 0 && v > s[1] && v > s[-1] && v > s[-kCellMax - 1] && v > s[-kCellMax] && v > s[-kCellMax + 1] &&
+           v > s[kCellMax - 1] && v > s[kCellMax] && v > s[kCellMax + 1];
+  };
+  int th = min(max(ini_th, 0), 255);
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int p = tid; p < kCellMax * kCellMax; p += 256) sc[p] = 0;
+    __syncthreads();
+    for (int p = tid; p < n; p += 256) {
+      const int y = p / c.w, x = p - y * c.w;
+      if (y < 3 || y >= c.h - 3 || x < 3 || x >= c.w - 3) continue;
+      sc[y * kCellMax + x] = (uint8_t)fast_pixel(&pix[y * kCellMax + x], pixel, th);
+    }
+    __syncthreads();
+    int mine = 0;
+    for (int p = tid; p < n; p += 256) mine += keep(p);
+    for (int m = 32; m >= 1; m >>= 1) mine += __shfl_xor(mine, m, 64);
+    if (lane == 0) wsum[wave] = mine;
+    __syncthreads();
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+    if (total > 0 || pass == 1) break;
+    th = min(max(min_th, 0), 255);
+  }
+  // emission in row-major order (OpenCV pushes row i-1 after scanning row i)
+  int base = 0;
+  for (int r0 = 0; r0 < n; r0 += 256) {
+    const int p = r0 + tid;
+    const bool k = p < n && keep(p);
+    const unsigned long long m = __ballot(k);
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wave] = __popcll(m);
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wave; ++w) off += wsum[w];
+    if (k && off + pre < kCellCap) {
+      const int y = p / c.w, x = p - y * c.w;
+      out[(size_t)blockIdx.x * kCellCap + off + pre] =
+          (uint32_t)(x + c.offx) | ((uint32_t)(y + c.offy) << 12) | ((uint32_t)sc[y * kCellMax + x] << 24);
+    }
+    base += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (tid == 0) cnt[blockIdx.x] = min(base, kCellCap);
+}
+
+// exclusive scan of n counts (one workgroup of 1024)
+__global__ __launch_bounds__(1024) void k_orb_scan(const int *__restrict__ cnt, int n, int *__restrict__ off) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x, chunk = (n + 1023) / 1024, b = t * chunk, e = min(n, b + chunk);
+  int s = 0;
+  for (int i = b; i < e; ++i) s += cnt[i];
+  part[t] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = t ? part[t - 1] : 0;
+  for (int i = b; i < e; ++i) {
+    off[i] = run;
+    run += cnt[i];
+  }
+  if (t == 1023) off[n] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_orb_compact(const uint32_t *__restrict__ cellkp, const int *__restrict__ cnt,
+                                                     const int *__restrict__ off, uint32_t *__restrict__ outc) {
+  const int c = blockIdx.x, n = cnt[c], o = off[c];
+  for (int i = threadIdx.x; i < n; i += 256) outc[o + i] = cellkp[(size_t)c * kCellCap + i];
+}
+
+// ---- GaussianBlur 7x7, sigma 2, BORDER_REFLECT_101 ----------------------------------
+struct BlurK {
+  int ik[4];    // center .. edge, x256 integers
+  float fk[4];  // ik / 65536 (SSE2 column kernel)
+};
+
+__device__ __forceinline__ int refl101(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) i = i < 0 ? -i : 2 * n - 2 - i;
+  return i;
+}
+
+constexpr int kBTX = 32, kBTY = 8;
+__global__ __launch_bounds__(256) void k_orb_blur(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int w,
+                                                  int h, BlurK k) {
+  __shared__ uint8_t pix[kBTY + 6][kBTX + 6];
+  __shared__ int R[kBTY + 6][kBTX];
+  const int tx = threadIdx.x % kBTX, ty = threadIdx.x / kBTX;
+  const int x0 = blockIdx.x * kBTX, y0 = blockIdx.y * kBTY;
+  for (int p = threadIdx.x; p < (kBTY + 6) * (kBTX + 6); p += 256) {
+    const int yy = p / (kBTX + 6), xx = p - yy * (kBTX + 6);
+    pix[yy][xx] = src[(size_t)refl101(y0 + yy - 3, h) * w + refl101(x0 + xx - 3, w)];
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < (kBTY + 6) * kBTX; p += 256) {
+    const int yy = p / kBTX, xx = p - yy * kBTX;
+    const uint8_t *s = &pix[yy][xx + 3];
+    R[yy][xx] = k.ik[0] * s[0] + k.ik[1] * (s[1] + s[-1]) + k.ik[2] * (s[2] + s[-2]) + k.ik[3] * (s[3] + s[-3]);
+  }
+  __syncthreads();
+  const int x = x0 + tx, y = y0 + ty;
+  if (x >= w || y >= h) return;
+  // the row sums of rows beyond the image come from reflected pixel rows, as
+  // OpenCV's filter engine reflects the row buffer index
+  int v;
+  if (x < (w & ~3)) {
+    float s = (float)R[ty + 3][tx] * k.fk[0];
+    s = s + 0.0f;
+#pragma unroll
+    for (int j = 1; j <= 3; ++j) s = s + (float)(R[ty + 3 + j][tx] + R[ty + 3 - j][tx]) * k.fk[j];
+    v = d_sat16((int)__builtin_rintf(s));
+  } else {
+    int s = k.ik[0] * R[ty + 3][tx];
+#pragma unroll
+    for (int j = 1; j <= 3; ++j) s += k.ik[j] * (R[ty + 3 + j][tx] + R[ty + 3 - j][tx]);
+    v = (s + (1 << 15)) >> 16;
+  }
+  dst[(size_t)y * w + x] = (uint8_t)d_sat_u8(v);
+}
+
+// ---- orientation + steered BRIEF, one wavefront per keypoint -----------------------
+__device__ float fast_atan2_deg(float y, float x) {
+  const float p1 = 0.9997878412794807f * (float)(180 / 3.1415926535897932384626433832795);
+  const float p3 = -0.3258083974640975f * (float)(180 / 3.1415926535897932384626433832795);
+  const float p5 = 0.1555786518463281f * (float)(180 / 3.1415926535897932384626433832795);
+  const float p7 = -0.04432655554792128f * (float)(180 / 3.1415926535897932384626433832795);
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = __fdiv_rn(ay, ax + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = __fdiv_rn(ax, ay + (float)2.2204460492503131e-16);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+__global__ __launch_bounds__(256) void k_orb_describe(const uint8_t *__restrict__ pyr, const uint8_t *__restrict__ blur,
+                                                      LevelTab tab, const signed char *__restrict__ pattern,
+                                                      const OrbDescIn *__restrict__ in, int n,
+                                                      sqlm_keypoint *__restrict__ kout, uint8_t *__restrict__ dout) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const OrbDescIn q = in[i];
+  const int L = q.level, step = tab.pitch[L];
+  const int cx = d_round(q.x), cy = d_round(q.y);
+  // IC_Angle (ORBextractor.cc:92-141): m_10 = sum u I, m_01 = sum v I over the disc
+  const uint8_t *center = pyr + tab.off[L] + (size_t)cy * step + cx;
+  int m10 = 0, m01 = 0;
+  for (int v = -kHalf; v <= kHalf; ++v) {
+    const int d = tab.umax[v < 0 ? -v : v];
+    for (int u = -d + lane; u <= d; u += 64) {
+      const int val = center[v * step + u];
+      m10 += u * val;
+      m01 += v * val;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    m10 += __shfl_xor(m10, m, 64);
+    m01 += __shfl_xor(m01, m, 64);
+  }
+  const float angle = fast_atan2_deg((float)m01, (float)m10);
+  // computeOrbDescriptor (:155-206) on the blurred level
+  const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+  const float ang = angle * factorPI;
+  const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+  const uint8_t *bc = blur + tab.off[L] + (size_t)cy * step + cx;
+  int nib = 0;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const signed char *pp = pattern + 4 * (4 * lane + t);
+    const float x0 = (float)pp[0], y0 = (float)pp[1], x1 = (float)pp[2], y1 = (float)pp[3];
+    const int t0 = bc[d_round(x0 * b + y0 * a) * step + d_round(x0 * a - y0 * b)];
+    const int t1 = bc[d_round(x1 * b + y1 * a) * step + d_round(x1 * a - y1 * b)];
+    nib |= (t0 < t1) << t;
+  }
+  int byte = nib << (4 * (lane & 1));
+  byte |= __shfl_xor(byte, 1, 64);
+  if (!(lane & 1)) dout[(size_t)32 * i + (lane >> 1)] = (uint8_t)byte;
+  if (lane == 0) {
+    sqlm_keypoint k;
+    k.x = q.x;
+    k.y = q.y;
+    if (L != 0) {
+      k.x *= tab.scale[L];
+      k.y *= tab.scale[L];
+    }
+    k.size = tab.size[L];
+    k.angle = angle;
+    k.response = q.response;
+    k.octave = L;
+    kout[i] = k;
+  }
+}
+
+// ---- Hamming matching ------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_orb_bf(const uint32_t *__restrict__ q, int nq, const uint32_t *__restrict__ t,
+                                                int nt, int *__restrict__ bidx, int *__restrict__ bd,
+                                                int *__restrict__ bd2) {
+  __shared__ uint32_t tile[256][9];  // +1 word: conflict-free column reads
+  const int qi = blockIdx.x * 256 + threadIdx.x;
+  uint32_t my[8];
+#pragma unroll
+  for (int w = 0; w < 8; ++w) my[w] = qi < nq ? q[(size_t)8 * qi + w] : 0u;
+  int best = INT_MAX, best2 = INT_MAX, bi = -1;
+  for (int t0 = 0; t0 < nt; t0 += 256) {
+    __syncthreads();
+    for (int p = threadIdx.x; p < 256 * 8; p += 256) {
+      const int r = p >> 3, w = p & 7;
+      tile[r][w] = t0 + r < nt ? t[(size_t)8 * (t0 + r) + w] : 0u;
+    }
+    __syncthreads();
+    const int m = min(256, nt - t0);
+    for (int r = 0; r < m; ++r) {
+      int dist = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) dist += __builtin_popcount(my[w] ^ tile[r][w]);
+      if (dist < best) {
+        best2 = best;
+        best = dist;
+        bi = t0 + r;
+      } else if (dist < best2) {
+        best2 = dist;
+      }
+    }
+  }
+  if (qi < nq) {
+    bidx[qi] = bi;
+    bd[qi] = best;
+    bd2[qi] = best2;
+  }
+}
+
+struct SfiArgs {
+  const float *q;          // [n1][4] prev.x prev.y octave(as float bits: level) pad
+  const uint32_t *d1;      // [n1][8]
+  const float *k2;         // [n2][4] x y octave pad
+  const uint32_t *d2;      // [n2][8]
+  const int *cell_ptr;     // [64*48+1] grid CSR (cell = ix*48 + iy)
+  const int *cell_idx;     // keypoint indices in cell order
+  float min_x, min_y, wi, hi, r;
+  int n1;
+};
+
+// GetFeaturesInArea (Frame.cc:1463-1552) + DescriptorDistance for one query:
+// pass 0 counts the candidates, pass 1 writes (i2, dist) in the reference's
+// iteration order (cells ix-major, then cell insertion order).
+template <int PASS>
+__global__ __launch_bounds__(256) void k_sfi_list(SfiArgs A, int *__restrict__ cnt, const int *__restrict__ off,
+                                                  int2 *__restrict__ pairs) {
+  const int lane = threadIdx.x & 63;
+  const int i1 = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i1 >= A.n1) return;
+  const float x = A.q[4 * i1], y = A.q[4 * i1 + 1];
+  const int level = __float_as_int(A.q[4 * i1 + 2]);
+  int run = 0;
+  bool ok = level <= 0;
+  int nMinCellX = 0, nMaxCellX = -1, nMinCellY = 0, nMaxCellY = -1;
+  if (ok) {
+    nMinCellX = max(0, (int)floorf((x - A.min_x - A.r) * A.wi));
+    ok = nMinCellX < kGridCols;
+  }
+  if (ok) {
+    nMaxCellX = min(kGridCols - 1, (int)ceilf((x - A.min_x + A.r) * A.wi));
+    ok = nMaxCellX >= 0;
+  }
+  if (ok) {
+    nMinCellY = max(0, (int)floorf((y - A.min_y - A.r) * A.hi));
+    ok = nMinCellY < kGridRows;
+  }
+  if (ok) {
+    nMaxCellY = min(kGridRows - 1, (int)ceilf((y - A.min_y + A.r) * A.hi));
+    ok = nMaxCellY >= 0;
+  }
+  uint32_t my[8];
+  if (PASS == 1) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) my[w] = A.d1[(size_t)8 * i1 + w];
+  }
+  const int base = PASS == 1 ? off[i1] : 0;
+  if (ok) {
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+      for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+        const int c = ix * kGridRows + iy, b = A.cell_ptr[c], e = A.cell_ptr[c + 1];
+        for (int j0 = b; j0 < e; j0 += 64) {
+          const int j = j0 + lane;
+          bool hit = false;
+          int i2 = 0;
+          if (j < e) {
+            i2 = A.cell_idx[j];
+            const float kx = A.k2[4 * i2], ky = A.k2[4 * i2 + 1];
+            const int oct = __float_as_int(A.k2[4 * i2 + 2]);
+            // bCheckLevels with minLevel = maxLevel = level1 (= 0)
+            hit = !(oct < level) && !(oct > level);
+            const float distx = kx - x, disty = ky - y;
+            hit = hit && fabsf(distx) < A.r && fabsf(disty) < A.r;
+          }
+          const unsigned long long m = __ballot(hit);
+          if (PASS == 1 && hit) {
+            int dist = 0;
+#pragma unroll
+            for (int w = 0; w < 8; ++w) dist += __builtin_popcount(my[w] ^ A.d2[(size_t)8 * i2 + w]);
+            pairs[base + run + __popcll(m & ((1ull << lane) - 1ull))] = make_int2(i2, dist);
+          }
+          run += __popcll(m);
+        }
+      }
+  }
+  if (PASS == 0 && lane == 0) cnt[i1] = run;
+}
+
+// ---- host: DistributeOctTree (ORBextractor.cc:606-1043) -----------------------------
+struct Cand {
+  float x, y, response;
+};
+
+struct ExtractorNode {
+  int ulx = 0, uly = 0, urx = 0, ury = 0, blx = 0, bly = 0, brx = 0, bry = 0;
+  std::vector<Cand> keys;
+  bool no_more = false;
+  std::list<ExtractorNode>::iterator self;
+};
+
+void divide_node(const ExtractorNode &p, ExtractorNode &n1, ExtractorNode &n2, ExtractorNode &n3,
+                 ExtractorNode &n4) {
+  const int halfX = (int)std::ceil(static_cast<float>(p.urx - p.ulx) / 2);
+  const int halfY = (int)std::ceil(static_cast<float>(p.bry - p.uly) / 2);
+  n1.ulx = p.ulx; n1.uly = p.uly;
+  n1.urx = p.ulx + halfX; n1.ury = p.uly;
+  n1.blx = p.ulx; n1.bly = p.uly + halfY;
+  n1.brx = p.ulx + halfX; n1.bry = p.uly + halfY;
+  n2.ulx = n1.urx; n2.uly = n1.ury;
+  n2.urx = p.urx; n2.ury = p.ury;
+  n2.blx = n1.brx; n2.bly = n1.bry;
+  n2.brx = p.urx; n2.bry = p.uly + halfY;
+  n3.ulx = n1.blx; n3.uly = n1.bly;
+  n3.urx = n1.brx; n3.ury = n1.bry;
+  n3.blx = p.blx; n3.bly = p.bly;
+  n3.brx = n1.brx; n3.bry = p.bly;
+  n4.ulx = n3.urx; n4.uly = n3.ury;
+  n4.urx = n2.brx; n4.ury = n2.bry;
+  n4.blx = n3.brx; n4.bly = n3.bry;
+  n4.brx = p.brx; n4.bry = p.bry;
+  for (const Cand &k : p.keys) {
+    if (k.x < n1.urx) (k.y < n1.bry ? n1 : n3).keys.push_back(k);
+    else (k.y < n1.bry ? n2 : n4).keys.push_back(k);
+  }
+  n1.no_more = n1.keys.size() == 1;
+  n2.no_more = n2.keys.size() == 1;
+  n3.no_more = n3.keys.size() == 1;
+  n4.no_more = n4.keys.size() == 1;
+}
+
+std::vector<Cand> distribute_quadtree(const std::vector<Cand> &keys, int minX, int maxX, int minY, int maxY, int N) {
+  const int nIni = (int)std::round(static_cast<float>(maxX - minX) / (maxY - minY));
+  const float hX = static_cast<float>(maxX - minX) / nIni;
+  std::list<ExtractorNode> nodes;
+  std::vector<ExtractorNode *> ini(nIni);
+  for (int i = 0; i < nIni; i++) {
+    ExtractorNode ni;
+    ni.ulx = (int)(hX * static_cast<float>(i));
+    ni.urx = (int)(hX * static_cast<float>(i + 1));
+    ni.blx = ni.ulx;
+    ni.bly = maxY - minY;
+    ni.brx = ni.urx;
+    ni.bry = maxY - minY;
+    nodes.push_back(std::move(ni));
+    ini[i] = &nodes.back();
+  }
+  for (const Cand &k : keys) ini[(size_t)(k.x / hX)]->keys.push_back(k);
+  for (auto it = nodes.begin(); it != nodes.end();) {
+    if (it->keys.size() == 1) {
+      it->no_more = true;
+      ++it;
+    } else if (it->keys.empty())
+      it = nodes.erase(it);
+    else
+      ++it;
+  }
+  std::vector<std::pair<int, ExtractorNode *>> expand;
+  auto push_children = [&](ExtractorNode *c[4], int *n_to_expand) {
+    for (int k = 0; k < 4; ++k) {
+      if (c[k]->keys.empty()) continue;
+      nodes.push_front(std::move(*c[k]));
+      if (nodes.front().keys.size() > 1) {
+        if (n_to_expand) ++*n_to_expand;
+        expand.emplace_back((int)nodes.front().keys.size(), &nodes.front());
+        nodes.front().self = nodes.begin();
+      }
+    }
+  };
+  bool finish = false;
+  while (!finish) {
+    int prev_size = (int)nodes.size();
+    int n_to_expand = 0;
+    expand.clear();
+    for (auto it = nodes.begin(); it != nodes.end();) {
+      if (it->no_more) {
+        ++it;
+        continue;
+      }
+      ExtractorNode n1, n2, n3, n4;
+      divide_node(*it, n1, n2, n3, n4);
+      ExtractorNode *c[4] = {&n1, &n2, &n3, &n4};
+      push_children(c, &n_to_expand);
+      it = nodes.erase(it);
+    }
+    if ((int)nodes.size() >= N || (int)nodes.size() == prev_size) {
+      finish = true;
+    } else if ((int)nodes.size() + n_to_expand * 3 > N) {
+      while (!finish) {
+        prev_size = (int)nodes.size();
+        std::vector<std::pair<int, ExtractorNode *>> prev = expand;
+        expand.clear();
+        std::stable_sort(prev.begin(), prev.end(),
+                         [](const std::pair<int, ExtractorNode *> &a, const std::pair<int, ExtractorNode *> &b) {
+                           return a.first < b.first;
+                         });
+        for (int j = (int)prev.size() - 1; j >= 0; j--) {
+          ExtractorNode n1, n2, n3, n4;
+          divide_node(*prev[j].second, n1, n2, n3, n4);
+          ExtractorNode *c[4] = {&n1, &n2, &n3, &n4};
+          push_children(c, nullptr);
+          nodes.erase(prev[j].second->self);
+          if ((int)nodes.size() >= N) break;
+        }
+        if ((int)nodes.size() >= N || (int)nodes.size() == prev_size) finish = true;
+      }
+    }
+  }
+  std::vector<Cand> out;
+  out.reserve(nodes.size());
+  for (const ExtractorNode &nd : nodes) {
+    const Cand *best = &nd.keys[0];
+    float max_resp = best->response;
+    for (size_t k = 1; k < nd.keys.size(); k++)
+      if (nd.keys[k].response > max_resp) {
+        best = &nd.keys[k];
+        max_resp = nd.keys[k].response;
+      }
+    out.push_back(*best);
+  }
+  return out;
+}
+
+int resize_vec_end(int width) {  // VResizeLinearVec_32s8u loop bounds
+  int x = 0;
+  for (; x <= width - 16; x += 16) {
+  }
+  for (; x < width - 4; x += 4) {
+  }
+  return x;
+}
+
+BlurK gauss_kernel_7x7_s2() {  // getGaussianKernel(7, 2, CV_32F) -> x256 ints
+  const double scale2X = -0.5 / (2.0 * 2.0);
+  float cf[7];
+  double sum = 0;
+  for (int i = 0; i < 7; i++) {
+    const double x = i - (7 - 1) * 0.5;
+    cf[i] = (float)std::exp(scale2X * x * x);
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  BlurK k;
+  for (int i = 0; i < 7; i++) {
+    cf[i] = (float)(cf[i] * sum);
+    if (i >= 3) k.ik[i - 3] = (int)std::lrint(cf[i] * 256.0f);
+  }
+  for (int j = 0; j < 4; ++j) k.fk[j] = (float)((double)k.ik[j] / 65536.0);
+  return k;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------- engine
+
+struct OrbEngine {
+  hipStream_t st = nullptr;
+  struct Buf {
+    void *p = nullptr;
+    size_t bytes = 0;
+  };
+  Buf img, pyr, blur, cells, cellkp, cnt, off, cand, din, kout, dout, pattern, q, qd, t, td, bidx, bd, bd2, grid,
+      gidx, pairs;
+  std::vector<int> lw, lh, loff;
+  float lscale[kMaxLevels] = {};
+  hipEvent_t ev[8] = {};
+  hipEvent_t ev_copy = nullptr;  // default flags: the host waits on it for a D2H copy
+  double stage_ms[6] = {};
+  bool timing = false;
+  std::vector<int> h_off;
+  std::vector<uint32_t> h_cand;
+
+  ~OrbEngine() {
+    for (Buf *b : {&img, &pyr, &blur, &cells, &cellkp, &cnt, &off, &cand, &din, &kout, &dout, &pattern, &q, &qd, &t,
+                   &td, &bidx, &bd, &bd2, &grid, &gidx, &pairs})
+      if (b->p) (void)hipFree(b->p);
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (ev_copy) (void)hipEventDestroy(ev_copy);
+  }
+  template <class T>
+  T *get(Buf &b, size_t n) {
+    const size_t need = std::max<size_t>(n, 1) * sizeof(T);
+    if (b.bytes < need) {
+      if (b.p) (void)hipFree(b.p);
+      b.p = nullptr;
+      b.bytes = 0;
+      if (hipMalloc(&b.p, need) != hipSuccess) return nullptr;
+      b.bytes = need;
+    }
+    return static_cast<T *>(b.p);
+  }
+  void mark(int i) {
+    if (timing) (void)hipEventRecord(ev[i], st);
+  }
+
+  int extract(const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride, bool upload,
+              std::vector<sqlm_keypoint> &kps, std::vector<uint8_t> &desc);
+  int extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<sqlm_keypoint> &kps,
+                   std::vector<uint8_t> &desc);
+};
+
+OrbEngine *orb_create(hipStream_t st) {
+  OrbEngine *e = new (std::nothrow) OrbEngine();
+  if (!e) return nullptr;
+  e->st = st;
+  for (auto &v : e->ev)
+    if (hipEventCreateWithFlags(&v, hipEventDisableSystemFence) != hipSuccess) {
+      delete e;
+      return nullptr;
+    }
+  if (hipEventCreate(&e->ev_copy) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  signed char *pat = e->get<signed char>(e->pattern, 1024);
+  if (!pat || hipMemcpy(pat, kOrbPattern, 1024, hipMemcpyHostToDevice) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  return e;
+}
+
+void orb_destroy(OrbEngine *e) { delete e; }
+
+int OrbEngine::extract(const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride, bool upload,
+                       std::vector<sqlm_keypoint> &kps, std::vector<uint8_t> &desc) {
+  if (!p || !image || w <= 0 || h <= 0 || stride < w) return SQLM_ERR_INVALID_ARG;
+  if (upload) {
+    uint8_t *d = get<uint8_t>(img, (size_t)w * h);
+    if (!d) return SQLM_ERR_OOM;
+    if (hipMemcpy2DAsync(d, w, image, stride, w, h, hipMemcpyHostToDevice, st) != hipSuccess) return SQLM_ERR_HIP;
+  }
+  return extract_impl(p, w, h, kps, desc);
+}
+
+int OrbEngine::extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<sqlm_keypoint> &kps,
+                            std::vector<uint8_t> &desc) {
+  const int L = p->nlevels;
+  if (L < 1 || L > kMaxLevels || !(p->scale_factor > 1.0f) || p->nfeatures < 0) return SQLM_ERR_INVALID_ARG;
+  // level geometry (ORBextractor ctor :474-560, ComputePyramid :1224-1282)
+  float sf[kMaxLevels];
+  sf[0] = 1.0f;
+  for (int i = 1; i < L; ++i) sf[i] = sf[i - 1] * p->scale_factor;
+  lw.assign(L, 0);
+  lh.assign(L, 0);
+  loff.assign(L + 1, 0);
+  for (int i = 0; i < L; ++i) {
+    const float inv = 1.0f / sf[i];
+    lw[i] = (int)std::lrint((float)w * inv);
+    lh[i] = (int)std::lrint((float)h * inv);
+    lscale[i] = sf[i];
+    if (lw[i] - 2 * (kEdge - 3) < 30 || lh[i] - 2 * (kEdge - 3) < 30 || lw[i] > 4096 || lh[i] > 4096)
+      return SQLM_ERR_UNSUPPORTED;
+    loff[i + 1] = loff[i] + lw[i] * lh[i];
+  }
+  std::vector<int> nfeat(L);
+  {
+    const float factor = 1.0f / p->scale_factor;
+    float nd = p->nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; ++l) {
+      nfeat[l] = (int)std::lrint(nd);
+      sum += nfeat[l];
+      nd *= factor;
+    }
+    nfeat[L - 1] = std::max(p->nfeatures - sum, 0);
+  }
+  // cells of every level (ComputeKeyPointsOctTree :1045-1110)
+  std::vector<OrbCell> hc;
+  std::vector<int> level_cell(L + 1, 0);
+  for (int l = 0; l < L; ++l) {
+    level_cell[l] = (int)hc.size();
+    const float W = 30;
+    const int minB = kEdge - 3, maxBX = lw[l] - kEdge + 3, maxBY = lh[l] - kEdge + 3;
+    const float width = (float)(maxBX - minB), height = (float)(maxBY - minB);
+    const int nCols = (int)(width / W), nRows = (int)(height / W);
+    const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+    for (int i = 0; i < nRows; i++) {
+      const float iniY = (float)(minB + i * hCell);
+      float maxY = iniY + hCell + 6;
+      if (iniY >= maxBY - 3) continue;
+      if (maxY > maxBY) maxY = (float)maxBY;
+      for (int j = 0; j < nCols; j++) {
+        const float iniX = (float)(minB + j * wCell);
+        float maxX = iniX + wCell + 6;
+        if (iniX >= maxBX - 3) continue;
+        if (maxX > maxBX) maxX = (float)maxBX;
+        OrbCell c;
+        c.img_off = loff[l];
+        c.pitch = lw[l];
+        c.x0 = (int)iniX;
+        c.y0 = (int)iniY;
+        c.w = (int)maxX - (int)iniX;
+        c.h = (int)maxY - (int)iniY;
+        c.offx = j * wCell;
+        c.offy = i * hCell;
+        if (c.w > kCellMax || c.h > kCellMax) return SQLM_ERR_UNSUPPORTED;
+        hc.push_back(c);
+      }
+    }
+  }
+  level_cell[L] = (int)hc.size();
+  const int ncell = (int)hc.size();
+  uint8_t *d_pyr = get<uint8_t>(pyr, loff[L]), *d_blur = get<uint8_t>(blur, loff[L]);
+  OrbCell *d_cells = get<OrbCell>(cells, ncell);
+  uint32_t *d_cellkp = get<uint32_t>(cellkp, (size_t)ncell * kCellCap);
+  int *d_cnt = get<int>(cnt, ncell), *d_off = get<int>(off, ncell + 1);
+  uint32_t *d_cand = get<uint32_t>(cand, (size_t)ncell * kCellCap);
+  if (!d_pyr || !d_blur || !d_cells || !d_cellkp || !d_cnt || !d_off || !d_cand) return SQLM_ERR_OOM;
+  mark(0);
+  if (hipMemcpyAsync(d_pyr, img.p, (size_t)w * h, hipMemcpyDeviceToDevice, st) != hipSuccess) return SQLM_ERR_HIP;
+  for (int l = 1; l < L; ++l) {
+    const double scale_x = 1. / ((double)lw[l] / lw[l - 1]), scale_y = 1. / ((double)lh[l] / lh[l - 1]);
+    hipLaunchKernelGGL(k_orb_resize, dim3((lw[l] + 255) / 256, lh[l]), dim3(256), 0, st, d_pyr + loff[l - 1],
+                       lw[l - 1], lh[l - 1], d_pyr + loff[l], lw[l], lh[l], scale_x, scale_y, resize_vec_end(lw[l]));
+  }
+  mark(1);
+  if (hipMemcpyAsync(d_cells, hc.data(), sizeof(OrbCell) * ncell, hipMemcpyHostToDevice, st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  hipLaunchKernelGGL(k_orb_fast, dim3(ncell), dim3(256), 0, st, d_pyr, d_cells, p->ini_th_fast, p->min_th_fast,
+                     d_cellkp, d_cnt);
+  mark(2);
+  hipLaunchKernelGGL(k_orb_scan, dim3(1), dim3(1024), 0, st, d_cnt, ncell, d_off);
+  hipLaunchKernelGGL(k_orb_compact, dim3(ncell), dim3(256), 0, st, d_cellkp, d_cnt, d_off, d_cand);
+  mark(3);
+  h_off.resize(ncell + 1);
+  if (hipMemcpyAsync(h_off.data(), d_off, sizeof(int) * (ncell + 1), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  const int ncand = h_off[ncell];
+  h_cand.resize(std::max(ncand, 1));
+  if (ncand &&
+      hipMemcpyAsync(h_cand.data(), d_cand, sizeof(uint32_t) * ncand, hipMemcpyDeviceToHost, st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  if (hipEventRecord(ev_copy, st) != hipSuccess) return SQLM_ERR_HIP;
+  // the blur does not depend on the quadtree: it runs while the host distributes
+  const BlurK bk = gauss_kernel_7x7_s2();
+  for (int l = 0; l < L; ++l)
+    hipLaunchKernelGGL(k_orb_blur, dim3((lw[l] + kBTX - 1) / kBTX, (lh[l] + kBTY - 1) / kBTY), dim3(256), 0, st,
+                       d_pyr + loff[l], d_blur + loff[l], lw[l], lh[l], bk);
+  mark(4);
+  if (hipEventSynchronize(ev_copy) != hipSuccess) return SQLM_ERR_HIP;
+  // quadtree per level (host)
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<OrbDescIn> hin;
+  for (int l = 0; l < L; ++l) {
+    const int b = h_off[level_cell[l]], e = h_off[level_cell[l + 1]];
+    std::vector<Cand> keys(e - b);
+    for (int i = b; i < e; ++i) {
+      const uint32_t v = h_cand[i];
+      keys[i - b] = Cand{(float)(v & 4095u), (float)((v >> 12) & 4095u), (float)(v >> 24)};
+    }
+    const int minB = kEdge - 3;
+    const std::vector<Cand> sel =
+        distribute_quadtree(keys, minB, lw[l] - kEdge + 3, minB, lh[l] - kEdge + 3, nfeat[l]);
+    for (const Cand &c : sel) hin.push_back(OrbDescIn{c.x + minB, c.y + minB, c.response, l});
+  }
+  stage_ms[5] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const int n = (int)hin.size();
+  kps.resize(n);
+  desc.resize((size_t)32 * n);
+  if (n == 0) return SQLM_OK;
+  OrbDescIn *d_in = get<OrbDescIn>(din, n);
+  sqlm_keypoint *d_kout = get<sqlm_keypoint>(kout, n);
+  uint8_t *d_dout = get<uint8_t>(dout, (size_t)32 * n);
+  if (!d_in || !d_kout || !d_dout) return SQLM_ERR_OOM;
+  LevelTab tab;
+  for (int l = 0; l < L; ++l) {
+    tab.off[l] = loff[l];
+    tab.pitch[l] = lw[l];
+    tab.scale[l] = lscale[l];
+    tab.size[l] = (float)(int)(kPatch * lscale[l]);
+  }
+  {  // umax (ORBextractor ctor :546-560)
+    int v, v0, vmax = (int)std::floor(kHalf * std::sqrt(2.f) / 2 + 1);
+    int vmin = (int)std::ceil(kHalf * std::sqrt(2.f) / 2);
+    const double hp2 = kHalf * kHalf;
+    for (v = 0; v <= vmax; ++v) tab.umax[v] = (int)std::lrint(std::sqrt(hp2 - v * v));
+    for (v = kHalf, v0 = 0; v >= vmin; --v) {
+      while (tab.umax[v0] == tab.umax[v0 + 1]) ++v0;
+      tab.umax[v] = v0;
+      ++v0;
+    }
+  }
+  mark(5);
+  if (hipMemcpyAsync(d_in, hin.data(), sizeof(OrbDescIn) * n, hipMemcpyHostToDevice, st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  hipLaunchKernelGGL(k_orb_describe, dim3((n + 3) / 4), dim3(256), 0, st, d_pyr, d_blur, tab,
+                     (const signed char *)pattern.p, d_in, n, d_kout, d_dout);
+  mark(6);
+  if (hipMemcpyAsync(kps.data(), d_kout, sizeof(sqlm_keypoint) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipMemcpyAsync(desc.data(), d_dout, (size_t)32 * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  if (timing) {
+    float ms;
+    const int pairs_[5][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {5, 6}};
+    for (int s = 0; s < 5; ++s) {
+      if (hipEventElapsedTime(&ms, ev[pairs_[s][0]], ev[pairs_[s][1]]) == hipSuccess) stage_ms[s] += ms;
+    }
+  }
+  return SQLM_OK;
+}
+
+int orb_extract(OrbEngine *e, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                sqlm_keypoint *kps, uint8_t *desc, int cap, int *n_out) {
+  std::vector<sqlm_keypoint> k;
+  std::vector<uint8_t> d;
+  const int r = e->extract(p, image, w, h, stride, true, k, d);
+  if (r) return r;
+  const int n = (int)k.size();
+  if (n_out) *n_out = n;
+  const int m = std::min(n, std::max(cap, 0));
+  if (m > 0 && (!kps || !desc)) return SQLM_ERR_INVALID_ARG;
+  if (m > 0) {
+    std::memcpy(kps, k.data(), sizeof(sqlm_keypoint) * m);
+    std::memcpy(desc, d.data(), (size_t)32 * m);
+  }
+  return SQLM_OK;
+}
+
+int orb_get_level(OrbEngine *e, int level, uint8_t *out, int cap, int *w, int *h) {
+  if (level < 0 || level >= (int)e->lw.size()) return SQLM_ERR_STATE;
+  if (w) *w = e->lw[level];
+  if (h) *h = e->lh[level];
+  const int n = e->lw[level] * e->lh[level];
+  if (!out || cap < n) return SQLM_ERR_INVALID_ARG;
+  if (hipMemcpyAsync(out, (uint8_t *)e->pyr.p + e->loff[level], n, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  return SQLM_OK;
+}
+
+int orb_bench_extract(OrbEngine *e, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
+                      int reps, double *ms_per_frame, double *stage_ms) {
+  std::vector<sqlm_keypoint> k;
+  std::vector<uint8_t> d;
+  int r = e->extract(p, image, w, h, stride, true, k, d);  // warm-up + upload
+  if (r) return r;
+  for (double &s : e->stage_ms) s = 0.0;
+  e->timing = true;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int i = 0; i < reps && !r; ++i) r = e->extract_impl(p, w, h, k, d);
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  e->timing = false;
+  if (r) return r;
+  if (ms_per_frame) *ms_per_frame = ms / std::max(reps, 1);
+  if (stage_ms)
+    for (int s = 0; s < 6; ++s) stage_ms[s] = e->stage_ms[s] / std::max(reps, 1);
+  return SQLM_OK;
+}
+
+int orb_match_bf(OrbEngine *e, const uint8_t *query, int nq, const uint8_t *train, int nt, int32_t *best_idx,
+                 int32_t *best_dist, int32_t *second_dist) {
+  if (nq < 0 || nt < 0 || (nq && (!query || !best_idx || !best_dist || !second_dist)) || (nt && !train))
+    return SQLM_ERR_INVALID_ARG;
+  if (nq == 0) return SQLM_OK;
+  uint32_t *dq = e->get<uint32_t>(e->qd, (size_t)8 * nq), *dt = e->get<uint32_t>(e->td, (size_t)8 * std::max(nt, 1));
+  int *bi = e->get<int>(e->bidx, nq), *b1 = e->get<int>(e->bd, nq), *b2 = e->get<int>(e->bd2, nq);
+  if (!dq || !dt || !bi || !b1 || !b2) return SQLM_ERR_OOM;
+  if (hipMemcpyAsync(dq, query, (size_t)32 * nq, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      (nt && hipMemcpyAsync(dt, train, (size_t)32 * nt, hipMemcpyHostToDevice, e->st) != hipSuccess))
+    return SQLM_ERR_HIP;
+  hipLaunchKernelGGL(k_orb_bf, dim3((nq + 255) / 256), dim3(256), 0, e->st, dq, nq, dt, nt, bi, b1, b2);
+  if (hipMemcpyAsync(best_idx, bi, sizeof(int) * nq, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipMemcpyAsync(best_dist, b1, sizeof(int) * nq, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipMemcpyAsync(second_dist, b2, sizeof(int) * nq, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  return SQLM_OK;
+}
+
+int orb_search_for_init(OrbEngine *e, const sqlm_keypoint *k1, const uint8_t *d1, int n1, const sqlm_keypoint *k2,
+                        const uint8_t *d2, int n2, const sqlm_frame_bounds *f2, float *prev, int32_t *m12, int window,
+                        float nnratio, int check_ori, int *n_matches) {
+  if (n1 < 0 || n2 < 0 || !f2 || (n1 && (!k1 || !d1 || !prev || !m12)) || (n2 && (!k2 || !d2)))
+    return SQLM_ERR_INVALID_ARG;
+  for (int i = 0; i < n1; ++i) m12[i] = -1;
+  if (n_matches) *n_matches = 0;
+  if (n1 == 0) return SQLM_OK;
+  const float wi = static_cast<float>(kGridCols) / static_cast<float>(f2->max_x - f2->min_x);
+  const float hi = static_cast<float>(kGridRows) / static_cast<float>(f2->max_y - f2->min_y);
+  // Frame::AssignFeaturesToGrid (Frame.cc:1268-1285) with PosInGrid (:1554-1565)
+  std::vector<int> cell_of(n2), ptr(kGridCols * kGridRows + 1, 0), idx;
+  for (int i = 0; i < n2; ++i) {
+    const int px = (int)std::round((k2[i].x - f2->min_x) * wi), py = (int)std::round((k2[i].y - f2->min_y) * hi);
+    cell_of[i] = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px * kGridRows + py;
+    if (cell_of[i] >= 0) ptr[cell_of[i] + 1]++;
+  }
+  for (int c = 0; c < kGridCols * kGridRows; ++c) ptr[c + 1] += ptr[c];
+  idx.resize(std::max(ptr.back(), 1));
+  {
+    std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+    for (int i = 0; i < n2; ++i)
+      if (cell_of[i] >= 0) idx[fill[cell_of[i]]++] = i;
+  }
+  std::vector<float> hq((size_t)4 * n1), hk2((size_t)4 * std::max(n2, 1));
+  for (int i = 0; i < n1; ++i) {
+    hq[4 * i] = prev[2 * i];
+    hq[4 * i + 1] = prev[2 * i + 1];
+    std::memcpy(&hq[4 * i + 2], &k1[i].octave, 4);
+  }
+  for (int i = 0; i < n2; ++i) {
+    hk2[4 * i] = k2[i].x;
+    hk2[4 * i + 1] = k2[i].y;
+    std::memcpy(&hk2[4 * i + 2], &k2[i].octave, 4);
+  }
+  SfiArgs A;
+  float *dq = e->get<float>(e->q, hq.size());
+  uint32_t *dd1 = e->get<uint32_t>(e->qd, (size_t)8 * n1);
+  float *dk2 = e->get<float>(e->t, hk2.size());
+  uint32_t *dd2 = e->get<uint32_t>(e->td, (size_t)8 * std::max(n2, 1));
+  int *dptr = e->get<int>(e->grid, ptr.size()), *didx = e->get<int>(e->gidx, idx.size());
+  int *dcnt = e->get<int>(e->bidx, n1), *doff = e->get<int>(e->bd, n1 + 1);
+  if (!dq || !dd1 || !dk2 || !dd2 || !dptr || !didx || !dcnt || !doff) return SQLM_ERR_OOM;
+  if (hipMemcpyAsync(dq, hq.data(), sizeof(float) * hq.size(), hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(dd1, d1, (size_t)32 * n1, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(dk2, hk2.data(), sizeof(float) * hk2.size(), hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      (n2 && hipMemcpyAsync(dd2, d2, (size_t)32 * n2, hipMemcpyHostToDevice, e->st) != hipSuccess) ||
+      hipMemcpyAsync(dptr, ptr.data(), sizeof(int) * ptr.size(), hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(didx, idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, e->st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  A.q = dq;
+  A.d1 = dd1;
+  A.k2 = dk2;
+  A.d2 = dd2;
+  A.cell_ptr = dptr;
+  A.cell_idx = didx;
+  A.min_x = f2->min_x;
+  A.min_y = f2->min_y;
+  A.wi = wi;
+  A.hi = hi;
+  A.r = (float)window;
+  A.n1 = n1;
+  const dim3 g((n1 + 3) / 4);
+  hipLaunchKernelGGL(k_sfi_list<0>, g, dim3(256), 0, e->st, A, dcnt, (const int *)nullptr, (int2 *)nullptr);
+  hipLaunchKernelGGL(k_orb_scan, dim3(1), dim3(1024), 0, e->st, dcnt, n1, doff);
+  std::vector<int> hoff(n1 + 1);
+  if (hipMemcpyAsync(hoff.data(), doff, sizeof(int) * (n1 + 1), hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  const int total = hoff[n1];
+  int2 *dpairs = e->get<int2>(e->pairs, std::max(total, 1));
+  if (!dpairs) return SQLM_ERR_OOM;
+  hipLaunchKernelGGL(k_sfi_list<1>, g, dim3(256), 0, e->st, A, (int *)nullptr, (const int *)doff, dpairs);
+  std::vector<int2> hp(std::max(total, 1));
+  if (total && hipMemcpyAsync(hp.data(), dpairs, sizeof(int2) * total, hipMemcpyDeviceToHost, e->st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  if (hipStreamSynchronize(e->st) != hipSuccess) return SQLM_ERR_HIP;
+  // acceptance loop (ORBmatcher.cc:594-682): order-dependent, over the GPU lists
+  std::vector<int> vMatchedDistance(n2, INT_MAX), vnMatches21(n2, -1), rot_i, rot_bin;
+  int hist[kHistoLength] = {0};
+  const float factor = kHistoLength / 360.0f;
+  int nmatches = 0;
+  for (int i1 = 0; i1 < n1; i1++) {
+    if (k1[i1].octave > 0 || hoff[i1 + 1] == hoff[i1]) continue;
+    int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+    for (int q = hoff[i1]; q < hoff[i1 + 1]; ++q) {
+      const int i2 = hp[q].x, dist = hp[q].y;
+      if (vMatchedDistance[i2] <= dist) continue;
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestIdx2 = i2;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= kThLow && bestDist < (float)bestDist2 * nnratio) {
+      if (vnMatches21[bestIdx2] >= 0) {
+        m12[vnMatches21[bestIdx2]] = -1;
+        nmatches--;
+      }
+      m12[i1] = bestIdx2;
+      vnMatches21[bestIdx2] = i1;
+      vMatchedDistance[bestIdx2] = bestDist;
+      nmatches++;
+      if (check_ori) {
+        float rot = k1[i1].angle - k2[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == kHistoLength) bin = 0;
+        rot_i.push_back(i1);
+        rot_bin.push_back(bin);
+        hist[bin]++;
+      }
+    }
+  }
+  if (check_ori) {  // ComputeThreeMaxima (ORBmatcher.cc:2048-2090)
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < kHistoLength; i++) {
+      const int s = hist[i];
+      if (s > max1) {
+        max3 = max2; max2 = max1; max1 = s;
+        ind3 = ind2; ind2 = ind1; ind1 = i;
+      } else if (s > max2) {
+        max3 = max2; max2 = s;
+        ind3 = ind2; ind2 = i;
+      } else if (s > max3) {
+        max3 = s;
+        ind3 = i;
+      }
+    }
+    if (max2 < 0.1f * (float)max1) {
+      ind2 = -1;
+      ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+      ind3 = -1;
+    }
+    for (size_t q = 0; q < rot_i.size(); ++q) {
+      const int b = rot_bin[q];
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      if (m12[rot_i[q]] >= 0) {
+        m12[rot_i[q]] = -1;
+        nmatches--;
+      }
+    }
+  }
+  for (int i1 = 0; i1 < n1; i1++)
+    if (m12[i1] >= 0) {
+      prev[2 * i1] = k2[m12[i1]].x;
+      prev[2 * i1 + 1] = k2[m12[i1]].y;
+    }
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+}  // namespace sqlm

@@ -441,3 +441,44 @@ def make_pose_graph(n_kf: int = 200, *, window: int = 4, n_loops: int = 3, seed:
     fixed[0] = 1
     return PoseGraph(Siw=S0, fixed=fixed, fix_scale=int(fix_scale), ei=ei, ej=ej, Sji=Sji,
                      meta=dict(gt=gt, seed=seed))
+
+
+# ---- synthetic grey images for the ORB front end ----------
+
+def make_scene(w: int, h: int, *, seed: int = 0, n_rect: int = 0, n_disk: int = 0) -> np.ndarray:
+    """A textured 8-bit scene (float, unclipped): gradient background, random
+    filled rectangles and disks of random grey levels (corners for FAST), and a
+    fine random texture. Sized w x h; n_rect / n_disk default to the area."""
+    rng = np.random.default_rng(seed)
+    n_rect = n_rect or max(40, w * h // 2500)
+    n_disk = n_disk or max(20, w * h // 5000)
+    yy, xx = np.mgrid[0:h, 0:w]
+    img = 60.0 + 80.0 * (xx / w) + 40.0 * np.sin(yy / 37.0)
+    for _ in range(n_rect):
+        rw, rh = rng.integers(6, 60, 2)
+        x0, y0 = rng.integers(-20, w), rng.integers(-20, h)
+        img[max(y0, 0):max(y0 + rh, 0), max(x0, 0):max(x0 + rw, 0)] = rng.uniform(0, 255)
+    for _ in range(n_disk):
+        r = rng.uniform(3, 25)
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        x0, x1 = int(max(cx - r, 0)), int(min(cx + r + 1, w))
+        y0, y1 = int(max(cy - r, 0)), int(min(cy + r + 1, h))
+        if x1 <= x0 or y1 <= y0:
+            continue
+        m = (xx[y0:y1, x0:x1] - cx) ** 2 + (yy[y0:y1, x0:x1] - cy) ** 2 <= r * r
+        img[y0:y1, x0:x1][m] = rng.uniform(0, 255)
+    img += rng.normal(0, 6.0, img.shape)
+    return img
+
+
+def make_image_pair(w: int = 1241, h: int = 376, *, seed: int = 0, shift=(7.0, 3.0), noise: float = 2.0):
+    """Two frames of one scene (KITTI-00 size by default): frame 2 is the scene
+    translated by `shift` pixels (integer part by cropping, so FAST corners
+    move exactly) with independent sensor noise. Returns (img1, img2) uint8."""
+    rng = np.random.default_rng(seed + 1)
+    pad = 16
+    scene = make_scene(w + 2 * pad, h + 2 * pad, seed=seed)
+    sx, sy = int(round(shift[0])), int(round(shift[1]))
+    a = scene[pad:pad + h, pad:pad + w] + rng.normal(0, noise, (h, w))
+    b = scene[pad - sy:pad - sy + h, pad - sx:pad - sx + w] + rng.normal(0, noise, (h, w))
+    return (np.clip(np.rint(a), 0, 255).astype(np.uint8), np.clip(np.rint(b), 0, 255).astype(np.uint8))

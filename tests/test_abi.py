@@ -24,9 +24,15 @@ def test_capture_header_and_binding_agree():
     assert declared == set(_lib.CAPTURE_EXPORTS), declared ^ set(_lib.CAPTURE_EXPORTS)
 
 
+def test_orb_header_and_binding_agree():
+    hdr = open(os.path.join(ROOT, "include", "sqrtlm_orb.h")).read()
+    declared = set(re.findall(r"\b(sqlm_[A-Za-z0-9_]+)\s*\(", hdr))
+    assert declared == set(_lib.ORB_EXPORTS), declared ^ set(_lib.ORB_EXPORTS)
+
+
 def test_library_exports_every_symbol():
     L = _lib.lib()
-    for s in _lib.EXPORTS + _lib.CAPTURE_EXPORTS:
+    for s in _lib.EXPORTS + _lib.CAPTURE_EXPORTS + _lib.ORB_EXPORTS:
         assert hasattr(L, s), s
     assert b"gfx950" in L.sqlm_version()
     assert L.sqlm_status_string(-8) == b"problem shape not supported by this build"

@@ -1,0 +1,316 @@
+"""Pins of the ORB oracle (oracle/orb_ref.c) by independent restatements.
+
+OpenCV is absent here and the reference ships no ORB fixtures, so the
+OpenCV-implemented stages (resize, GaussianBlur, FAST) are parity UNPINNED
+against the reference binary (oracle/orb_ref.h); they are pinned below by
+their defining properties (FAST: the 9-of-16 arc definition and the score as
+the largest threshold that keeps the corner; resize / blur: within one grey
+level of the exact bilinear / Gaussian filter). The stages the reference
+implements itself (IC_Angle, steered BRIEF, Hamming distance, quadtree,
+SearchForInitialization) are checked against direct numpy / Python
+transliterations of the reference source, and the whole extractor output is
+frozen in tests/golden/orb_golden.npz."""
+import os
+
+import numpy as np
+import pytest
+
+from sqrtlm import synth
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "orb_golden.npz")
+CIRCLE = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
+          (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+@pytest.fixture(scope="module")
+def OB(oracle):
+    from oracle import orb
+    return orb
+
+
+def test_level_geometry(OB):
+    lw, lh, nf, sc = OB.levels(OB.params(), 1241, 376)
+    assert list(lw) == [1241, 1034, 862, 718, 598, 499, 416, 346]
+    assert list(lh) == [376, 313, 261, 218, 181, 151, 126, 105]
+    assert nf.sum() == 2000 and list(nf[:3]) == [434, 362, 302]
+    np.testing.assert_allclose(sc, 1.2 ** np.arange(8), rtol=1e-6)
+
+
+def test_gauss_kernel(OB):
+    k = OB.gauss_kernel()  # getGaussianKernel(7, 2) x 256: 18 34 49 55 49 34 18
+    assert list(k) == [18, 34, 49, 55, 49, 34, 18]
+
+
+def test_hamming_matches_popcount(OB):
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        a, b = rng.integers(0, 256, (2, 32), dtype=np.uint8)
+        assert OB.hamming(a, b) == int(np.unpackbits(a ^ b).sum())
+
+
+def _brute_fast(img, th):
+    """9-contiguous-of-16 definition; score = max over arcs of min |d| - 1."""
+    h, w = img.shape
+    I = img.astype(int)
+    score = np.zeros((h, w), int)
+    for y in range(3, h - 3):
+        for x in range(3, w - 3):
+            v = I[y, x]
+            d = np.array([v - I[y + dy, x + dx] for dx, dy in CIRCLE])
+            best = -1
+            for s in range(16):
+                arc = d[[(s + k) % 16 for k in range(9)]]
+                best = max(best, arc.min() - 1, (-arc).min() - 1)
+            if best >= th:
+                score[y, x] = best
+    return score
+
+
+def test_fast_against_definition(OB):
+    img, _ = synth.make_image_pair(90, 70, seed=2)
+    for th in (7, 20):
+        kps = OB.fast(img, th)
+        score = _brute_fast(img, th)
+        exp = []
+        h, w = img.shape
+        for y in range(3, h - 3):
+            for x in range(3, w - 3):
+                s = score[y, x]
+                if s and all(s > score[y + dy, x + dx] for dy in (-1, 0, 1) for dx in (-1, 0, 1) if dy or dx):
+                    exp.append((x, y, s))
+        got = [(int(k["x"]), int(k["y"]), int(k["response"])) for k in kps]
+        assert got == exp and len(got) > 5
+
+
+def test_resize_close_to_bilinear(OB):
+    img, _ = synth.make_image_pair(300, 200, seed=3)
+    out = OB.resize(img, 250, 167)
+    sx, sy = 300 / 250, 200 / 167
+    fx = (np.arange(250) + 0.5) * sx - 0.5
+    fy = (np.arange(167) + 0.5) * sy - 0.5
+    x0 = np.clip(np.floor(fx).astype(int), 0, 298)
+    y0 = np.clip(np.floor(fy).astype(int), 0, 198)
+    ax = np.clip(fx - x0, 0, 1)[None, :]
+    ay = np.clip(fy - y0, 0, 1)[:, None]
+    I = img.astype(float)
+    ref = ((1 - ay) * ((1 - ax) * I[y0][:, x0] + ax * I[y0][:, x0 + 1]) +
+           ay * ((1 - ax) * I[y0 + 1][:, x0] + ax * I[y0 + 1][:, x0 + 1]))
+    assert np.abs(out.astype(float) - ref).max() <= 1.0
+
+
+def test_blur_close_to_gaussian(OB):
+    img, _ = synth.make_image_pair(120, 90, seed=4)
+    out = OB.blur(img)
+    x = np.arange(7) - 3.0
+    g = np.exp(-x * x / 8.0)
+    g /= g.sum()
+    P = np.pad(img.astype(float), 3, mode="reflect")  # numpy "reflect" = BORDER_REFLECT_101
+    R = sum(g[i] * P[:, i:i + 120] for i in range(7))
+    ref = sum(g[i] * R[i:i + 90, :] for i in range(7))
+    assert np.abs(out.astype(float) - ref).max() <= 2.5  # the x256 integer taps sum to 257
+    # exactly the integer-tap filter, rounded to nearest (ties either way)
+    ik = OB.gauss_kernel().astype(np.int64)
+    Pi = np.pad(img.astype(np.int64), 3, mode="reflect")
+    Ri = sum(ik[i] * Pi[:, i:i + 120] for i in range(7))
+    N = sum(ik[i] * Ri[i:i + 90, :] for i in range(7))
+    assert np.abs(out.astype(float) - np.minimum(N / 65536.0, 255.0)).max() <= 0.5
+
+
+def _umax():
+    import math
+    umax = [0] * 16
+    vmax = math.floor(15 * math.sqrt(2) / 2 + 1)
+    vmin = math.ceil(15 * math.sqrt(2) / 2)
+    for v in range(vmax + 1):
+        umax[v] = int(np.rint(math.sqrt(225 - v * v)))
+    v0 = 0
+    for v in range(15, vmin - 1, -1):
+        while umax[v0] == umax[v0 + 1]:
+            v0 += 1
+        umax[v] = v0
+        v0 += 1
+    return umax
+
+
+def test_ic_angle_is_intensity_centroid(OB):
+    img, _ = synth.make_image_pair(200, 120, seed=5)
+    umax = _umax()
+    I = img.astype(np.int64)
+    for (x, y) in [(40, 40), (100, 60), (150, 80), (77, 33)]:
+        m10 = m01 = 0
+        for v in range(-15, 16):
+            d = umax[abs(v)]
+            for u in range(-d, d + 1):
+                m10 += u * I[y + v, x + u]
+                m01 += v * I[y + v, x + u]
+        ang = OB.ic_angle(img, x, y)
+        exact = np.degrees(np.arctan2(m01, m10)) % 360.0
+        diff = abs((ang - exact + 180.0) % 360.0 - 180.0)
+        assert diff < 0.02  # fastAtan2 polynomial accuracy
+
+
+def test_fast_atan2_quadrants(OB):
+    for y, x in [(1, 1), (1, -1), (-1, -1), (-1, 1), (0, 1), (1, 0), (3, 7), (-7, 3)]:
+        ref = np.degrees(np.arctan2(y, x)) % 360.0
+        assert abs((OB.fast_atan2(y, x) - ref + 180) % 360 - 180) < 0.02
+
+
+def _pattern():
+    import re
+    txt = open(os.path.join(os.path.dirname(GOLDEN), "..", "..", "oracle", "orb_pattern.h")).read()
+    body = txt[txt.index("{") + 1:txt.index("};")]
+    vals = [int(v) for v in re.findall(r"-?\d+", body)]
+    assert len(vals) == 1024
+    return vals
+
+
+def test_descriptor_matches_steered_brief(OB):
+    pattern = _pattern()
+    img, _ = synth.make_image_pair(160, 120, seed=6)
+    I = img.astype(int)
+    for (x, y, ang) in [(50, 50, 0.0), (80, 60, 37.5), (100, 70, 211.25), (60, 40, 359.0)]:
+        kp = np.zeros(1, OB.KP_DTYPE)
+        kp["x"], kp["y"], kp["angle"] = x, y, ang
+        d = OB.describe(img, kp)
+        angle = np.float32(np.float32(ang) * np.float32(np.pi / 180.0))
+        a, b = np.float32(np.cos(np.float64(angle))), np.float32(np.sin(np.float64(angle)))
+        bits = []
+        for i in range(256):
+            x0, y0, x1, y1 = (np.float32(v) for v in pattern[4 * i:4 * i + 4])
+            t0 = I[y + int(np.rint(x0 * b + y0 * a)), x + int(np.rint(x0 * a - y0 * b))]
+            t1 = I[y + int(np.rint(x1 * b + y1 * a)), x + int(np.rint(x1 * a - y1 * b))]
+            bits.append(int(t0 < t1))
+        exp = np.packbits(np.array(bits, np.uint8).reshape(32, 8), axis=1, bitorder="little").ravel()
+        np.testing.assert_array_equal(d, exp)
+
+
+def test_distribute_invariants(OB):
+    rng = np.random.default_rng(7)
+    n = 3000
+    keys = np.zeros(n, OB.KP_DTYPE)
+    keys["x"] = rng.integers(0, 1209, n)
+    keys["y"] = rng.integers(0, 344, n)
+    keys["response"] = rng.integers(7, 120, n)
+    for N in (50, 434, 2000):
+        out = OB.distribute(keys, 16, 1225, 16, 360, N)
+        assert N <= len(out) <= N + 3 * 64 or len(out) == n
+        src = set(zip(keys["x"].tolist(), keys["y"].tolist(), keys["response"].tolist()))
+        assert all((k["x"], k["y"], k["response"]) in src for k in out)
+    out = OB.distribute(keys[:1], 16, 1225, 16, 360, 10)
+    assert len(out) == 1
+    assert len(OB.distribute(keys[:0], 16, 1225, 16, 360, 10)) == 0
+
+
+def _py_search_for_init(k1, d1, k2, d2, grid, prev, window, nnratio, check_ori):
+    """Direct transliteration of ORBmatcher::SearchForInitialization
+    (ORBmatcher.cc:573-718) with Frame::GetFeaturesInArea / PosInGrid."""
+    import math
+    f32 = np.float32
+    minx, maxx, miny, maxy = (f32(v) for v in grid)
+    wi, hi = f32(64) / (maxx - minx), f32(48) / (maxy - miny)
+    cells = [[[] for _ in range(48)] for _ in range(64)]
+    for i in range(len(k2)):
+        px = math.floor(float((f32(k2["x"][i]) - minx) * wi) + 0.5)
+        py = math.floor(float((f32(k2["y"][i]) - miny) * hi) + 0.5)
+        if 0 <= px < 64 and 0 <= py < 48:
+            cells[px][py].append(i)
+    D = np.unpackbits(d1[:, None, :] ^ d2[None, :, :], axis=2).sum(axis=2)
+    m12 = [-1] * len(k1)
+    vmd = [2 ** 31 - 1] * len(k2)
+    m21 = [-1] * len(k2)
+    hist = [[] for _ in range(30)]
+    n = 0
+    r = f32(window)
+    for i1 in range(len(k1)):
+        if k1["octave"][i1] > 0:
+            continue
+        x, y = f32(prev[i1, 0]), f32(prev[i1, 1])
+        x0 = max(0, math.floor((x - minx - r) * wi))
+        x1 = min(63, math.ceil((x - minx + r) * wi))
+        y0 = max(0, math.floor((y - miny - r) * hi))
+        y1 = min(47, math.ceil((y - miny + r) * hi))
+        if x0 >= 64 or x1 < 0 or y0 >= 48 or y1 < 0:
+            continue
+        cand = [j for ix in range(x0, x1 + 1) for iy in range(y0, y1 + 1) for j in cells[ix][iy]
+                if k2["octave"][j] == 0 and abs(f32(k2["x"][j]) - x) < r and abs(f32(k2["y"][j]) - y) < r]
+        if not cand:
+            continue
+        b1 = b2 = 2 ** 31 - 1
+        bi = -1
+        for j in cand:
+            dist = int(D[i1, j])
+            if vmd[j] <= dist:
+                continue
+            if dist < b1:
+                b2, b1, bi = b1, dist, j
+            elif dist < b2:
+                b2 = dist
+        if b1 <= 50 and b1 < f32(b2) * f32(nnratio):
+            if m21[bi] >= 0:
+                m12[m21[bi]] = -1
+                n -= 1
+            m12[i1], m21[bi], vmd[bi] = bi, i1, b1
+            n += 1
+            if check_ori:
+                rot = f32(k1["angle"][i1]) - f32(k2["angle"][bi])
+                if rot < 0:
+                    rot = f32(rot + f32(360))
+                v = float(rot * (f32(30) / f32(360)))
+                b = int(math.floor(v + 0.5))
+                hist[0 if b == 30 else b].append(i1)
+    if check_ori:
+        sizes = [len(h) for h in hist]
+        m1 = m2 = m3 = 0
+        i1_ = i2_ = i3_ = -1
+        for i, s in enumerate(sizes):
+            if s > m1:
+                m3, m2, m1, i3_, i2_, i1_ = m2, m1, s, i2_, i1_, i
+            elif s > m2:
+                m3, m2, i3_, i2_ = m2, s, i2_, i
+            elif s > m3:
+                m3, i3_ = s, i
+        if f32(m2) < f32(0.1) * f32(m1):
+            i2_ = i3_ = -1
+        elif f32(m3) < f32(0.1) * f32(m1):
+            i3_ = -1
+        for i in range(30):
+            if i in (i1_, i2_, i3_):
+                continue
+            for idx in hist[i]:
+                if m12[idx] >= 0:
+                    m12[idx] = -1
+                    n -= 1
+    return n, np.array(m12, np.int32)
+
+
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_for_init_matches_transliteration(OB, check_ori):
+    a, b = synth.make_image_pair(640, 300, seed=12, shift=(5.0, 2.0))
+    p = OB.params(800)
+    k1, d1 = OB.extract(p, a)
+    k2, d2 = OB.extract(p, b)
+    prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1), np.float32)
+    grid = (0.0, 640.0, 0.0, 300.0)
+    n, m12, pr = OB.search_for_init(k1, d1, k2, d2, grid, prev, 100, 0.9, check_ori)
+    n_py, m_py = _py_search_for_init(k1, d1, k2, d2, grid, prev, 100, 0.9, check_ori)
+    assert n == n_py and n > 20
+    np.testing.assert_array_equal(m12, m_py)
+    ok = m12 >= 0
+    np.testing.assert_array_equal(pr[ok, 0], k2["x"][m12[ok]])
+
+
+def test_golden_extract_and_match(OB):
+    g = np.load(GOLDEN)
+    a, b = synth.make_image_pair(640, 300, seed=int(g["seed"]), shift=tuple(g["shift"]))
+    p = OB.params(800)
+    k1, d1 = OB.extract(p, a)
+    k2, d2 = OB.extract(p, b)
+    np.testing.assert_array_equal(np.asarray(a), g["img1"])
+    for f in OB.KP_DTYPE.names:
+        np.testing.assert_array_equal(k1[f], g["k1_" + f])
+    np.testing.assert_array_equal(d1, g["d1"])
+    np.testing.assert_array_equal(d2, g["d2"])
+    prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1), np.float32)
+    n, m12, _ = OB.search_for_init(k1, d1, k2, d2, (0.0, 640.0, 0.0, 300.0), prev, 100, 0.9, True)
+    assert n == int(g["n_matches"])
+    np.testing.assert_array_equal(m12, g["m12"])
