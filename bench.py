@@ -209,12 +209,94 @@ def bench_eg(args, world):
         dist.destroy_process_group()
 
 
+def bench_orb(args, world):
+    """ORB front end (SURVEY.md §8 f3): ORBextractor::operator() on a
+    KITTI-00-size synthetic grey frame (1241x376, cfg/KITTI00-02.yaml: 2000
+    features, 1.2, 8 levels, FAST 20/7). A step is one frame, image already in
+    HBM, including the host quadtree step and the keypoint / descriptor D2H.
+    Replicas only (one camera stream per GPU)."""
+    from sqrtlm import synth
+    from sqrtlm.optimizer import Context
+    from sqrtlm.orb import ORBextractor
+    img, _ = synth.make_image_pair(1241, 376, seed=3)
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+    with Context(local_rank) as ctx:
+        ex = ORBextractor(2000, 1.2, 8, 20, 7, ctx=ctx)
+        for _ in range(max(1, args.warmup)):
+            kps, _d = ex(img)
+        if world > 1:
+            dist.barrier()
+        reps = max(50, args.steps * 10)
+        ms, stages = ex.bench(img, reps)
+        # algorithmic bytes of k_orb_fast per launch: every cell view it stages
+        # (overlapping 30-px cells + 6-px overlap) + 4 B per candidate + 4 B count
+        from oracle import orb as OB  # geometry only: the same cell loop as the reference
+        lw, lh, _, _ = OB.levels(OB.params(), 1241, 376)
+        view_bytes = 0
+        ncell = 0
+        for w, h in zip(lw.tolist(), lh.tolist()):
+            width, height = float(w - 32), float(h - 32)
+            nc, nr = int(width / 30), int(height / 30)
+            wc, hc = int(np.ceil(np.float32(width) / nc)), int(np.ceil(np.float32(height) / nr))
+            for i in range(nr):
+                y0 = 16 + i * hc
+                if y0 >= h - 16 - 3:
+                    continue
+                for j in range(nc):
+                    x0 = 16 + j * wc
+                    if x0 >= w - 16 - 3:
+                        continue
+                    view_bytes += (min(x0 + wc + 6, w - 16) - x0) * (min(y0 + hc + 6, h - 16) - y0)
+                    ncell += 1
+        OB.build()
+        _k, _d, pyr = OB.extract(OB.params(), img, with_levels=True)
+        ncand = sum(len(OB.level_candidates(OB.params(), lev)) for lev in pyr)
+    if world > 1:
+        import torch
+        tt = torch.tensor([ms], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        ms = float(tt.item())
+    if rank == 0:
+        alg = int(view_bytes) + 4 * int(ncand) + 4 * int(ncell)
+        t_fast = stages[1]
+        out = {"metric": "frames/sec (ORB extraction, KITTI-00 frame)", "value": world * 1000.0 / ms,
+               "unit": "frames/s", "n_gpus": world, "steps": reps, "warmup": args.warmup, "ms_per_step": ms,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+               "data": "synthetic grey frame (repo scene generator, seed 3)",
+               "config": {"workload": "ORBextractor 1241x376, 2000 features, 8 levels", "keypoints": int(len(kps)),
+                          "parallelism": f"replicas x{world}"},
+               "stage_ms": dict(zip(["pyramid", "fast", "compact", "blur", "describe", "host_quadtree"], stages)),
+               "roofline": {"bound": "hbm", "kernel": "k_orb_fast", "algorithmic_bytes": alg,
+                            "achieved": alg / (t_fast * 1e-3) / 1e9 if t_fast > 0 else 0.0, "peak": HBM_PEAK_GBPS,
+                            "unit": "GB/s", "traffic": None, "launch_ms": t_fast,
+                            "note": "one launch per frame over all 30-px cells of all levels; latency-bound"}}
+        out["roofline"]["frac"] = out["roofline"]["achieved"] / HBM_PEAK_GBPS
+        if not args.no_cpu_baseline and world == 1:
+            OB.build()
+            p = OB.params()
+            t0 = time.perf_counter()
+            nf = 0
+            while time.perf_counter() - t0 < 5.0:
+                OB.extract(p, img)
+                nf += 1
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": nf / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+                                   "sample": f"{nf} extractions of the same frame, single thread, {dt:.1f} s"}
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["gba", "lba", "eg"], default="gba")
+    ap.add_argument("--config", choices=["gba", "lba", "eg", "orb"], default="gba")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink config 4 (parity / debugging only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -224,6 +306,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.config == "eg":
         return bench_eg(args, world)
+    if args.config == "orb":
+        return bench_orb(args, world)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None

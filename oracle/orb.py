@@ -9,7 +9,7 @@ import ctypes as C
 
 import numpy as np
 
-from .oracle import _p, lib
+from .oracle import _p, build, lib  # noqa: F401 (build re-exported)
 
 # cv::KeyPoint fields the reference uses (orc_kp / sqlm_keypoint layout)
 KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),

@@ -52,6 +52,8 @@ int orc_orb_levels(const orc_orb_params *p, int cols, int rows, int *lw, int *lh
   /* the cell grid needs at least one 30-pixel cell per axis on every level */
   for (int i = 0; i < L; ++i)
     if (lw[i] - 2 * (EDGE_THRESHOLD - 3) < 30 || lh[i] - 2 * (EDGE_THRESHOLD - 3) < 30) return -2;
+  for (int i = 0; i < L; ++i) /* DistributeOctTree needs round(width / height) >= 1 */
+    if ((int)roundf((float)(lw[i] - 2 * (EDGE_THRESHOLD - 3)) / (lh[i] - 2 * (EDGE_THRESHOLD - 3))) < 1) return -3;
   return 0;
 }
 

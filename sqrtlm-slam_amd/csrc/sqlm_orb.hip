@@ -40,7 +40,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
-#include <list>
+#include <thread>
 #include <vector>
 
 #include "../../include/sqrtlm_orb.h"
@@ -549,130 +549,169 @@ struct Cand {
   float x, y, response;
 };
 
-struct ExtractorNode {
-  int ulx = 0, uly = 0, urx = 0, ury = 0, blx = 0, bly = 0, brx = 0, bry = 0;
-  std::vector<Cand> keys;
-  bool no_more = false;
-  std::list<ExtractorNode>::iterator self;
+// Node pool + index-linked list with the reference's std::list semantics
+// (push_front, erase-returns-next, iterator kept per expandable node); each
+// node owns a contiguous slice of a key-index arena, children are filled by a
+// stable 4-way partition, so key order inside a node is the reference's.
+struct QNode {
+  int ulx, uly, urx, ury, blx, bly, brx, bry;
+  int koff, kcnt;
+  int prev, next;
+  bool no_more;
 };
 
-void divide_node(const ExtractorNode &p, ExtractorNode &n1, ExtractorNode &n2, ExtractorNode &n3,
-                 ExtractorNode &n4) {
-  const int halfX = (int)std::ceil(static_cast<float>(p.urx - p.ulx) / 2);
-  const int halfY = (int)std::ceil(static_cast<float>(p.bry - p.uly) / 2);
-  n1.ulx = p.ulx; n1.uly = p.uly;
-  n1.urx = p.ulx + halfX; n1.ury = p.uly;
-  n1.blx = p.ulx; n1.bly = p.uly + halfY;
-  n1.brx = p.ulx + halfX; n1.bry = p.uly + halfY;
-  n2.ulx = n1.urx; n2.uly = n1.ury;
-  n2.urx = p.urx; n2.ury = p.ury;
-  n2.blx = n1.brx; n2.bly = n1.bry;
-  n2.brx = p.urx; n2.bry = p.uly + halfY;
-  n3.ulx = n1.blx; n3.uly = n1.bly;
-  n3.urx = n1.brx; n3.ury = n1.bry;
-  n3.blx = p.blx; n3.bly = p.bly;
-  n3.brx = n1.brx; n3.bry = p.bly;
-  n4.ulx = n3.urx; n4.uly = n3.ury;
-  n4.urx = n2.brx; n4.ury = n2.bry;
-  n4.blx = n3.brx; n4.bly = n3.bry;
-  n4.brx = p.brx; n4.bry = p.bry;
-  for (const Cand &k : p.keys) {
-    if (k.x < n1.urx) (k.y < n1.bry ? n1 : n3).keys.push_back(k);
-    else (k.y < n1.bry ? n2 : n4).keys.push_back(k);
+struct QuadTree {
+  std::vector<QNode> pool;
+  std::vector<int> arena;  // key indices
+  std::vector<uint8_t> tag;
+  int head = -1, size = 0;
+
+  void push_front(int n) {
+    pool[n].prev = -1;
+    pool[n].next = head;
+    if (head >= 0) pool[head].prev = n;
+    head = n;
+    ++size;
   }
-  n1.no_more = n1.keys.size() == 1;
-  n2.no_more = n2.keys.size() == 1;
-  n3.no_more = n3.keys.size() == 1;
-  n4.no_more = n4.keys.size() == 1;
-}
+  int erase(int n) {
+    const int nx = pool[n].next, pv = pool[n].prev;
+    if (pv >= 0) pool[pv].next = nx;
+    else head = nx;
+    if (nx >= 0) pool[nx].prev = pv;
+    --size;
+    return nx;
+  }
+  // ExtractorNode::DivideNode (ORBextractor.cc:606-690): children c[0..3] = n1..n4
+  void divide(int pi, const std::vector<Cand> &keys, int c[4]) {
+    const QNode p = pool[pi];
+    const int halfX = (int)std::ceil(static_cast<float>(p.urx - p.ulx) / 2);
+    const int halfY = (int)std::ceil(static_cast<float>(p.bry - p.uly) / 2);
+    QNode n[4];
+    n[0] = QNode{p.ulx, p.uly, p.ulx + halfX, p.uly, p.ulx, p.uly + halfY, p.ulx + halfX, p.uly + halfY,
+                 0, 0, -1, -1, false};
+    n[1] = QNode{n[0].urx, n[0].ury, p.urx, p.ury, n[0].brx, n[0].bry, p.urx, p.uly + halfY, 0, 0, -1, -1, false};
+    n[2] = QNode{n[0].blx, n[0].bly, n[0].brx, n[0].bry, p.blx, p.bly, n[0].brx, p.bly, 0, 0, -1, -1, false};
+    n[3] = QNode{n[2].urx, n[2].ury, n[1].brx, n[1].bry, n[2].brx, n[2].bry, p.brx, p.bry, 0, 0, -1, -1, false};
+    int cnt[4] = {0, 0, 0, 0};
+    if ((int)tag.size() < p.kcnt) tag.resize(p.kcnt);
+    for (int i = 0; i < p.kcnt; ++i) {
+      const Cand &k = keys[arena[p.koff + i]];
+      const int t = k.x < n[0].urx ? (k.y < n[0].bry ? 0 : 2) : (k.y < n[0].bry ? 1 : 3);
+      tag[i] = (uint8_t)t;
+      ++cnt[t];
+    }
+    int pos[4];
+    int base = (int)arena.size();
+    for (int t = 0; t < 4; ++t) {
+      n[t].koff = base;
+      n[t].kcnt = cnt[t];
+      n[t].no_more = cnt[t] == 1;
+      pos[t] = base;
+      base += cnt[t];
+    }
+    arena.resize(base);
+    for (int i = 0; i < p.kcnt; ++i) arena[pos[tag[i]]++] = arena[p.koff + i];
+    for (int t = 0; t < 4; ++t) {
+      c[t] = (int)pool.size();
+      pool.push_back(n[t]);
+    }
+  }
+};
 
 std::vector<Cand> distribute_quadtree(const std::vector<Cand> &keys, int minX, int maxX, int minY, int maxY, int N) {
   const int nIni = (int)std::round(static_cast<float>(maxX - minX) / (maxY - minY));
   const float hX = static_cast<float>(maxX - minX) / nIni;
-  std::list<ExtractorNode> nodes;
-  std::vector<ExtractorNode *> ini(nIni);
+  QuadTree T;
+  T.pool.reserve(4 * keys.size() + nIni + 16);
+  T.arena.reserve(keys.size() * 6 + 16);
+  // initial nodes (lNodes.push_back in order) and their keys in input order
+  std::vector<int> which(keys.size()), cnt(nIni, 0);
+  for (size_t i = 0; i < keys.size(); ++i) {
+    which[i] = (int)(size_t)(keys[i].x / hX);
+    ++cnt[which[i]];
+  }
+  std::vector<int> pos(nIni);
+  int base = 0;
   for (int i = 0; i < nIni; i++) {
-    ExtractorNode ni;
-    ni.ulx = (int)(hX * static_cast<float>(i));
-    ni.urx = (int)(hX * static_cast<float>(i + 1));
+    QNode ni{(int)(hX * static_cast<float>(i)), 0, (int)(hX * static_cast<float>(i + 1)), 0, 0, maxY - minY, 0,
+             maxY - minY, base, cnt[i], -1, -1, false};
     ni.blx = ni.ulx;
-    ni.bly = maxY - minY;
     ni.brx = ni.urx;
-    ni.bry = maxY - minY;
-    nodes.push_back(std::move(ni));
-    ini[i] = &nodes.back();
+    pos[i] = base;
+    base += cnt[i];
+    T.pool.push_back(ni);
   }
-  for (const Cand &k : keys) ini[(size_t)(k.x / hX)]->keys.push_back(k);
-  for (auto it = nodes.begin(); it != nodes.end();) {
-    if (it->keys.size() == 1) {
-      it->no_more = true;
-      ++it;
-    } else if (it->keys.empty())
-      it = nodes.erase(it);
+  T.arena.resize(base);
+  for (size_t i = 0; i < keys.size(); ++i) T.arena[pos[which[i]]++] = (int)i;
+  for (int i = nIni - 1; i >= 0; --i) T.push_front(i);
+  for (int it = T.head; it >= 0;) {
+    if (T.pool[it].kcnt == 1) {
+      T.pool[it].no_more = true;
+      it = T.pool[it].next;
+    } else if (T.pool[it].kcnt == 0)
+      it = T.erase(it);
     else
-      ++it;
+      it = T.pool[it].next;
   }
-  std::vector<std::pair<int, ExtractorNode *>> expand;
-  auto push_children = [&](ExtractorNode *c[4], int *n_to_expand) {
+  std::vector<std::pair<int, int>> expand, prev;  // (size, node)
+  auto push_children = [&](const int c[4], int *n_to_expand) {
     for (int k = 0; k < 4; ++k) {
-      if (c[k]->keys.empty()) continue;
-      nodes.push_front(std::move(*c[k]));
-      if (nodes.front().keys.size() > 1) {
+      if (T.pool[c[k]].kcnt == 0) continue;
+      T.push_front(c[k]);
+      if (T.pool[c[k]].kcnt > 1) {
         if (n_to_expand) ++*n_to_expand;
-        expand.emplace_back((int)nodes.front().keys.size(), &nodes.front());
-        nodes.front().self = nodes.begin();
+        expand.emplace_back(T.pool[c[k]].kcnt, c[k]);
       }
     }
   };
   bool finish = false;
   while (!finish) {
-    int prev_size = (int)nodes.size();
+    int prev_size = T.size;
     int n_to_expand = 0;
     expand.clear();
-    for (auto it = nodes.begin(); it != nodes.end();) {
-      if (it->no_more) {
-        ++it;
+    for (int it = T.head; it >= 0;) {
+      if (T.pool[it].no_more) {
+        it = T.pool[it].next;
         continue;
       }
-      ExtractorNode n1, n2, n3, n4;
-      divide_node(*it, n1, n2, n3, n4);
-      ExtractorNode *c[4] = {&n1, &n2, &n3, &n4};
+      int c[4];
+      T.divide(it, keys, c);
       push_children(c, &n_to_expand);
-      it = nodes.erase(it);
+      it = T.erase(it);
     }
-    if ((int)nodes.size() >= N || (int)nodes.size() == prev_size) {
+    if (T.size >= N || T.size == prev_size) {
       finish = true;
-    } else if ((int)nodes.size() + n_to_expand * 3 > N) {
+    } else if (T.size + n_to_expand * 3 > N) {
       while (!finish) {
-        prev_size = (int)nodes.size();
-        std::vector<std::pair<int, ExtractorNode *>> prev = expand;
+        prev_size = T.size;
+        prev = expand;
         expand.clear();
         std::stable_sort(prev.begin(), prev.end(),
-                         [](const std::pair<int, ExtractorNode *> &a, const std::pair<int, ExtractorNode *> &b) {
-                           return a.first < b.first;
-                         });
+                         [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return a.first < b.first; });
         for (int j = (int)prev.size() - 1; j >= 0; j--) {
-          ExtractorNode n1, n2, n3, n4;
-          divide_node(*prev[j].second, n1, n2, n3, n4);
-          ExtractorNode *c[4] = {&n1, &n2, &n3, &n4};
+          int c[4];
+          T.divide(prev[j].second, keys, c);
           push_children(c, nullptr);
-          nodes.erase(prev[j].second->self);
-          if ((int)nodes.size() >= N) break;
+          T.erase(prev[j].second);
+          if (T.size >= N) break;
         }
-        if ((int)nodes.size() >= N || (int)nodes.size() == prev_size) finish = true;
+        if (T.size >= N || T.size == prev_size) finish = true;
       }
     }
   }
   std::vector<Cand> out;
-  out.reserve(nodes.size());
-  for (const ExtractorNode &nd : nodes) {
-    const Cand *best = &nd.keys[0];
+  out.reserve(T.size);
+  for (int it = T.head; it >= 0; it = T.pool[it].next) {
+    const QNode &nd = T.pool[it];
+    const Cand *best = &keys[T.arena[nd.koff]];
     float max_resp = best->response;
-    for (size_t k = 1; k < nd.keys.size(); k++)
-      if (nd.keys[k].response > max_resp) {
-        best = &nd.keys[k];
-        max_resp = nd.keys[k].response;
+    for (int k = 1; k < nd.kcnt; k++) {
+      const Cand &c = keys[T.arena[nd.koff + k]];
+      if (c.response > max_resp) {
+        best = &c;
+        max_resp = c.response;
       }
+    }
     out.push_back(*best);
   }
   return out;
@@ -809,6 +848,9 @@ int OrbEngine::extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<
     lscale[i] = sf[i];
     if (lw[i] - 2 * (kEdge - 3) < 30 || lh[i] - 2 * (kEdge - 3) < 30 || lw[i] > 4096 || lh[i] > 4096)
       return SQLM_ERR_UNSUPPORTED;
+    // DistributeOctTree needs >= 1 initial node (round(width / height) >= 1)
+    if ((int)std::round(static_cast<float>(lw[i] - 2 * (kEdge - 3)) / (lh[i] - 2 * (kEdge - 3))) < 1)
+      return SQLM_ERR_UNSUPPORTED;
     loff[i + 1] = loff[i] + lw[i] * lh[i];
   }
   std::vector<int> nfeat(L);
@@ -900,8 +942,8 @@ int OrbEngine::extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<
   if (hipEventSynchronize(ev_copy) != hipSuccess) return SQLM_ERR_HIP;
   // quadtree per level (host)
   const auto t0 = std::chrono::steady_clock::now();
-  std::vector<OrbDescIn> hin;
-  for (int l = 0; l < L; ++l) {
+  std::vector<std::vector<Cand>> sel(L);
+  auto level_tree = [&](int l) {
     const int b = h_off[level_cell[l]], e = h_off[level_cell[l + 1]];
     std::vector<Cand> keys(e - b);
     for (int i = b; i < e; ++i) {
@@ -909,10 +951,17 @@ int OrbEngine::extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<
       keys[i - b] = Cand{(float)(v & 4095u), (float)((v >> 12) & 4095u), (float)(v >> 24)};
     }
     const int minB = kEdge - 3;
-    const std::vector<Cand> sel =
-        distribute_quadtree(keys, minB, lw[l] - kEdge + 3, minB, lh[l] - kEdge + 3, nfeat[l]);
-    for (const Cand &c : sel) hin.push_back(OrbDescIn{c.x + minB, c.y + minB, c.response, l});
+    sel[l] = distribute_quadtree(keys, minB, lw[l] - kEdge + 3, minB, lh[l] - kEdge + 3, nfeat[l]);
+  };
+  {  // levels are independent: level 0 (the largest) here, the others on helper threads
+    std::vector<std::thread> th;
+    for (int l = 1; l < L; ++l) th.emplace_back(level_tree, l);
+    level_tree(0);
+    for (auto &t : th) t.join();
   }
+  std::vector<OrbDescIn> hin;
+  for (int l = 0; l < L; ++l)
+    for (const Cand &c : sel[l]) hin.push_back(OrbDescIn{c.x + (kEdge - 3), c.y + (kEdge - 3), c.response, l});
   stage_ms[5] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   const int n = (int)hin.size();
   kps.resize(n);

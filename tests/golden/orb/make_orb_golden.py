@@ -1,13 +1,13 @@
-"""Freeze the ORB oracle's output (tests/golden/orb_golden.npz): one synthetic
+"""Freeze the ORB oracle's output (tests/golden/orb/orb_golden.npz): one synthetic
 640x300 image pair, extractor keypoints / descriptors (800 features) and the
 SearchForInitialization matches. The oracle is pinned by tests/test_orb_oracle.py;
-this file guards it against silent drift. Run: python tests/golden/make_orb_golden.py"""
+this file guards it against silent drift. Run: python tests/golden/orb/make_orb_golden.py"""
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 sys.path[:0] = [os.path.join(ROOT, "sqrtlm-slam_amd"), ROOT]
 
 from oracle import orb as OB  # noqa: E402

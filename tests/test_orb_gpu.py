@@ -28,7 +28,7 @@ def _cmp_kps(kg, kr):
         np.testing.assert_array_equal(kg[f], kr[f], err_msg=f)
 
 
-@pytest.mark.parametrize("seed,w,h", [(3, 1241, 376), (5, 640, 480), (9, 753, 301)])
+@pytest.mark.parametrize("seed,w,h", [(3, 1241, 376), (5, 640, 480), (9, 753, 301), (13, 480, 400)])
 def test_extract_bit_exact(extractor, orb_oracle, seed, w, h):
     img, _ = synth.make_image_pair(w, h, seed=seed)
     kg, dg = extractor(img)
@@ -66,6 +66,8 @@ def test_extract_rejects_too_small(extractor):
     from sqrtlm._lib import SqlmError
     with pytest.raises(SqlmError):
         extractor(np.zeros((120, 160), np.uint8))  # level 7 narrower than one 30-px cell
+    with pytest.raises(SqlmError):
+        extractor(np.zeros((900, 300), np.uint8))  # portrait: no initial quadtree node
 
 
 def test_match_bf(gpu_ctx, orb_oracle):

@@ -9,7 +9,7 @@ level of the exact bilinear / Gaussian filter). The stages the reference
 implements itself (IC_Angle, steered BRIEF, Hamming distance, quadtree,
 SearchForInitialization) are checked against direct numpy / Python
 transliterations of the reference source, and the whole extractor output is
-frozen in tests/golden/orb_golden.npz."""
+frozen in tests/golden/orb/orb_golden.npz."""
 import os
 
 import numpy as np
@@ -17,7 +17,7 @@ import pytest
 
 from sqrtlm import synth
 
-GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "orb_golden.npz")
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "orb", "orb_golden.npz")
 CIRCLE = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3), (-2, -2),
           (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
 
@@ -157,7 +157,7 @@ def test_fast_atan2_quadrants(OB):
 
 def _pattern():
     import re
-    txt = open(os.path.join(os.path.dirname(GOLDEN), "..", "..", "oracle", "orb_pattern.h")).read()
+    txt = open(os.path.join(os.path.dirname(GOLDEN), "..", "..", "..", "oracle", "orb_pattern.h")).read()
     body = txt[txt.index("{") + 1:txt.index("};")]
     vals = [int(v) for v in re.findall(r"-?\d+", body)]
     assert len(vals) == 1024
