@@ -110,6 +110,19 @@ def _gloo_allreduce(arr, op):
         arr[:] = t.numpy().astype(np.uint8)
 
 
+def _gloo_p2p(arr, peer, op):
+    """Host point-to-point for --comm host (sqlm_ctx_set_host_p2p)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(arr.view(np.uint8))
+    if op == "send":
+        dist.send(t, dst=peer)
+    elif op == "recv":
+        dist.recv(t, src=peer)
+    else:
+        dist.broadcast(t, src=peer)
+
+
 def reprojection_sse(p, q, t, X):
     """(sum ||obs - proj||^2, number of edges) at the given state; the RMSE
     over all shards is sqrt(sum sse / sum n)."""
@@ -330,7 +343,7 @@ def main():
         dist.broadcast(t, 0)
         ctx.set_comm(bytes(t.tolist()), rank, world)
     elif world > 1:
-        ctx.set_host_comm(rank, world, _gloo_allreduce)
+        ctx.set_host_comm(rank, world, _gloo_allreduce, _gloo_p2p)
     ctx.set_problem(local)
     ms, kms, st = ctx.bench(args.warmup, args.steps)
     sse, nres = reprojection_sse(local, *ctx.poses(), ctx.points())

@@ -179,6 +179,16 @@ int sqlm_ctx_set_comm(sqlm_ctx *ctx, const char *unique_id, int rank, int nranks
 #define SQLM_OP_MAX 1
 typedef int (*sqlm_allreduce_fn)(void *user, void *buf, int64_t count, int dtype, int op);
 int sqlm_ctx_set_host_comm(sqlm_ctx *ctx, int rank, int nranks, sqlm_allreduce_fn fn, void *user);
+/* Point-to-point half of the host transport (the per-trial gather of the
+ * reduced camera system to rank 0 and the broadcast of its solution):
+ * fn(user, buf, count, dtype, peer, op) with op SQLM_P2P_SEND (buf -> peer),
+ * SQLM_P2P_RECV (peer -> buf) or SQLM_P2P_BCAST (in place from root = peer).
+ * Required with sqlm_ctx_set_host_comm for nranks > 1; set it first. */
+#define SQLM_P2P_SEND 0
+#define SQLM_P2P_RECV 1
+#define SQLM_P2P_BCAST 2
+typedef int (*sqlm_p2p_fn)(void *user, void *buf, int64_t count, int dtype, int peer, int op);
+int sqlm_ctx_set_host_p2p(sqlm_ctx *ctx, sqlm_p2p_fn fn, void *user);
 
 /* Device-resident benchmarking hooks: time `n` LM iterations on the set
  * problem with data already in HBM (bench.py). Per-kernel averaged durations

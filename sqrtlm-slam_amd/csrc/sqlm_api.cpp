@@ -78,6 +78,11 @@ struct sqlm_ctx {
   // ---- comm ----
   Comm comm;
   // ---- essential graph (sqlm_eg.hip) ----
+  // sharded runs: every rank's nonzero S block-row range [lo, hi), the BSR
+  // row pointer (host), and on rank 0 the gather table into xstage
+  std::vector<int> sh_lo, sh_hi, s_row_host;
+  GatherTab gather;
+  bool need_maxdiag = false;
   EGSolver *eg = nullptr;
   OrbEngine *orb = nullptr;
   // ---- timing ----
@@ -125,7 +130,7 @@ enum BufId {
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
-  B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR
+  B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -535,7 +540,7 @@ int prepare(sqlm_ctx *c, int level) {
   }
   AL(B_S, 36 * (size_t)d.nnzb, d.S);
   AL(B_G, 6 * (size_t)nP, d.g);
-  AL(B_DX, 6 * (size_t)nP, d.dx);
+  AL(B_DX, 6 * (size_t)nP + 1, d.dx);
   if (c->cr.enabled) {
     const size_t nb = (size_t)c->cr.p * c->cr.n * c->cr.n;
     AL(B_CRD, nb, d.cr_D);
@@ -552,6 +557,45 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_SCAL, (size_t)kNScalars, d.scalars);
   AL(B_MAXD, 1, d.maxdiag);
   AL(B_FLAGS, 4, d.flags);
+  d.hdiag = nullptr;
+  d.xstage = nullptr;
+  if (c->comm.enabled()) {
+    AL(B_HDIAG, 6 * (size_t)nP, d.hdiag);
+    c->s_row_host = s_row;
+    // every rank's nonzero S rows: the free cameras its own edges (and, on
+    // rank 0, the LiDAR edges) touch; rank 0 stages the others' rows
+    int lo = nP, hi = 0;
+    for (int64_t o = 0; o < nE; ++o)
+      if (obs_camh[o] >= 0) { lo = std::min(lo, obs_camh[o]); hi = std::max(hi, obs_camh[o] + 1); }
+    for (int i = 0; i < nP; ++i)
+      if (lid_ptr[i + 1] > lid_ptr[i]) { lo = std::min(lo, i); hi = std::max(hi, i + 1); }
+    if (lo >= hi) lo = hi = 0;
+    const int R = c->comm.nranks, me = c->comm.rank;
+    if (R > kMaxRanks) return SQLM_ERR_UNSUPPORTED;
+    std::vector<int> rng(2 * R, 0);
+    rng[2 * me] = lo;
+    rng[2 * me + 1] = hi;
+    if (comm_allreduce_host(c->comm, rng.data(), 2 * R, SQLM_DT_I32, SQLM_OP_SUM, c->stream)) return SQLM_ERR_COMM;
+    c->sh_lo.assign(R, 0);
+    c->sh_hi.assign(R, 0);
+    for (int r = 0; r < R; ++r) { c->sh_lo[r] = rng[2 * r]; c->sh_hi[r] = rng[2 * r + 1]; }
+    GatherTab &t = c->gather;
+    t.n = 0;
+    int64_t off = 0;
+    for (int r = 1; r < R; ++r) {
+      const int a = c->sh_lo[r], b = c->sh_hi[r];
+      t.s_lo[t.n] = 36 * (int64_t)s_row[a];
+      t.s_hi[t.n] = 36 * (int64_t)s_row[b];
+      t.s_src[t.n] = off;
+      off += t.s_hi[t.n] - t.s_lo[t.n];
+      t.g_lo[t.n] = 6 * (int64_t)a;
+      t.g_hi[t.n] = 6 * (int64_t)b;
+      t.g_src[t.n] = off;
+      off += t.g_hi[t.n] - t.g_lo[t.n];
+      ++t.n;
+    }
+    if (me == 0) AL(B_XSTAGE, (size_t)std::max<int64_t>(off, 1), d.xstage);
+  }
 #undef UP
 #undef AL
   HIP_OK(hipMemsetAsync(d.partials, 0, sizeof(double) * kMaxPartials, c->stream));
@@ -608,8 +652,10 @@ int linearize(sqlm_ctx *c) {
   tmark(c, 0, true);
   tmark(c, 1, false);
   launch_camera_pass(d, c->stream);
-  if (c->comm.enabled()) {
-    if (comm_allreduce_hpp(c->comm, d, c->stream)) return SQLM_ERR_COMM;
+  if (c->comm.enabled() && c->need_maxdiag) {  // lambda_0 needs the summed pose diagonals
+    launch_pose_diag(d, c->stream);
+    if (comm_allreduce_dev(c->comm, d.hdiag, 6 * (int64_t)d.nP, SQLM_DT_F64, SQLM_OP_SUM, c->stream))
+      return SQLM_ERR_COMM;
     launch_pose_maxdiag(d, c->stream);
   }
   tmark(c, 1, true);
@@ -624,7 +670,7 @@ struct TrialOut {
 int reduce_and_fetch(sqlm_ctx *c, TrialOut &o) {
   DevProblem &d = c->d;
   launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream);
-  int s = comm_allreduce_scalars(c->comm, d.scalars, c->stream);
+  int s = comm_allreduce_scalars(c->comm, d.scalars, c->need_maxdiag, c->stream);
   if (s) return s;
   HIP_OK(hipMemcpyAsync(c->h_scalars, d.scalars, sizeof(double) * kNScalars, hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
@@ -656,11 +702,35 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
     launch_rcs_reduce(d, lambda, c->stream);
   }
   tmark(c, 8, true);
-  int s = comm_allreduce_rcs(c->comm, d, c->stream);
-  if (s) return s;
+  int s = 0;
+  const bool sharded = c->comm.enabled(), root = !sharded || c->comm.rank == 0;
+  if (sharded) {  // gather every rank's S / g rows on rank 0
+    std::vector<P2POp> ops;
+    if (root) {
+      const GatherTab &t = c->gather;
+      for (int k = 0; k < t.n; ++k) {
+        ops.push_back(P2POp{k + 1, false, d.xstage + t.s_src[k], t.s_hi[k] - t.s_lo[k], SQLM_DT_F64});
+        ops.push_back(P2POp{k + 1, false, d.xstage + t.g_src[k], t.g_hi[k] - t.g_lo[k], SQLM_DT_F64});
+      }
+    } else {
+      const int me = c->comm.rank, a = c->sh_lo[me], b = c->sh_hi[me];
+      const int64_t s0 = 36 * (int64_t)c->s_row_host[a], s1 = 36 * (int64_t)c->s_row_host[b];
+      ops.push_back(P2POp{0, true, d.S + s0, s1 - s0, SQLM_DT_F64});
+      ops.push_back(P2POp{0, true, d.g + 6 * (int64_t)a, 6 * (int64_t)(b - a), SQLM_DT_F64});
+    }
+    if (comm_group_p2p(c->comm, ops, c->stream)) return SQLM_ERR_COMM;
+    if (root) launch_gather_add(d, c->gather, c->stream);
+  }
   tmark(c, 4, false);
-  s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream) : launch_dense_solve(d, c->stream);
-  if (s) return s == -2 ? SQLM_ERR_HIP : SQLM_ERR_UNSUPPORTED;
+  if (root) {
+    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream) : launch_dense_solve(d, c->stream);
+    if (s) return s == -2 ? SQLM_ERR_HIP : SQLM_ERR_UNSUPPORTED;
+  }
+  if (sharded) {  // dx and the solve flag from rank 0
+    if (root) launch_flag_pack(d, false, c->stream);
+    if (comm_bcast_dev(c->comm, d.dx, 6 * (int64_t)d.nP + 1, SQLM_DT_F64, 0, c->stream)) return SQLM_ERR_COMM;
+    if (!root) launch_flag_pack(d, true, c->stream);
+  }
   tmark(c, 4, true);
   tmark(c, 5, false);
   launch_pose_update(d, lambda, c->stream);
@@ -697,12 +767,14 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
   Timer tt;
   for (int it = 0; it < iterations && !stopped(stop) && (result == 0 || bench); ++it) {
     Timer tl;
+    c->need_maxdiag = it == 0;
     int s = linearize(c);
     if (s) return s;
     double currentChi = 0.0;
     if (it == 0) {
       TrialOut o0{};
       s = reduce_and_fetch(c, o0);
+      c->need_maxdiag = false;
       if (s) return s;
       currentChi = o0.chi_cur;
       st->chi2_begin = currentChi;
@@ -1095,6 +1167,13 @@ void sqlm_pose_to_Tcw_f32(const double q[4], const double t[3], float T[16]) {
 int sqlm_ctx_set_host_comm(sqlm_ctx *c, int rank, int nranks, sqlm_allreduce_fn fn, void *user) {
   if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn)) return SQLM_ERR_INVALID_ARG;
   return comm_init_host(c->comm, rank, nranks, fn, user);
+}
+
+int sqlm_ctx_set_host_p2p(sqlm_ctx *c, sqlm_p2p_fn fn, void *user) {
+  if (!c || !fn) return SQLM_ERR_INVALID_ARG;
+  c->comm.host_p2p = fn;
+  c->comm.host_p2p_user = user;
+  return SQLM_OK;
 }
 
 int sqlm_comm_id_size(void) { return comm_id_size(); }

@@ -4,13 +4,18 @@
 // observations). The exchange steps are:
 //   setup (per optimize() call): union of the active pose set, max of the
 //     S block bandwidth  -> every rank builds the same camera index and the
-//     same banded S pattern;
-//   per LM iteration: sum of H_pp / b_p;
-//   per trial: sum of S and g, of the trial scalars (chi2, computeScale), max
-//     of the landmark diagonal.
+//     same banded S pattern; every rank's nonzero S row range;
+//   iteration 0: sum of the pose Hessian diagonals (lambda_0 = tau max diag);
+//   per trial: gather of every rank's S / g row range to rank 0 (point-to-
+//     point, all links of rank 0 in parallel), the solve on rank 0, broadcast
+//     of dx (+ the solve flag); sum of the trial scalars (chi2, computeScale);
+//     max of the landmark diagonal at iteration 0.
+// Rank r's landmarks only touch the cameras they observe, a contiguous window
+// of the trajectory, so its S rows are ~1/N of S: the gather moves each S
+// entry once (an all-reduce would move it twice, zeros included).
 // Everything else is local. Two transports share this interface: RCCL over
-// xGMI (production, one process per GPU), and a host callback (the caller's
-// own collective, e.g. torch.distributed gloo) used to test the sharded
+// xGMI (production, one process per GPU), and host callbacks (the caller's
+// own collectives, e.g. torch.distributed gloo) used to test the sharded
 // algorithm with several ranks on one GPU.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -28,6 +33,8 @@ struct Comm {
   ncclComm_t comm = nullptr;
   sqlm_allreduce_fn host_fn = nullptr;
   void *host_user = nullptr;
+  sqlm_p2p_fn host_p2p = nullptr;  // send / recv / broadcast for the host transport
+  void *host_p2p_user = nullptr;
   int rank = 0, nranks = 1;
   std::vector<char> stage;  // host staging for the callback transport
   bool enabled() const { return nranks > 1 && (comm != nullptr || host_fn != nullptr); }
@@ -47,6 +54,8 @@ inline void comm_destroy(Comm &c) {
   c.comm = nullptr;
   c.host_fn = nullptr;
   c.host_user = nullptr;
+  c.host_p2p = nullptr;
+  c.host_p2p_user = nullptr;
   c.rank = 0;
   c.nranks = 1;
 }
@@ -66,7 +75,11 @@ inline int comm_init(Comm &c, const char *idbytes, int rank, int nranks) {
 }
 
 inline int comm_init_host(Comm &c, int rank, int nranks, sqlm_allreduce_fn fn, void *user) {
+  const sqlm_p2p_fn p2p = c.host_p2p;  // survives a re-init of the collective
+  void *p2p_user = c.host_p2p_user;
   comm_destroy(c);
+  c.host_p2p = p2p;
+  c.host_p2p_user = p2p_user;
   c.rank = rank;
   c.nranks = nranks;
   c.host_fn = fn;
@@ -115,27 +128,71 @@ inline int comm_allreduce_host(Comm &c, void *hptr, int64_t count, int dt, int o
   return r;
 }
 
-// Sum H_pp and b_p across shards (in place), once per LM iteration.
-inline int comm_allreduce_hpp(Comm &c, const DevProblem &d, hipStream_t st) {
-  if (!c.enabled() || d.nP == 0) return 0;
-  if (comm_allreduce_dev(c, d.Hpp, (int64_t)36 * d.nP, SQLM_DT_F64, SQLM_OP_SUM, st)) return -9;
-  return comm_allreduce_dev(c, d.bp, (int64_t)8 * d.nP, SQLM_DT_F64, SQLM_OP_SUM, st);
-}
-
-// Sum the reduced camera system S (BSR upper, identical banded pattern on
-// every rank) and its right-hand side g; every rank then runs the same
-// deterministic solve, so dx agrees without a broadcast.
-inline int comm_allreduce_rcs(Comm &c, const DevProblem &d, hipStream_t st) {
-  if (!c.enabled() || d.nP == 0) return 0;
-  if (comm_allreduce_dev(c, d.S, (int64_t)36 * d.nnzb, SQLM_DT_F64, SQLM_OP_SUM, st)) return -9;
-  return comm_allreduce_dev(c, d.g, (int64_t)6 * d.nP, SQLM_DT_F64, SQLM_OP_SUM, st);
-}
-
-// scalars: [chi_cur, chi_new, scale] summed, [maxdiag] max.
-inline int comm_allreduce_scalars(Comm &c, double *scalars, hipStream_t st) {
+// scalars: [chi_cur, chi_new, scale] summed; [maxdiag] max (iteration 0 only).
+inline int comm_allreduce_scalars(Comm &c, double *scalars, bool with_max, hipStream_t st) {
   if (!c.enabled()) return 0;
   if (comm_allreduce_dev(c, scalars, 3, SQLM_DT_F64, SQLM_OP_SUM, st)) return -9;
-  return comm_allreduce_dev(c, scalars + kMaxDiag, 1, SQLM_DT_F64, SQLM_OP_MAX, st);
+  return with_max ? comm_allreduce_dev(c, scalars + kMaxDiag, 1, SQLM_DT_F64, SQLM_OP_MAX, st) : 0;
+}
+
+// One point-to-point transfer of a DEVICE buffer.
+struct P2POp {
+  int peer;
+  bool send;
+  void *dptr;
+  int64_t count;
+  int dt;
+};
+
+// A group of sends / receives, ordered on `st`. RCCL: one ncclGroup (the
+// transfers of rank 0 from all peers proceed in parallel over its links).
+// Host transport: in list order through the p2p callback (each peer pairs its
+// operations with rank 0 in the same order, so blocking transports cannot
+// deadlock).
+inline int comm_group_p2p(Comm &c, const std::vector<P2POp> &ops, hipStream_t st) {
+  if (!c.enabled() || ops.empty()) return 0;
+  if (c.comm) {
+    if (ncclGroupStart() != ncclSuccess) return -9;
+    int r = 0;
+    for (const P2POp &o : ops) {
+      if (o.count <= 0) continue;
+      const ncclResult_t e = o.send ? ncclSend(o.dptr, (size_t)o.count, dt_nccl(o.dt), o.peer, c.comm, st)
+                                    : ncclRecv(o.dptr, (size_t)o.count, dt_nccl(o.dt), o.peer, c.comm, st);
+      if (e != ncclSuccess) r = -9;
+    }
+    if (ncclGroupEnd() != ncclSuccess) r = -9;
+    return r;
+  }
+  if (!c.host_p2p) return -9;
+  if (hipStreamSynchronize(st) != hipSuccess) return -2;
+  for (const P2POp &o : ops) {
+    if (o.count <= 0) continue;
+    const size_t bytes = (size_t)o.count * dt_size(o.dt);
+    if (c.stage.size() < bytes) c.stage.resize(bytes);
+    if (o.send) {
+      if (hipMemcpy(c.stage.data(), o.dptr, bytes, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+      if (c.host_p2p(c.host_p2p_user, c.stage.data(), o.count, o.dt, o.peer, SQLM_P2P_SEND) != 0) return -9;
+    } else {
+      if (c.host_p2p(c.host_p2p_user, c.stage.data(), o.count, o.dt, o.peer, SQLM_P2P_RECV) != 0) return -9;
+      if (hipMemcpy(o.dptr, c.stage.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -2;
+    }
+  }
+  return 0;
+}
+
+// In-place broadcast of a DEVICE buffer from `root`, ordered on `st`.
+inline int comm_bcast_dev(Comm &c, void *dptr, int64_t count, int dt, int root, hipStream_t st) {
+  if (!c.enabled() || count == 0) return 0;
+  if (c.comm)
+    return ncclBroadcast(dptr, dptr, (size_t)count, dt_nccl(dt), root, c.comm, st) == ncclSuccess ? 0 : -9;
+  if (!c.host_p2p) return -9;
+  const size_t bytes = (size_t)count * dt_size(dt);
+  if (c.stage.size() < bytes) c.stage.resize(bytes);
+  if (hipStreamSynchronize(st) != hipSuccess) return -2;
+  if (c.rank == root && hipMemcpy(c.stage.data(), dptr, bytes, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+  if (c.host_p2p(c.host_p2p_user, c.stage.data(), count, dt, root, SQLM_P2P_BCAST) != 0) return -9;
+  if (c.rank != root && hipMemcpy(dptr, c.stage.data(), bytes, hipMemcpyHostToDevice) != hipSuccess) return -2;
+  return 0;
 }
 
 inline int comm_barrier(Comm &c, hipStream_t st) {

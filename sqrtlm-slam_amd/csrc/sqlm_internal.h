@@ -68,7 +68,9 @@ struct DevProblem {
   int *s_row = nullptr;                     // [nnzb] block row (direct CR assembly)
   double *S = nullptr;                      // [nnzb][36]
   double *g = nullptr;                      // [6 nP]
-  double *dx = nullptr;                     // [6 nP]
+  double *dx = nullptr;                     // [6 nP + 1] (+ the solve flag in sharded runs)
+  double *hdiag = nullptr;                  // [6 nP] pose Hessian diagonals (sharded lambda_0)
+  double *xstage = nullptr;                 // rank 0 of a sharded run: gathered S / g row ranges
   double *dense = nullptr;                  // [n][n] dense workspace (upper)
   // tiled RCS assembly (landmark tiles with a small camera window)
   int n_tiles = 0;
@@ -135,6 +137,16 @@ void launch_pose_prep(const DevProblem &d, int buf, hipStream_t st);
 void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStream_t st);
 void launch_camera_pass(const DevProblem &d, hipStream_t st);
 void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
+void launch_pose_diag(const DevProblem &d, hipStream_t st);
+// rank 0 of a sharded run: destination / source ranges of the gathered rows
+constexpr int kMaxRanks = 16;
+struct GatherTab {
+  int n = 0;
+  int64_t s_lo[kMaxRanks], s_hi[kMaxRanks], s_src[kMaxRanks];
+  int64_t g_lo[kMaxRanks], g_hi[kMaxRanks], g_src[kMaxRanks];
+};
+void launch_gather_add(const DevProblem &d, const GatherTab &t, hipStream_t st);
+void launch_flag_pack(const DevProblem &d, bool unpack, hipStream_t st);
 void launch_damp(const DevProblem &d, double lambda, hipStream_t st);
 void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st);
 void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st);

@@ -501,19 +501,65 @@ void launch_camera_pass(const DevProblem &d, hipStream_t st) {
   else hipLaunchKernelGGL(k_camera_pass<false>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d);
 }
 
-// Sharded runs: max |diag(H_pp)| after the cross-rank sum of H_pp.
+// Sharded runs, iteration 0: the pose Hessian diagonals of this rank (summed
+// across ranks by the caller), then their max |.| for lambda_0.
+__global__ __launch_bounds__(256) void k_pose_diag(DevProblem d) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < 6 * d.nP) d.hdiag[k] = d.Hpp[36 * (k / 6) + 7 * (k % 6)];
+}
+
 __global__ __launch_bounds__(256) void k_pose_maxdiag(DevProblem d) {
   __shared__ double red[4];
   double mx = 0.0;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.nP; i += gridDim.x * blockDim.x)
-    for (int k = 0; k < 6; ++k) mx = fmax(mx, fabs(d.Hpp[36 * i + 7 * k]));
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 6 * d.nP; k += gridDim.x * blockDim.x)
+    mx = fmax(mx, fabs(d.hdiag[k]));
   mx = block_max(mx, red);
   if (threadIdx.x == 0) atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
 }
 
+void launch_pose_diag(const DevProblem &d, hipStream_t st) {
+  if (d.nP == 0) return;
+  hipLaunchKernelGGL(k_pose_diag, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d);
+}
+
 void launch_pose_maxdiag(const DevProblem &d, hipStream_t st) {
   if (d.nP == 0) return;
-  hipLaunchKernelGGL(k_pose_maxdiag, dim3(std::min(64, (d.nP + 255) / 256)), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(k_pose_maxdiag, dim3(std::min(64, (6 * d.nP + 255) / 256)), dim3(256), 0, st, d);
+}
+
+// Sharded runs, rank 0: S / g += the row ranges gathered from the other ranks
+// (staged contiguously). Each destination entry sums its sources in rank
+// order, so the result is deterministic and no two threads write one entry.
+__global__ __launch_bounds__(256) void k_gather_add(DevProblem d, GatherTab t) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nS = 36 * d.nnzb;
+  if (i < nS) {
+    double v = d.S[i];
+    for (int r = 0; r < t.n; ++r)
+      if (i >= t.s_lo[r] && i < t.s_hi[r]) v += d.xstage[t.s_src[r] + (i - t.s_lo[r])];
+    d.S[i] = v;
+  } else if (i < nS + 6 * d.nP) {
+    const int64_t k = i - nS;
+    double v = d.g[k];
+    for (int r = 0; r < t.n; ++r)
+      if (k >= t.g_lo[r] && k < t.g_hi[r]) v += d.xstage[t.g_src[r] + (k - t.g_lo[r])];
+    d.g[k] = v;
+  }
+}
+
+void launch_gather_add(const DevProblem &d, const GatherTab &t, hipStream_t st) {
+  const int64_t n = 36 * d.nnzb + 6 * (int64_t)d.nP;
+  if (n > 0) hipLaunchKernelGGL(k_gather_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, t);
+}
+
+// The solve flag rides in the dx broadcast (slot 6 nP).
+__global__ void k_flag_pack(DevProblem d, int unpack) {
+  if (unpack) d.flags[0] = d.dx[6 * d.nP] > 0.5 ? 1 : 0;
+  else d.dx[6 * d.nP] = (double)d.flags[0];
+}
+
+void launch_flag_pack(const DevProblem &d, bool unpack, hipStream_t st) {
+  hipLaunchKernelGGL(k_flag_pack, dim3(1), dim3(1), 0, st, d, unpack ? 1 : 0);
 }
 
 // ---------------------------------------------------------------- damping
@@ -630,15 +676,15 @@ __global__ __launch_bounds__(256) void k_rcs(DevProblem d, double lambda, int ns
   for (int k = threadIdx.x; k < nslot * 36; k += 256) {
     const int nsm = nslot_max * 36;
     double v = ((smem[k] + smem[nsm + k]) + smem[2 * nsm + k]) + smem[3 * nsm + k];
-    if (k < 36 && (!d.sharded || d.rank == 0)) {  // slot 0 = diagonal block (cols[0] == i)
+    if (k < 36) {  // slot 0 = diagonal block (cols[0] == i); sharded: this rank's H_pp share
       v += d.Hpp[36 * i + k];
-      if (k % 7 == 0) v += lambda;
+      if (k % 7 == 0 && (!d.sharded || d.rank == 0)) v += lambda;
     }
     Srow[k] = v;
   }
   if (threadIdx.x < 6) {
     const int rr = threadIdx.x;
-    const double bpv = (!d.sharded || d.rank == 0) ? d.bp[8 * i + rr] : 0.0;
+    const double bpv = d.bp[8 * i + rr];  // sharded: this rank's b_p share
     d.g[6 * i + rr] = bpv + (((gw[rr] + gw[8 + rr]) + gw[16 + rr]) + gw[24 + rr]);
   }
 }
@@ -954,9 +1000,9 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
       v += d.part[d.tile_part_ptr[ct.x] + (int64_t)R * ld + C];
     }
     const int j = d.s_col[s];
-    if (own && s == d.s_row_ptr[j]) {  // diagonal block (first block of row j)
+    if (s == d.s_row_ptr[j]) {  // diagonal block (first block of row j); sharded: this rank's share
       v += d.Hpp[36 * j + e];
-      if (r == c) v += lambda;
+      if (r == c && own) v += lambda;
     }
     if (!d.cr_direct) {
       d.S[gid] = v;
@@ -976,7 +1022,7 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
       const int2 ct = d.gred_idx[k];
       v += d.gpart[d.tile_gpart_ptr[ct.x] + 6 * ct.y + r];
     }
-    v += own ? d.bp[8 * i + r] : 0.0;
+    v += d.bp[8 * i + r];
     d.g[6 * i + r] = v;
     if (d.cr_direct) {
       const int I = i / d.cr_B, li = i - I * d.cr_B;
@@ -1116,8 +1162,9 @@ __global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda
       const double *dx = d.dx + 6 * h;
       const double dd[6] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5]};
       se3_oplus(q, t, dd);
-      if (!d.sharded || d.rank == 0)
-        for (int k = 0; k < 6; ++k) sc += dd[k] * (lambda * dd[k] + d.bp[8 * h + k]);
+      // computeScale dx^T (lambda dx + b): sharded, b_p is summed over ranks and lambda counted once
+      const double lam = (!d.sharded || d.rank == 0) ? lambda : 0.0;
+      for (int k = 0; k < 6; ++k) sc += dd[k] * (lam * dd[k] + d.bp[8 * h + k]);
     }
     double *o = d.pose_qt[1] + 8 * p;
     store2(o, q[0], q[1]); store2(o + 2, q[2], q[3]); store2(o + 4, t[0], t[1]); store2(o + 6, t[2], 0.0);

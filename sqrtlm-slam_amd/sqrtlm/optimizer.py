@@ -109,10 +109,28 @@ class Context:
         buf = C.create_string_buffer(unique_id, len(unique_id))
         check(lib().sqlm_ctx_set_comm(self._h, buf, int(rank), int(nranks)), "sqlm_ctx_set_comm")
 
-    def set_host_comm(self, rank: int, nranks: int, allreduce) -> None:
-        """Shard over a host collective: ``allreduce(arr, op)`` must reduce the
-        numpy array ``arr`` in place across ranks (op "sum" or "max"), e.g.
-        with torch.distributed gloo. Runs several ranks on one GPU (tests)."""
+    def set_host_comm(self, rank: int, nranks: int, allreduce, p2p) -> None:
+        """Shard over host collectives: ``allreduce(arr, op)`` must reduce the
+        numpy array ``arr`` in place across ranks (op "sum" or "max");
+        ``p2p(arr, peer, op)`` sends ``arr`` to / receives it from ``peer``
+        (op "send" / "recv") or broadcasts it in place from root ``peer``
+        (op "bcast"), e.g. with torch.distributed gloo. Runs several ranks on
+        one GPU (tests)."""
+        ops = {0: "send", 1: "recv", 2: "bcast"}
+
+        def _p2p(_user, buf, count, dtype, peer, op):
+            try:
+                dt = _lib.DTYPES[dtype]
+                arr = np.ctypeslib.as_array((C.c_char * (int(count) * np.dtype(dt).itemsize)).from_address(buf))
+                p2p(arr.view(dt), int(peer), ops[int(op)])
+                return 0
+            except Exception:  # noqa: BLE001 — never unwind through the C ABI
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._host_p2p = _lib.P2P_FN(_p2p)
+        check(lib().sqlm_ctx_set_host_p2p(self._h, self._host_p2p, None), "sqlm_ctx_set_host_p2p")
+
         def _cb(_user, buf, count, dtype, op):
             try:
                 dt = _lib.DTYPES[dtype]

@@ -32,6 +32,20 @@ def gloo_allreduce(arr: np.ndarray, op: str) -> None:
         dist.all_reduce(t, op=rop)
 
 
+def gloo_p2p(arr: np.ndarray, peer: int, op: str) -> None:
+    """Point-to-point half of the host transport (sqlm_ctx_set_host_p2p):
+    send to / receive from `peer`, or broadcast in place from root `peer`."""
+    import torch
+    import torch.distributed as dist
+    t = torch.from_numpy(arr.view(np.uint8))  # byte view: every dtype, shares memory with arr
+    if op == "send":
+        dist.send(t, dst=peer)
+    elif op == "recv":
+        dist.recv(t, src=peer)
+    else:
+        dist.broadcast(t, src=peer)
+
+
 def _entry(fn, rank, world, port, args, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))

@@ -1,12 +1,12 @@
 """Landmark-sharded global BA on the GPU: `world` ranks (spawned processes on
 the one GPU of the box, exchanging through sqlm_ctx_set_host_comm over gloo)
 must reproduce the CPU oracle on the full problem, like the single-rank path.
-The RCCL transport runs the same prepare/trial code with ncclAllReduce in
-place of the host callback (sqlm_comm.h)."""
+The RCCL transport runs the same prepare/trial code with ncclSend / ncclRecv /
+ncclBroadcast / ncclAllReduce in place of the host callbacks (sqlm_comm.h)."""
 import numpy as np
 import pytest
 
-from dist_util import gloo_allreduce, run_ranks
+from dist_util import gloo_allreduce, gloo_p2p, run_ranks
 from sqrtlm import synth
 from sqrtlm.shard import landmark_ranges, shard
 
@@ -21,7 +21,7 @@ def _gpu_rank(rank, world, scale, iters):
     prob = synth.config4(seed=4, scale=scale)
     loc = shard(prob, rank, world)
     with Context(0) as ctx:
-        ctx.set_host_comm(rank, world, gloo_allreduce)
+        ctx.set_host_comm(rank, world, gloo_allreduce, gloo_p2p)
         ctx.set_problem(loc)
         n, st = ctx.global_ba(iters)
         q, t = ctx.poses()

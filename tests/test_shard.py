@@ -5,7 +5,7 @@ test_gpu_sharded.py."""
 import numpy as np
 import pytest
 
-from dist_util import gloo_allreduce, run_ranks
+from dist_util import gloo_allreduce, gloo_p2p, run_ranks
 from sqrtlm import synth
 from sqrtlm.shard import landmark_ranges, shard
 
@@ -65,3 +65,41 @@ def test_lidar_edges_only_on_rank0():
     prob = synth.add_lidar_flat(synth.config4(seed=4, scale=0.01), pose=5, n=20, seed=1)
     assert shard(prob, 0, 2).n_lid == prob.n_lid
     assert shard(prob, 1, 2).n_lid == 0
+
+
+def _gather_work(rank, world, n_rows, seed):
+    """The per-trial exchange of sqlm_api.cpp trial() with the host transport:
+    every rank > 0 sends its nonzero row range of S (here a dense [n_rows, 4]
+    stand-in) to rank 0, which adds the ranges in rank order, then broadcasts
+    the result (dx stand-in). Ranges are agreed by an all-reduce."""
+    rng = np.random.default_rng(seed + rank)
+    lo = rank * n_rows // world - (3 if rank else 0)
+    hi = min(n_rows, (rank + 1) * n_rows // world + 3)
+    S = np.zeros((n_rows, 4))
+    S[lo:hi] = rng.normal(size=(hi - lo, 4))
+    rngs = np.zeros(2 * world, np.int32)
+    rngs[2 * rank], rngs[2 * rank + 1] = lo, hi
+    gloo_allreduce(rngs, "sum")
+    if rank == 0:
+        tot = S.copy()
+        for r in range(1, world):
+            a, b = rngs[2 * r], rngs[2 * r + 1]
+            buf = np.zeros((b - a, 4))
+            gloo_p2p(buf, r, "recv")
+            tot[a:b] += buf
+        x = tot.sum(axis=1)
+    else:
+        gloo_p2p(np.ascontiguousarray(S[lo:hi]), 0, "send")
+        x = np.zeros(n_rows)
+    gloo_p2p(x, 0, "bcast")
+    full = S.copy()
+    gloo_allreduce(full, "sum")
+    return dict(x=x, ref=full.sum(axis=1))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_to_root_and_broadcast(world):
+    res = run_ranks(_gather_work, world, 50, 7)
+    for r in res:
+        np.testing.assert_allclose(r["x"], r["ref"], rtol=1e-12, atol=1e-12)
+        np.testing.assert_array_equal(r["x"], res[0]["x"])
