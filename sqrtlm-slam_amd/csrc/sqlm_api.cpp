@@ -130,7 +130,7 @@ enum BufId {
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
-  B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE
+  B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -549,9 +549,14 @@ int prepare(sqlm_ctx *c, int level) {
     AL(B_CRC, nb, d.cr_C);
     AL(B_CRG, (size_t)c->cr.p * c->cr.n, d.cr_g);
     AL(B_CRX, (size_t)c->cr.p * c->cr.n, d.cr_x);
-  } else {
-    if ((size_t)6 * nP * sizeof(double) > 150 * 1024) return SQLM_ERR_UNSUPPORTED;
-    AL(B_DENSE, (size_t)6 * nP * 6 * nP, d.dense);
+  } else {  // blocked MFMA Cholesky of the dense S (sqlm_rcs_solve.hip)
+    const int np_ = (6 * nP + kCRMaxN - 1) / kCRMaxN * kCRMaxN;
+    d.dense_n = np_;
+    AL(B_DENSE, (size_t)np_ * np_, d.dense);
+    AL(B_DENSEL, (size_t)np_ * np_, d.dense_L);
+    AL(B_DENSELI, (size_t)np_ * kCRMaxN, d.dense_Linv);
+    AL(B_DENSER, (size_t)np_, d.dense_r);
+    AL(B_DENSEX, (size_t)np_, d.dense_x);
   }
   AL(B_PART, (size_t)kMaxPartials, d.partials);
   AL(B_SCAL, (size_t)kNScalars, d.scalars);

@@ -71,7 +71,13 @@ struct DevProblem {
   double *dx = nullptr;                     // [6 nP + 1] (+ the solve flag in sharded runs)
   double *hdiag = nullptr;                  // [6 nP] pose Hessian diagonals (sharded lambda_0)
   double *xstage = nullptr;                 // rank 0 of a sharded run: gathered S / g row ranges
-  double *dense = nullptr;                  // [n][n] dense workspace (upper)
+  // dense path (S not block-banded enough for the CR solver, e.g. a real LBA
+  // window in keyframe-id order): n_pad = 6 nP rounded up to kCRMaxN
+  int dense_n = 0;
+  double *dense = nullptr;                  // [n_pad][n_pad] A (lower), factored in place
+  double *dense_L = nullptr;                // [n_pad][n_pad] L
+  double *dense_Linv = nullptr;             // [n_pad / kCRMaxN][kCRMaxN][kCRMaxN]
+  double *dense_r = nullptr, *dense_x = nullptr;  // [n_pad]
   // tiled RCS assembly (landmark tiles with a small camera window)
   int n_tiles = 0;
   int *tile_lm_ptr = nullptr;               // [T+1] landmark slot ranges

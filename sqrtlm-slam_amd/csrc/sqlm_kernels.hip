@@ -13,7 +13,7 @@
 //                      [setLambda + D->inverse(), block_solver.hpp:564-589, :389]
 //   k_rcs              reduced camera system rows S_i*, g_i
 //                      [Schur loop, block_solver.hpp:381-439]
-//   k_dense_chol_solve S dx = g  [LinearSolverEigen::solve]
+//   launch_dense_solve S dx = g  [LinearSolverEigen::solve] when S is not banded
 //   k_pose_update      T <- exp(dx) T, pose part of computeScale
 //   k_landmark_update<W> back-substitution, X += dl, new residuals + chi2
 //                      [block_solver.hpp:459-483, sparse_optimizer.cpp:422-435]
@@ -1075,76 +1075,42 @@ void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st) {
 
 // ---------------------------------------------------------------- dense solve
 
-// Single-workgroup Cholesky S = U^T U of the (small) reduced camera system and
-// the two triangular solves. Used for local-BA sized systems.
-__global__ __launch_bounds__(1024) void k_dense_chol_solve(DevProblem d, int n) {
-  extern __shared__ __attribute__((aligned(16))) double vec[];  // [n]
-  __shared__ int fail;
-  double *A = d.dense;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  // scatter BSR upper blocks to dense row-major upper
-  for (int64_t k = tid; k < (int64_t)n * n; k += nt) A[k] = 0.0;
-  __syncthreads();
-  for (int i = 0; i < d.nP; ++i) {
-    for (int s = d.s_row_ptr[i]; s < d.s_row_ptr[i + 1]; ++s) {
-      const int j = d.s_col[s];
-      for (int e = tid; e < 36; e += nt) {
-        const int r = 6 * i + e / 6, c = 6 * j + e % 6;
-        if (r <= c) A[(int64_t)r * n + c] = d.S[(int64_t)s * 36 + e];
-      }
-    }
+// BSR upper blocks of S -> lower triangle of the padded dense matrix (row-major,
+// ld n_pad, zeroed beforehand): one thread per BSR entry writes its transposed
+// position; then identity on the padded rows and r = g (zero padded).
+__global__ __launch_bounds__(256) void k_dense_scatter(DevProblem d) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int np_ = d.dense_n, n = 6 * d.nP;
+  if (k < d.nnzb * 36) {
+    const int s = (int)(k / 36), e = (int)(k % 36);
+    const int r = 6 * d.s_row[s] + e / 6, c = 6 * d.s_col[s] + e % 6;  // upper entry (r, c)
+    if (r <= c) d.dense[(int64_t)c * np_ + r] = d.S[k];
+  } else if (k < d.nnzb * 36 + np_) {
+    const int r = (int)(k - d.nnzb * 36);
+    d.dense_r[r] = r < n ? d.g[r] : 0.0;
+    if (r >= n) d.dense[(int64_t)r * np_ + r] = 1.0;
   }
-  if (tid == 0) fail = 0;
-  for (int k = tid; k < n; k += nt) vec[k] = d.g[k];
-  __syncthreads();
-  for (int k = 0; k < n; ++k) {
-    if (tid == 0) {
-      const double akk = A[(int64_t)k * n + k];
-      if (!(akk > 0.0)) fail = 1;
-      A[(int64_t)k * n + k] = sqrt(akk);
-    }
-    __syncthreads();
-    if (fail) break;
-    const double ukk = A[(int64_t)k * n + k];
-    for (int j = k + 1 + tid; j < n; j += nt) A[(int64_t)k * n + j] /= ukk;
-    __syncthreads();
-    const int m = n - k - 1;
-    for (int64_t idx = tid; idx < (int64_t)m * m; idx += nt) {
-      const int ii = k + 1 + (int)(idx / m), jj = k + 1 + (int)(idx % m);
-      if (jj >= ii) A[(int64_t)ii * n + jj] -= A[(int64_t)k * n + ii] * A[(int64_t)k * n + jj];
-    }
-    __syncthreads();
-  }
-  if (fail) {
-    if (tid == 0) d.flags[0] = 0;
-    for (int k = tid; k < n; k += nt) d.dx[k] = 0.0;
-    return;
-  }
-  // U^T y = g
-  for (int k = 0; k < n; ++k) {
-    const double yk = vec[k] / A[(int64_t)k * n + k];
-    __syncthreads();
-    if (tid == 0) vec[k] = yk;
-    for (int j = k + 1 + tid; j < n; j += nt) vec[j] -= A[(int64_t)k * n + j] * yk;
-    __syncthreads();
-  }
-  // U x = y
-  for (int k = n - 1; k >= 0; --k) {
-    const double xk = vec[k] / A[(int64_t)k * n + k];
-    __syncthreads();
-    if (tid == 0) vec[k] = xk;
-    for (int j = tid; j < k; j += nt) vec[j] -= A[(int64_t)j * n + k] * xk;
-    __syncthreads();
-  }
-  for (int k = tid; k < n; k += nt) d.dx[k] = vec[k];
-  if (tid == 0) d.flags[0] = 1;
 }
 
+__global__ void k_dense_copy_dx(DevProblem d) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < 6 * d.nP) d.dx[k] = d.flags[0] ? d.dense_x[k] : 0.0;
+}
+
+// LinearSolverEigen::solve on a dense S: blocked right-looking Cholesky with
+// 112-wide LDS diagonal factors and MFMA panel / trailing updates, then the two
+// block triangular solves. A non-positive pivot clears flags[0] (rejected trial).
 int launch_dense_solve(const DevProblem &d, hipStream_t st) {
   const int n = 6 * d.nP;
   if (n == 0) return 0;
-  if ((size_t)n * sizeof(double) > 150 * 1024) return -8;  // SQLM_ERR_UNSUPPORTED
-  hipLaunchKernelGGL(k_dense_chol_solve, dim3(1), dim3(1024), (size_t)n * sizeof(double), st, d, n);
+  const int64_t nn = (int64_t)d.dense_n * d.dense_n;
+  if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d.flags), 1, 1, st) != hipSuccess) return -2;
+  if (hipMemsetAsync(d.dense, 0, sizeof(double) * nn, st) != hipSuccess) return -2;
+  const int64_t items = d.nnzb * 36 + d.dense_n;
+  hipLaunchKernelGGL(k_dense_scatter, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, d);
+  if (launch_dense_spd_solve(d.dense, d.dense_L, d.dense_Linv, d.dense_r, d.dense_x, d.flags, d.dense_n, st))
+    return -2;
+  hipLaunchKernelGGL(k_dense_copy_dx, dim3((n + 255) / 256), dim3(256), 0, st, d);
   return 0;
 }
 

@@ -150,3 +150,18 @@ def test_all_fixed_or_empty_level(gpu_ctx, oracle):
     ref = oracle.OracleGraph(prob)
     nr, sr = ref.optimize(0, 10)
     assert n == nr == -1
+
+
+@pytest.mark.parametrize("n_kf,k_min,k_max", [(30, 20, 30), (64, 40, 64)])
+def test_dense_solve_path(gpu_ctx, oracle, n_kf, k_min, k_max):
+    """Tracks spanning most of the window: the reduced camera system is not
+    block-banded enough for the CR solver (bandwidth >= 19 cameras), so S is
+    solved by the blocked MFMA dense Cholesky (1 and 4 diagonal blocks of 112)."""
+    prob = synth.make_problem(n_kf, 1500, k_min=k_min, k_max=k_max, seed=9, robust=True)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(0, 10)
+    gpu_ctx.set_problem(prob)
+    ng, sg = gpu_ctx.optimize(0, 10)
+    assert ng == nr
+    _compare_stats(sg, sr)
+    _compare_state(gpu_ctx, ref)
