@@ -145,7 +145,7 @@ struct TilePlan {
 };
 
 void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::vector<int> &obs_camh,
-                 const std::vector<int> &s_row, const std::vector<int> &s_col, TilePlan &tp) {
+                 const std::vector<int> &s_row, const std::vector<int> &s_col, int lm_cap, TilePlan &tp) {
   const int64_t nE = lm_begin[nL];
   tp.obs_local.assign(nE, -1);
   tp.urange.assign(nL, int2{-1, -1});
@@ -204,7 +204,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
       lmst[h] = sl;
       if (stamp[h] != t) ++nnew;
     }
-    if (cur_lm > 0 && ((int)cur.size() + nnew > kTileMaxCams || cur_lm >= kTileMaxLm)) close_tile(sl);
+    if (cur_lm > 0 && ((int)cur.size() + nnew > kTileMaxCams || cur_lm >= lm_cap)) close_tile(sl);
     for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
       const int h = obs_camh[o];
       if (h >= 0 && stamp[h] != t) { stamp[h] = t; cur.push_back(h); }
@@ -392,7 +392,11 @@ int prepare(sqlm_ctx *c, int level) {
     }
   }
   TilePlan tp;
-  build_tiles(nP, nL, lm_begin, obs_camh, s_row, s_col, tp);
+  // landmarks per tile: up to kTileMaxLm, fewer on small problems so that the
+  // tiles still cover every CU twice (a local-BA window of 5k landmarks would
+  // otherwise run ~40 long tiles on 256 CUs)
+  const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
+  build_tiles(nP, nL, lm_begin, obs_camh, s_row, s_col, lm_cap, tp);
   c->use_tiles = nP > 0 && tp.max_cp <= kTileHardCams;
   c->tile_max_cp = tp.max_cp;
   c->tile_max_k = 0;

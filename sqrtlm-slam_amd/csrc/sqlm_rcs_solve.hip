@@ -739,15 +739,95 @@ __global__ __launch_bounds__(64) void k_dchol_update(DenseView v, int k, int tot
   for (int j = 0; j < 4; ++j) o[(size_t)(k4 + 4 * j) * v.n + r16] -= acc[j];
 }
 
-// forward: y_k = Linv_kk r_k (into x), then r_i -= L_ik y_k for rows below
-__global__ __launch_bounds__(128) void k_dtrsv_fwd_diag(DenseView v, int k) {
-  constexpr int nb = kCRMaxN;
-  const int r = threadIdx.x;
-  if (r >= nb) return;
-  const double *Li = v.Linv + (size_t)k * nb * nb + (size_t)r * nb, *rk = v.r + (size_t)k * nb;
-  double s = 0.0;
-  for (int m = 0; m <= r; ++m) s += Li[m] * rk[m];
-  v.x[(size_t)k * nb + r] = s;
+// A_ij -= L_ik L_jk^T for one 112x112 block pair (bi, bj), bi >= bj > k, per
+// workgroup of 8 waves: the two 112 x 16 K-slices of L are staged in LDS (16-
+// byte loads, double-buffered), waves 0..6 each accumulate one row of 16x16
+// output tiles (lower 28 only on the diagonal pair) in registers with
+// v_mfma_f64_16x16x4f64. Per pair: 1372 MFMAs on 200 KB of L2 reads, so the
+// update runs on the matrix cores instead of the L2 (the one-wave-per-tile
+// k_dchol_update re-reads both 16 x 112 slices for every tile).
+constexpr int kUpdKC = 16, kUpdLd = kUpdKC + 2;  // row stride: 16-byte aligned, spreads the 16 rows over banks
+__global__ __launch_bounds__(512) void k_dchol_update_blk(DenseView v, int k, int npairs) {
+  constexpr int nb = kCRMaxN, nt = nb / 16, nkc = nb / kUpdKC;
+  __shared__ __attribute__((aligned(16))) double Xs[2][nb * kUpdLd];
+  __shared__ __attribute__((aligned(16))) double Ys[2][nb * kUpdLd];
+  const int lb = xcd_block(npairs);
+  if (lb >= npairs) return;
+  int ii = 0, rem = lb;
+  while (rem > ii) { rem -= ii + 1; ++ii; }
+  const int bi = k + 1 + ii, bj = k + 1 + rem;
+  const bool diag = bi == bj;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r16 = lane & 15, k4 = lane >> 4;
+  const double *X = v.L + (size_t)bi * nb * v.n + (size_t)k * nb;
+  const double *Y = v.L + (size_t)bj * nb * v.n + (size_t)k * nb;
+  // staging: 112 rows x 16 doubles = 896 double2 per operand; 512 threads, 2 passes
+  auto stage = [&](int buf, int kc) {
+    for (int e = tid; e < nb * kUpdKC / 2; e += 512) {
+      const int r = e >> 3, c2 = (e & 7) * 2;
+      const double2 xv = *reinterpret_cast<const double2 *>(X + (size_t)r * v.n + kc * kUpdKC + c2);
+      *reinterpret_cast<double2 *>(&Xs[buf][r * kUpdLd + c2]) = xv;
+      if (!diag) {
+        const double2 yv = *reinterpret_cast<const double2 *>(Y + (size_t)r * v.n + kc * kUpdKC + c2);
+        *reinterpret_cast<double2 *>(&Ys[buf][r * kUpdLd + c2]) = yv;
+      }
+    }
+  };
+  // wave w < 7 owns output tile row ti = w (tiles tj = 0..6, tj <= ti on the
+  // diagonal pair): its A operand is read once per K step for all 7 tiles
+  d4 acc[nt];
+#pragma unroll
+  for (int q = 0; q < nt; ++q) acc[q] = d4{0.0, 0.0, 0.0, 0.0};
+  const int ti = wave, tjmax = diag ? ti : nt - 1;
+  stage(0, 0);
+  __syncthreads();
+  for (int kc = 0; kc < nkc; ++kc) {
+    const int buf = kc & 1;
+    if (kc + 1 < nkc) stage(buf ^ 1, kc + 1);
+    const double *Xb = Xs[buf], *Yb = diag ? Xs[buf] : Ys[buf];
+    if (ti < nt) {
+#pragma unroll
+      for (int s = 0; s < kUpdKC / 4; ++s) {
+        const double a = Xb[(16 * ti + r16) * kUpdLd + 4 * s + k4];
+#pragma unroll
+        for (int tj = 0; tj < nt; ++tj)
+          if (tj <= tjmax) {
+            const double b = Yb[(16 * tj + r16) * kUpdLd + 4 * s + k4];
+            acc[tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[tj], 0, 0, 0);
+          }
+      }
+    }
+    __syncthreads();
+  }
+  if (ti < nt) {
+#pragma unroll
+    for (int tj = 0; tj < nt; ++tj)
+      if (tj <= tjmax) {
+        double *o = v.A + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)bj * nb + 16 * tj;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[(size_t)(k4 + 4 * j) * v.n + r16] -= acc[tj][j];
+      }
+  }
+}
+
+// forward: y_k = Linv_kk r_k (into x): thread (r, quarter) sums its 28
+// columns m <= r (fixed trip count, every load in flight at once), the four
+// quarters are added in LDS in a fixed order.
+__global__ __launch_bounds__(512) void k_dtrsv_fwd_diag(DenseView v, int k) {
+  constexpr int nb = kCRMaxN, q = nb / 4;
+  __shared__ double part[4][nb];
+  const int t = threadIdx.x, r = t % nb, h = t / nb;
+  const double *Lk = v.Linv + (size_t)k * nb * nb, *rk = v.r + (size_t)k * nb;
+  if (h < 4) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < q; ++i) {
+      const int m = h * q + i;
+      s += m <= r ? Lk[(size_t)r * nb + m] * rk[m] : 0.0;
+    }
+    part[h][r] = s;
+  }
+  __syncthreads();
+  if (t < nb) v.x[(size_t)k * nb + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
 }
 
 // one wavefront per row below block k: r_i -= L_i,k-block . y_k
@@ -762,15 +842,25 @@ __global__ __launch_bounds__(256) void k_dtrsv_fwd_update(DenseView v, int k) {
   if (lane == 0) v.r[row] -= s;
 }
 
-// backward: x_k = Linv_kk^T r_k, then r_j -= L_kj^T x_k for columns left of block k
-__global__ __launch_bounds__(128) void k_dtrsv_bwd_diag(DenseView v, int k) {
-  constexpr int nb = kCRMaxN;
-  const int c = threadIdx.x;
-  if (c >= nb) return;
+// backward: x_k = Linv_kk^T r_k: thread (c, part) sums rows m = c.. of its
+// quarter for column c (consecutive threads read consecutive columns of one
+// row: coalesced), the four quarters are added in LDS in a fixed order.
+__global__ __launch_bounds__(512) void k_dtrsv_bwd_diag(DenseView v, int k) {
+  constexpr int nb = kCRMaxN, q = nb / 4;
+  __shared__ double part[4][nb];
+  const int t = threadIdx.x, c = t % nb, h = t / nb;
   const double *Lk = v.Linv + (size_t)k * nb * nb, *rk = v.r + (size_t)k * nb;
-  double s = 0.0;
-  for (int m = c; m < nb; ++m) s += Lk[(size_t)m * nb + c] * rk[m];
-  v.x[(size_t)k * nb + c] = s;
+  if (h < 4) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < q; ++i) {
+      const int m = h * q + i;
+      s += m >= c ? Lk[(size_t)m * nb + c] * rk[m] : 0.0;
+    }
+    part[h][c] = s;
+  }
+  __syncthreads();
+  if (t < nb) v.x[(size_t)k * nb + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
 }
 
 __global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k) {
@@ -778,9 +868,10 @@ __global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= k * nb) return;
   const double *Lk = v.L + (size_t)k * nb * v.n + c, *xk = v.x + (size_t)k * nb;
-  double s = 0.0;
-  for (int m = 0; m < nb; ++m) s += Lk[(size_t)m * v.n] * xk[m];
-  v.r[c] -= s;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 28
+  for (int m = 0; m < nb; ++m) s[m & 3] += Lk[(size_t)m * v.n] * xk[m];
+  v.r[c] -= (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
@@ -794,19 +885,19 @@ int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double
     hipLaunchKernelGGL(k_dchol_diag, dim3(1), dim3(512), lds, st, v, k);
     const int m = nblk - 1 - k;
     if (m == 0) break;
-    const int np = m * nt * nt, nu = m * (m + 1) / 2 * nt * nt;
+    const int np = m * nt * nt, npairs = m * (m + 1) / 2;
     hipLaunchKernelGGL(k_dchol_panel, dim3(xcd_grid(np)), dim3(64), 0, st, v, k, np);
-    hipLaunchKernelGGL(k_dchol_update, dim3(xcd_grid(nu)), dim3(64), 0, st, v, k, nu);
+    hipLaunchKernelGGL(k_dchol_update_blk, dim3(xcd_grid(npairs)), dim3(512), 0, st, v, k, npairs);
   }
   for (int k = 0; k < nblk; ++k) {
-    hipLaunchKernelGGL(k_dtrsv_fwd_diag, dim3(1), dim3(128), 0, st, v, k);
+    hipLaunchKernelGGL(k_dtrsv_fwd_diag, dim3(1), dim3(512), 0, st, v, k);
     const int rows = n - (k + 1) * nb;
     if (rows > 0) hipLaunchKernelGGL(k_dtrsv_fwd_update, dim3((rows + 3) / 4), dim3(256), 0, st, v, k);
   }
   // y (in x) becomes the right-hand side of the backward pass
   if (hipMemcpyAsync(r, x, sizeof(double) * n, hipMemcpyDeviceToDevice, st) != hipSuccess) return -2;
   for (int k = nblk - 1; k >= 0; --k) {
-    hipLaunchKernelGGL(k_dtrsv_bwd_diag, dim3(1), dim3(128), 0, st, v, k);
+    hipLaunchKernelGGL(k_dtrsv_bwd_diag, dim3(1), dim3(512), 0, st, v, k);
     if (k > 0) hipLaunchKernelGGL(k_dtrsv_bwd_update, dim3((k * nb + 255) / 256), dim3(256), 0, st, v, k);
   }
   return 0;
