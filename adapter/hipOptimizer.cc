@@ -25,6 +25,7 @@
 #include <string>
 
 #include "Converter.h"
+#include "Thirdparty/g2o/g2o/types/sim3.h"  // value type only (the solve runs in libsqrtlm)
 #include "KeyFrame.h"
 #include "Map.h"
 #include "MapPoint.h"
@@ -533,6 +534,136 @@ void hipOptimizer::EndCaptureBA(unsigned long nLoopKF) {
   write_capture(*t_capture, "ba", nLoopKF);
   delete t_capture;
   t_capture = nullptr;
+}
+
+
+
+// ---------------------------------------------------------------- essential graph
+namespace {
+
+// g2o::Sim3 <-> the ABI's [qx qy qz qw tx ty tz s] (sqrtlm.h, sqlm_eg_set_problem)
+void sim3_pack(const g2o::Sim3& S, double* o) {
+  const Eigen::Quaterniond& q = S.rotation();
+  o[0] = q.x(); o[1] = q.y(); o[2] = q.z(); o[3] = q.w();
+  o[4] = S.translation()[0]; o[5] = S.translation()[1]; o[6] = S.translation()[2];
+  o[7] = S.scale();
+}
+g2o::Sim3 sim3_unpack(const double* o) {
+  return g2o::Sim3(Eigen::Quaterniond(o[3], o[0], o[1], o[2]), Eigen::Vector3d(o[4], o[5], o[6]), o[7]);
+}
+
+}  // namespace
+
+void hipOptimizer::OptimizeEssentialGraph(Map* pMap, KeyFrame* pLoopKF, KeyFrame* pCurKF,
+                                          const LoopClosing::KeyFrameAndPose& NonCorrectedSim3,
+                                          const LoopClosing::KeyFrameAndPose& CorrectedSim3,
+                                          const std::map<KeyFrame*, std::set<KeyFrame*> >& LoopConnections,
+                                          const bool& bFixScale) {
+  sqlm_ctx* ctx = thread_ctx();
+  if (!ctx) return;
+  const std::vector<KeyFrame*> vpKFs = pMap->GetAllKeyFrames();
+  const std::vector<MapPoint*> vpMPs = pMap->GetAllMapPoints();
+  const unsigned int nMaxKFid = pMap->GetMaxKFid();
+  std::vector<g2o::Sim3, Eigen::aligned_allocator<g2o::Sim3> > vScw(nMaxKFid + 1);
+  std::vector<g2o::Sim3, Eigen::aligned_allocator<g2o::Sim3> > vCorrectedSwc(nMaxKFid + 1);
+  const int minFeat = 100;
+  // vertices (g2oOptimizer.cc:1240-1278): one per good keyframe; the ABI wants
+  // them in g2o id order, so vertex v <-> mnId through a dense index
+  std::vector<int> vidx(nMaxKFid + 1, -1);
+  std::vector<KeyFrame*> order;
+  for (KeyFrame* pKF : vpKFs)
+    if (!pKF->isBad()) order.push_back(pKF);
+  std::sort(order.begin(), order.end(), [](KeyFrame* a, KeyFrame* b) { return a->mnId < b->mnId; });
+  std::vector<double> Siw(8 * order.size());
+  std::vector<uint8_t> fixed(order.size(), 0);
+  for (size_t v = 0; v < order.size(); ++v) {
+    KeyFrame* pKF = order[v];
+    const int nIDi = pKF->mnId;
+    auto it = CorrectedSim3.find(pKF);
+    if (it != CorrectedSim3.end()) {
+      vScw[nIDi] = it->second;
+    } else {
+      const Eigen::Matrix<double, 3, 3> Rcw = Converter::toMatrix3d(pKF->GetRotation());
+      const Eigen::Matrix<double, 3, 1> tcw = Converter::toVector3d(pKF->GetTranslation());
+      vScw[nIDi] = g2o::Sim3(Rcw, tcw, 1.0);
+    }
+    sim3_pack(vScw[nIDi], &Siw[8 * v]);
+    fixed[v] = pKF == pLoopKF;
+    vidx[nIDi] = (int)v;
+  }
+  // edges in the reference's insertion order (:1280-1417); an edge whose vertex
+  // is missing (a bad keyframe) is rejected by g2o's addEdge, so it is skipped
+  std::vector<int32_t> ei, ej;
+  std::vector<double> Sji;
+  auto add = [&](unsigned long i, unsigned long j, const g2o::Sim3& S) {
+    if (i > nMaxKFid || j > nMaxKFid || vidx[i] < 0 || vidx[j] < 0) return;
+    ei.push_back(vidx[i]);
+    ej.push_back(vidx[j]);
+    Sji.resize(Sji.size() + 8);
+    sim3_pack(S, &Sji[Sji.size() - 8]);
+  };
+  auto ncs = [&](KeyFrame* k) -> g2o::Sim3 {
+    auto f = NonCorrectedSim3.find(k);
+    return f != NonCorrectedSim3.end() ? f->second : vScw[k->mnId];
+  };
+  std::set<std::pair<long unsigned int, long unsigned int> > sInsertedEdges;
+  for (auto mit = LoopConnections.begin(); mit != LoopConnections.end(); ++mit) {
+    KeyFrame* pKF = mit->first;
+    const long unsigned int nIDi = pKF->mnId;
+    const g2o::Sim3 Swi = vScw[nIDi].inverse();
+    for (KeyFrame* pKFj : mit->second) {
+      const long unsigned int nIDj = pKFj->mnId;
+      if ((nIDi != pCurKF->mnId || nIDj != pLoopKF->mnId) && pKF->GetWeight(pKFj) < minFeat) continue;
+      add(nIDi, nIDj, vScw[nIDj] * Swi);
+      sInsertedEdges.insert(std::make_pair(std::min(nIDi, nIDj), std::max(nIDi, nIDj)));
+    }
+  }
+  for (KeyFrame* pKF : vpKFs) {
+    const long unsigned int nIDi = pKF->mnId;
+    const g2o::Sim3 Swi = ncs(pKF).inverse();
+    KeyFrame* pParentKF = pKF->GetParent();
+    if (pParentKF) add(nIDi, pParentKF->mnId, ncs(pParentKF) * Swi);  // spanning tree
+    const std::set<KeyFrame*> sLoopEdges = pKF->GetLoopEdges();
+    for (KeyFrame* pLKF : sLoopEdges)
+      if (pLKF->mnId < pKF->mnId) add(nIDi, pLKF->mnId, ncs(pLKF) * Swi);
+    for (KeyFrame* pKFn : pKF->GetCovisiblesByWeight(minFeat)) {  // covisibility
+      if (pKFn && pKFn != pParentKF && !pKF->hasChild(pKFn) && !sLoopEdges.count(pKFn) && !pKFn->isBad() &&
+          pKFn->mnId < pKF->mnId) {
+        if (sInsertedEdges.count(std::make_pair(std::min(pKF->mnId, pKFn->mnId), std::max(pKF->mnId, pKFn->mnId))))
+          continue;
+        add(nIDi, pKFn->mnId, ncs(pKFn) * Swi);
+      }
+    }
+  }
+  // initializeOptimization(); setUserLambdaInit(1e-16); optimize(20), identity information
+  if (!report(sqlm_eg_set_problem(ctx, (int)order.size(), Siw.data(), fixed.data(), bFixScale ? 1 : 0,
+                                  (int64_t)ei.size(), ei.data(), ej.data(), Sji.data(), nullptr),
+              "sqlm_eg_set_problem"))
+    return;
+  sqlm_stats st;
+  int n_iter = 0;
+  if (!report(sqlm_eg_optimize(ctx, 20, 1e-16, nullptr, &st, &n_iter), "sqlm_eg_optimize")) return;
+  if (!report(sqlm_eg_get_poses(ctx, Siw.data()), "sqlm_eg_get_poses")) return;
+  // write-back (:1427-1531): SE3 poses from the corrected Sim3, map points
+  // through their reference keyframe's correction
+  std::unique_lock<std::mutex> lock(pMap->mMutexMapUpdate);
+  for (size_t v = 0; v < order.size(); ++v) {
+    KeyFrame* pKFi = order[v];
+    const g2o::Sim3 CorrectedSiw = sim3_unpack(&Siw[8 * v]);
+    vCorrectedSwc[pKFi->mnId] = CorrectedSiw.inverse();
+    const Eigen::Matrix3d eigR = CorrectedSiw.rotation().toRotationMatrix();
+    Eigen::Vector3d eigt = CorrectedSiw.translation();
+    eigt *= (1. / CorrectedSiw.scale());
+    pKFi->SetPose(Converter::toCvSE3(eigR, eigt));
+  }
+  for (MapPoint* pMP : vpMPs) {
+    if (pMP->isBad()) continue;
+    const int nIDr = pMP->mnCorrectedByKF == pCurKF->mnId ? (int)pMP->mnCorrectedReference
+                                                          : (int)pMP->GetReferenceKeyFrame()->mnId;
+    const Eigen::Matrix<double, 3, 1> P = Converter::toVector3d(pMP->GetWorldPos());
+    pMP->SetWorldPos(Converter::toCvMat(vCorrectedSwc[nIDr].map(vScw[nIDr].map(P))));
+    pMP->UpdateNormalAndDepth();
+  }
 }
 
 }  // namespace ORB_SLAM2

@@ -2,7 +2,8 @@
 //
 // Drop-in sibling of g2oOptimizer (src/backend/g2oOptimizer.cc) for the
 // calls the MI355X backend implements: LocalBundleAdjustment,
-// BundleAdjustment and GlobalBundleAdjustemnt (include/backend/Optimizer.h:50-56).
+// BundleAdjustment, GlobalBundleAdjustemnt and OptimizeEssentialGraph
+// (include/backend/Optimizer.h:50-65).
 // It is meant to be added to the reference tree as include/backend/hipOptimizer.h
 // + src/backend/hipOptimizer.cc and selected in Optimizer.cc's dispatch
 // (see INTEGRATION.md §4); it builds against the reference's own headers and
@@ -15,9 +16,12 @@
 #ifndef HIP_OPTIMIZER_H
 #define HIP_OPTIMIZER_H
 
+#include <map>
+#include <set>
 #include <vector>
 
 #include "Eigen/Core"
+#include "LoopClosing.h"
 
 namespace ORB_SLAM2 {
 
@@ -36,6 +40,13 @@ class hipOptimizer {
   // g2oOptimizer::GlobalBundleAdjustemnt (g2oOptimizer.cc:80-95): every KF and MP of the map.
   static void GlobalBundleAdjustemnt(Map* pMap, int nIterations, bool* pbStopFlag, unsigned long nLoopKF,
                                      bool bRobust);
+  // g2oOptimizer::OptimizeEssentialGraph (g2oOptimizer.cc:1212-1534) on the GPU
+  // (sqlm_eg_*): same vertices, edges, insertion order and write-back.
+  static void OptimizeEssentialGraph(Map* pMap, KeyFrame* pLoopKF, KeyFrame* pCurKF,
+                                     const LoopClosing::KeyFrameAndPose& NonCorrectedSim3,
+                                     const LoopClosing::KeyFrameAndPose& CorrectedSim3,
+                                     const std::map<KeyFrame*, std::set<KeyFrame*> >& LoopConnections,
+                                     const bool& bFixScale);
 
   // Capture mode around the g2o backend (Optimizer.cc dispatch): Begin*
   // records the seam inputs, End* the g2o write-back, then the file is written.
