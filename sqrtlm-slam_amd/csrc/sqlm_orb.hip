@@ -40,6 +40,9 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -309,12 +312,23 @@ __device__ __forceinline__ int refl101(int i, int n) {
 }
 
 constexpr int kBTX = 32, kBTY = 8;
-__global__ __launch_bounds__(256) void k_orb_blur(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int w,
-                                                  int h, BlurK k) {
+// all levels in one launch: block b belongs to the level whose tile range holds it
+struct BlurLevels {
+  int n;
+  int off[kMaxLevels], w[kMaxLevels], h[kMaxLevels], tx[kMaxLevels], tile0[kMaxLevels + 1];
+};
+
+__global__ __launch_bounds__(256) void k_orb_blur(const uint8_t *__restrict__ pyr, uint8_t *__restrict__ blur,
+                                                  BlurLevels lv, BlurK k) {
   __shared__ uint8_t pix[kBTY + 6][kBTX + 6];
   __shared__ int R[kBTY + 6][kBTX];
+  int L = 0;
+  while (L + 1 < lv.n && (int)blockIdx.x >= lv.tile0[L + 1]) ++L;
+  const int b = blockIdx.x - lv.tile0[L], w = lv.w[L], h = lv.h[L];
+  const uint8_t *src = pyr + lv.off[L];
+  uint8_t *dst = blur + lv.off[L];
   const int tx = threadIdx.x % kBTX, ty = threadIdx.x / kBTX;
-  const int x0 = blockIdx.x * kBTX, y0 = blockIdx.y * kBTY;
+  const int x0 = (b % lv.tx[L]) * kBTX, y0 = (b / lv.tx[L]) * kBTY;
   for (int p = threadIdx.x; p < (kBTY + 6) * (kBTX + 6); p += 256) {
     const int yy = p / (kBTX + 6), xx = p - yy * (kBTX + 6);
     pix[yy][xx] = src[(size_t)refl101(y0 + yy - 3, h) * w + refl101(x0 + xx - 3, w)];
@@ -749,7 +763,69 @@ BlurK gauss_kernel_7x7_s2() {  // getGaussianKernel(7, 2, CV_32F) -> x256 ints
 
 // ---------------------------------------------------------------------- engine
 
+// Persistent host workers for the per-level quadtrees: run(n, f) calls f(i)
+// for i = 1..n-1 on the workers and f(0) on the caller, then waits. Workers
+// live as long as the engine (no thread start-up per frame).
+class LevelPool {
+ public:
+  ~LevelPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+  void run(int n, const std::function<void(int)> &f) {
+    while ((int)th_.size() < n - 1) {
+      const int id = (int)th_.size() + 1;
+      th_.emplace_back([this, id] { worker(id); });
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &f;
+      n_ = n;
+      pending_ = n - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void worker(int id) {
+    long seen = 0;
+    for (;;) {
+      const std::function<void(int)> *job = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        if (quit_) return;
+        seen = gen_;
+        if (id < n_) job = job_;
+      }
+      if (!job) continue;
+      (*job)(id);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)> *job_ = nullptr;
+  int n_ = 0, pending_ = 0;
+  long gen_ = 0;
+  bool quit_ = false;
+};
+
 struct OrbEngine {
+  LevelPool pool;
+  std::vector<int> cells_key;  // geometry of the uploaded cell table
+  void *cells_ptr = nullptr;
   hipStream_t st = nullptr;
   struct Buf {
     void *p = nullptr;
@@ -915,8 +991,14 @@ int OrbEngine::extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<
                        lw[l - 1], lh[l - 1], d_pyr + loff[l], lw[l], lh[l], scale_x, scale_y, resize_vec_end(lw[l]));
   }
   mark(1);
-  if (hipMemcpyAsync(d_cells, hc.data(), sizeof(OrbCell) * ncell, hipMemcpyHostToDevice, st) != hipSuccess)
-    return SQLM_ERR_HIP;
+  // the cell table depends only on the geometry: upload it when it changes
+  const std::vector<int> key = {w, h, L, (int)(p->scale_factor * 1e6f)};
+  if (key != cells_key || cells.p != cells_ptr) {
+    if (hipMemcpyAsync(d_cells, hc.data(), sizeof(OrbCell) * ncell, hipMemcpyHostToDevice, st) != hipSuccess)
+      return SQLM_ERR_HIP;
+    cells_key = key;
+    cells_ptr = cells.p;
+  }
   hipLaunchKernelGGL(k_orb_fast, dim3(ncell), dim3(256), 0, st, d_pyr, d_cells, p->ini_th_fast, p->min_th_fast,
                      d_cellkp, d_cnt);
   mark(2);
@@ -935,9 +1017,17 @@ int OrbEngine::extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<
   if (hipEventRecord(ev_copy, st) != hipSuccess) return SQLM_ERR_HIP;
   // the blur does not depend on the quadtree: it runs while the host distributes
   const BlurK bk = gauss_kernel_7x7_s2();
-  for (int l = 0; l < L; ++l)
-    hipLaunchKernelGGL(k_orb_blur, dim3((lw[l] + kBTX - 1) / kBTX, (lh[l] + kBTY - 1) / kBTY), dim3(256), 0, st,
-                       d_pyr + loff[l], d_blur + loff[l], lw[l], lh[l], bk);
+  BlurLevels bl;
+  bl.n = L;
+  bl.tile0[0] = 0;
+  for (int l = 0; l < L; ++l) {
+    bl.off[l] = loff[l];
+    bl.w[l] = lw[l];
+    bl.h[l] = lh[l];
+    bl.tx[l] = (lw[l] + kBTX - 1) / kBTX;
+    bl.tile0[l + 1] = bl.tile0[l] + bl.tx[l] * ((lh[l] + kBTY - 1) / kBTY);
+  }
+  hipLaunchKernelGGL(k_orb_blur, dim3(bl.tile0[L]), dim3(256), 0, st, d_pyr, d_blur, bl, bk);
   mark(4);
   if (hipEventSynchronize(ev_copy) != hipSuccess) return SQLM_ERR_HIP;
   // quadtree per level (host)
@@ -953,12 +1043,8 @@ int OrbEngine::extract_impl(const sqlm_orb_params *p, int w, int h, std::vector<
     const int minB = kEdge - 3;
     sel[l] = distribute_quadtree(keys, minB, lw[l] - kEdge + 3, minB, lh[l] - kEdge + 3, nfeat[l]);
   };
-  {  // levels are independent: level 0 (the largest) here, the others on helper threads
-    std::vector<std::thread> th;
-    for (int l = 1; l < L; ++l) th.emplace_back(level_tree, l);
-    level_tree(0);
-    for (auto &t : th) t.join();
-  }
+  // levels are independent: level 0 (the largest) here, the others on the pool
+  pool.run(L, std::function<void(int)>(level_tree));
   std::vector<OrbDescIn> hin;
   for (int l = 0; l < L; ++l)
     for (const Cand &c : sel[l]) hin.push_back(OrbDescIn{c.x + (kEdge - 3), c.y + (kEdge - 3), c.response, l});
