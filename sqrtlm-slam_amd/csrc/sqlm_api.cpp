@@ -87,6 +87,10 @@ struct sqlm_ctx {
   OrbEngine *orb = nullptr;
   // ---- timing ----
   hipEvent_t ev[2 * SQLM_NKERNEL_TIMERS] = {};
+  // side stream: the camera pass runs concurrently with the landmark QR
+  // (independent inputs and outputs); fork / join through two events
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   bool timing = false;
   double kernel_ms_acc[SQLM_NKERNEL_TIMERS] = {};
   int kernel_ms_n = 0;
@@ -656,18 +660,24 @@ void acc_events(sqlm_ctx *c, int i0, int i1) {
 // computeActiveErrors + buildSystem for the current state.
 int linearize(sqlm_ctx *c) {
   DevProblem &d = c->d;
+  // the camera pass (H_pp, b_p, LiDAR) reads only the state, like the landmark
+  // QR: fork it onto the side stream and join before anything consumes H_pp
+  HIP_OK(hipEventRecord(c->ev_fork, c->stream));
+  HIP_OK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  if (c->timing) HIP_OK(hipEventRecord(c->ev[2], c->side));
+  launch_camera_pass(d, c->side);
+  if (c->timing) HIP_OK(hipEventRecord(c->ev[3], c->side));
+  HIP_OK(hipEventRecord(c->ev_join, c->side));
   tmark(c, 0, false);  // maxdiag was zeroed by the last k_reduce (or prepare)
   for (size_t b = 0; b < c->buckets.size(); ++b) launch_linearize(d, c->buckets[b], c->bucket_part_off[b], c->stream);
   tmark(c, 0, true);
-  tmark(c, 1, false);
-  launch_camera_pass(d, c->stream);
+  HIP_OK(hipStreamWaitEvent(c->stream, c->ev_join, 0));
   if (c->comm.enabled() && c->need_maxdiag) {  // lambda_0 needs the summed pose diagonals
     launch_pose_diag(d, c->stream);
     if (comm_allreduce_dev(c->comm, d.hdiag, 6 * (int64_t)d.nP, SQLM_DT_F64, SQLM_OP_SUM, c->stream))
       return SQLM_ERR_COMM;
     launch_pose_maxdiag(d, c->stream);
   }
-  tmark(c, 1, true);
   return SQLM_OK;
 }
 
@@ -937,6 +947,12 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   // timing-only events: no system-scope fence, which would flush caches and
   // leave a ~10 us bubble between the kernels they separate
   for (auto &e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+    sqlm_ctx_destroy(c);
+    return SQLM_ERR_HIP;
+  }
   *out = c;
   return SQLM_OK;
 }
@@ -953,6 +969,9 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->side) (void)hipStreamDestroy(c->side);
   (void)hipStreamDestroy(c->stream);
   delete c;
   return SQLM_OK;
