@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|^E " gpurun_out/pytest_gpu.log | head -20; exit $rc; }
+timeout -k 10 300 python -u bench.py --config eg > gpurun_out/bench_eg.json 2> gpurun_out/bench_eg.err || exit 1
+bash scripts/gpu_egprof.sh

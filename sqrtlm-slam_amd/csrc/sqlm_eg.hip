@@ -33,6 +33,10 @@ constexpr int kEGMaxParts = 8192;  // per partial region
 
 struct EGDev {
   int nK = 0, nP = 0, n = 0, n_pad = 0, fix_scale = 0;
+  // vertex slots: band vertices in slots [0, band_slots), border vertices in
+  // [border0, border0 + border_slots); rows 7 slot .. 7 slot + 6; other rows
+  // are padding (identity in A, zero in b and x)
+  int band_slots = 0, border0 = 0, border_slots = 0;
   int64_t nE = 0;                       // active edges
   const int *act = nullptr;             // [nE] edge id
   const int *ei = nullptr, *ej = nullptr;  // [nE] vertex ids
@@ -49,6 +53,10 @@ struct EGDev {
   double *partials = nullptr;           // 3 regions of kEGMaxParts
   double *scalars = nullptr;            // chi_cur, chi_new, scale, maxdiag, ok
 };
+
+__device__ __forceinline__ bool row_valid(const EGDev &d, int r) {
+  return r < 7 * d.band_slots || (r >= 7 * d.border0 && r < 7 * (d.border0 + d.border_slots));
+}
 
 __device__ __forceinline__ double info_at(const EGDev &d, int64_t k, int r, int c) {
   return d.info ? d.info[49 * k + 7 * r + c] : (r == c ? 1.0 : 0.0);
@@ -218,7 +226,7 @@ __global__ __launch_bounds__(256) void k_eg_damp(EGDev d, double *A, double lamb
   const int r = (int)(g / np), c = (int)(g % np);
   double v = 0.0;
   if (c <= r) {
-    if (r < d.n) v = d.H0[g] + (r == c ? lambda : 0.0);
+    if (row_valid(d, r)) v = d.H0[g] + (r == c ? lambda : 0.0);
     else v = r == c ? 1.0 : 0.0;
   }
   A[g] = v;
@@ -227,7 +235,8 @@ __global__ __launch_bounds__(256) void k_eg_damp(EGDev d, double *A, double lamb
 __global__ __launch_bounds__(256) void k_eg_maxdiag(EGDev d) {
   __shared__ double red[4];
   double m = 0.0;
-  for (int j = threadIdx.x; j < d.n; j += blockDim.x) m = fmax(m, fabs(d.H0[(size_t)j * d.n_pad + j]));
+  for (int j = threadIdx.x; j < d.n_pad; j += blockDim.x)
+    if (row_valid(d, j)) m = fmax(m, fabs(d.H0[(size_t)j * d.n_pad + j]));
 #pragma unroll
   for (int s = 32; s >= 1; s >>= 1) m = fmax(m, __shfl_xor(m, s, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -254,7 +263,7 @@ __global__ __launch_bounds__(kEGBlock) void k_eg_scale(EGDev d, const double *__
   __shared__ double red[kEGBlock / 64];
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   double v = 0.0;
-  if (j < d.n) v = x[j] * (lambda * x[j] + d.b[j]);
+  if (j < d.n_pad && row_valid(d, j)) v = x[j] * (lambda * x[j] + d.b[j]);
   const double s = eg_block_sum(v, red);
   if (threadIdx.x == 0) d.partials[2 * kEGMaxParts + blockIdx.x] = s;
 }
@@ -334,12 +343,65 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
     if (vact[p] && !fixed[p]) hid[p] = nP++;
   if (nP == 0) return SQLM_OK;  // "0 vertices to optimize": optimize() returns -1
   const int64_t A_ = (int64_t)act.size();
-  const int n = 7 * nP, n_pad = std::max(kCRMaxN, (n + kCRMaxN - 1) / kCRMaxN * kCRMaxN);
+  const int n = 7 * nP;
+  // Block-arrow layout: g2o's id order keeps the essential graph banded except
+  // for the loop edges. Vertices covering every edge longer than one 112-row
+  // block (16 vertices) move to a dense border after the band, so the band is
+  // block-tridiagonal and the factor only touches the band + border blocks.
+  // Dense layout when the border would exceed a third of the system.
+  constexpr int kVB = kCRMaxN / 7;
+  std::vector<uint8_t> border(nP, 0);
+  {
+    std::vector<int> nlong(nP, 0);
+    std::vector<std::pair<int, int>> longe;
+    for (int e : act) {
+      const int hi = hid[ei[e]], hj = hid[ej[e]];
+      if (hi >= 0 && hj >= 0 && std::abs(hi - hj) > kVB) {
+        longe.emplace_back(hi, hj);
+        ++nlong[hi];
+        ++nlong[hj];
+      }
+    }
+    for (auto &pr : longe)
+      if (!border[pr.first] && !border[pr.second])
+        border[nlong[pr.first] > nlong[pr.second] || (nlong[pr.first] == nlong[pr.second] && pr.first > pr.second)
+                   ? pr.first
+                   : pr.second] = 1;
+  }
+  int nborder = 0;
+  for (int h = 0; h < nP; ++h) nborder += border[h];
+  const bool arrow = 3 * nborder <= nP && std::getenv("SQLM_EG_DENSE") == nullptr;
+  int band_slots = nP, border0 = nP, band_blk = 0;
+  {
+    std::vector<int> slot(nP);
+    if (arrow) {
+      int nb = 0;
+      for (int h = 0; h < nP; ++h)
+        if (!border[h]) slot[h] = nb++;
+      band_blk = (nb + kVB - 1) / kVB;
+      band_slots = nb;
+      border0 = band_blk * kVB;
+      int q = 0;
+      for (int h = 0; h < nP; ++h)
+        if (border[h]) slot[h] = border0 + q++;
+      nborder = q;
+    } else {
+      for (int h = 0; h < nP; ++h) slot[h] = h;
+      nborder = 0;
+    }
+    for (int p = 0; p < nK; ++p)
+      if (hid[p] >= 0) hid[p] = slot[hid[p]];
+  }
+  const int nslots = arrow ? border0 + nborder : nP;
+  const int n_pad = std::max(kCRMaxN, (7 * nslots + kCRMaxN - 1) / kCRMaxN * kCRMaxN);
   if ((int64_t)n_pad * n_pad > (int64_t)1 << 31) return SQLM_ERR_UNSUPPORTED;  // dense path limit (~46k dims)
-  if ((A_ + kEGBlock - 1) / kEGBlock > kEGMaxParts || (n + kEGBlock - 1) / kEGBlock > kEGMaxParts)
+  if ((A_ + kEGBlock - 1) / kEGBlock > kEGMaxParts || (n_pad + kEGBlock - 1) / kEGBlock > kEGMaxParts)
     return SQLM_ERR_UNSUPPORTED;
   // assembly lists: diagonal blocks, off-diagonal pairs (lower), b vectors; sources in edge order
-  std::vector<std::vector<int>> diag(nP), bvec(nP);
+  std::vector<std::vector<int>> diag(nslots), bvec(nslots);
+  std::vector<uint8_t> used(nslots, 0);
+  for (int p = 0; p < nK; ++p)
+    if (hid[p] >= 0) used[hid[p]] = 1;
   std::map<std::pair<int, int>, std::vector<int>> off;
   std::vector<int> aei(A_), aej(A_);
   std::vector<double> aC(8 * A_), ainfo(info.empty() ? 0 : 49 * A_);
@@ -358,7 +420,8 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
     }
   }
   std::vector<int> dst, sptr{0}, src;
-  for (int v = 0; v < nP; ++v) {
+  for (int v = 0; v < nslots; ++v) {
+    if (!used[v]) continue;
     dst.push_back(v << 16 | v);
     src.insert(src.end(), diag[v].begin(), diag[v].end());
     sptr.push_back((int)src.size());
@@ -368,16 +431,18 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
     src.insert(src.end(), kv.second.begin(), kv.second.end());
     sptr.push_back((int)src.size());
   }
-  for (int v = 0; v < nP; ++v) {
+  for (int v = 0; v < nslots; ++v) {
+    if (!used[v]) continue;
     dst.push_back(-(v + 1));
     src.insert(src.end(), bvec[v].begin(), bvec[v].end());
     sptr.push_back((int)src.size());
   }
-  if (nP > 0xffff) return SQLM_ERR_UNSUPPORTED;
+  if (nslots > 0xffff) return SQLM_ERR_UNSUPPORTED;
   release();
   if (!h_scal && hipHostMalloc((void **)&h_scal, 8 * sizeof(double)) != hipSuccess) return SQLM_ERR_HIP;
   EGDev d;
   d.nK = nK; d.nP = nP; d.n = n; d.n_pad = n_pad; d.fix_scale = fix_scale; d.nE = A_;
+  d.band_slots = band_slots; d.border0 = border0; d.border_slots = nborder;
   int *d_act = upload(act), *d_ei = upload(aei), *d_ej = upload(aej), *d_hid = upload(hid);
   double *d_C = upload(aC), *d_info = info.empty() ? nullptr : upload(ainfo);
   double *Sd[2] = {upload(S), alloc<double>(S.size())};
@@ -401,7 +466,7 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
   d.dst = d_dst; d.src_ptr = d_sptr; d.src = d_src;
   if (hipMemsetAsync(d.b, 0, sizeof(double) * n_pad, st) != hipSuccess) return SQLM_ERR_HIP;
   const int nD = (int)dst.size();
-  const int eb = (int)((A_ + kEGBlock - 1) / kEGBlock), sb = (n + kEGBlock - 1) / kEGBlock;
+  const int eb = (int)((A_ + kEGBlock - 1) / kEGBlock), sb = (n_pad + kEGBlock - 1) / kEGBlock;
   auto fetch = [&]() -> int {
     if (hipMemcpyAsync(h_scal, d.scalars, 8 * sizeof(double), hipMemcpyDeviceToHost, st) != hipSuccess) return -1;
     return hipStreamSynchronize(st) == hipSuccess ? 0 : -1;
@@ -434,7 +499,7 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
       hipLaunchKernelGGL(k_eg_damp, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, st, d, A, lambda);
       if (hipMemcpyAsync(r, d.b, sizeof(double) * n_pad, hipMemcpyDeviceToDevice, st) != hipSuccess)
         return SQLM_ERR_HIP;
-      if (launch_dense_spd_solve(A, L, Linv, r, x, flags, n_pad, st)) return SQLM_ERR_HIP;
+      if (launch_dense_spd_solve(A, L, Linv, r, x, flags, n_pad, st, arrow ? band_blk : 0)) return SQLM_ERR_HIP;
       hipLaunchKernelGGL(k_eg_update, dim3((nK + 255) / 256), dim3(256), 0, st, d, Sd[0], Sd[1], x);
       hipLaunchKernelGGL(k_eg_errors, dim3(eb), dim3(kEGBlock), 0, st, d, Sd[1], 1);
       hipLaunchKernelGGL(k_eg_scale, dim3(sb), dim3(kEGBlock), 0, st, d, x, lambda);

@@ -168,9 +168,12 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
                     hipStream_t st);
 // Dense SPD solve (sqlm_rcs_solve.hip): A (n x n, lower, n % kCRMaxN == 0) is
 // factored in place into L (+ diagonal block inverses Linv), r is consumed,
-// x = A^-1 r; flags[0] is cleared on a non-positive pivot.
+// x = A^-1 r; flags[0] is cleared on a non-positive pivot. band > 0: A is a
+// block arrow — its first `band` blocks of kCRMaxN form a block-tridiagonal
+// band, the rest a dense border — and only the blocks the factor fills are
+// touched (band = 0: fully dense).
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
-                           hipStream_t st);
+                           hipStream_t st, int band = 0);
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off,
                             hipStream_t st);

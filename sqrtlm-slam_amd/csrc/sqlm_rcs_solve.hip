@@ -26,6 +26,8 @@
 //     cross-lane reduction.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "sqlm_internal.h"
 
 namespace sqlm {
@@ -681,6 +683,22 @@ __global__ __launch_bounds__(512) void k_dchol_diag(DenseView v, int k) {
   double *Lo = v.Linv + (size_t)k * nb * nb;
   for (int r = wave; r < nb; r += nw)
     for (int c = lane; c < nb; c += 64) Lo[r * nb + c] = linv_at(L, ld, Dinv, r, c);
+  // fused forward step: y_k = Linv_kk r_k (r_k already holds every earlier
+  // block's update) into x_k; thread (row, quarter), quarters summed in order
+  constexpr int q = nb / 4;
+  const int t = threadIdx.x, row = t % nb, h = t / nb;
+  const double *rk = v.r + (size_t)k * nb;
+  if (h < 4) {
+    double s = 0.0;
+#pragma unroll 4
+    for (int i = 0; i < q; ++i) {
+      const int m = h * q + i;
+      if (m <= row) s += linv_at(L, ld, Dinv, row, m) * rk[m];
+    }
+    W[h * nb + row] = s;
+  }
+  __syncthreads();
+  if (t < nb) v.x[(size_t)k * nb + t] = ((W[t] + W[nb + t]) + W[2 * nb + t]) + W[3 * nb + t];
 }
 
 // 16x16 tile of X Y^T over K = kend (X, Y row-major with their own leading dims).
@@ -704,31 +722,31 @@ __device__ __forceinline__ d4 tile_xyt(const double *X, int ldx, const double *Y
   return acc;
 }
 
-// L_ik = A_ik Linv_kk^T for every block row i > k; one wavefront per 16x16 tile.
-__global__ __launch_bounds__(64) void k_dchol_panel(DenseView v, int k, int total) {
-  const int lb = xcd_block(total);
-  if (lb >= total) return;
-  constexpr int nb = kCRMaxN, nt = nb / 16;
-  const int bi = k + 1 + lb / (nt * nt), t = lb % (nt * nt), ti = t / nt, tj = t % nt;
-  const double *X = v.A + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb;
-  const double *Y = v.Linv + (size_t)k * nb * nb + (size_t)(16 * tj) * nb;  // Linv rows 16 tj..: lower, K <= 16 (tj+1)
-  const d4 acc = tile_xyt(X, v.n, Y, nb, 16 * (tj + 1));
-  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
-  double *o = v.L + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb + 16 * tj;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[(size_t)(k4 + 4 * j) * v.n + r16] = acc[j];
+// Block rows of L below block k that can be nonzero: an optional `extra` row
+// (the next band block of a block-arrow matrix) then the range [r0, r1).
+// Dense: extra = -1, [k+1, nblk). Arrow (block-tridiagonal band of `band`
+// blocks, dense border after it), band block k: extra = k+1 (if in the band),
+// range = the border.
+struct RowSet {
+  int extra, r0, r1;
+  __host__ __device__ int count() const { return (extra >= 0) + (r1 - r0); }
+  __host__ __device__ int at(int i) const { return extra >= 0 ? (i == 0 ? extra : r0 + i - 1) : r0 + i; }
+};
+
+inline RowSet rows_below(int k, int nblk, int band) {
+  if (k >= band) return RowSet{-1, k + 1, nblk};
+  return RowSet{k + 1 < band ? k + 1 : -1, band, nblk};
 }
 
-// A_ij -= L_ik L_jk^T for k < j <= i (diagonal blocks: lower tiles only).
-__global__ __launch_bounds__(64) void k_dchol_update(DenseView v, int k, int total) {
+__global__ __launch_bounds__(64) void k_dchol_update_tiles(DenseView v, int k, RowSet rs, int total) {
   const int lb = xcd_block(total);
   if (lb >= total) return;
   constexpr int nb = kCRMaxN, nt = nb / 16;
-  // block pair (bi, bj), bi >= bj > k, row-major over the lower block triangle; 49 tiles each
+  // block pair (bi, bj), bi >= bj, row-major over the lower triangle of rs; 49 tiles each
   const int pair = lb / (nt * nt), t = lb % (nt * nt);
   int ii = 0, rem = pair;
   while (rem > ii) { rem -= ii + 1; ++ii; }
-  const int bi = k + 1 + ii, bj = k + 1 + rem, ti = t / nt, tj = t % nt;
+  const int bi = rs.at(ii), bj = rs.at(rem), ti = t / nt, tj = t % nt;
   if (bi == bj && tj > ti) return;
   const double *X = v.L + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb;
   const double *Y = v.L + (size_t)(bj * nb + 16 * tj) * v.n + (size_t)k * nb;
@@ -739,6 +757,28 @@ __global__ __launch_bounds__(64) void k_dchol_update(DenseView v, int k, int tot
   for (int j = 0; j < 4; ++j) o[(size_t)(k4 + 4 * j) * v.n + r16] -= acc[j];
 }
 
+// L_ik = A_ik Linv_kk^T for the block rows i of rs; one wavefront per 16x16 tile.
+__global__ __launch_bounds__(64) void k_dchol_panel(DenseView v, int k, RowSet rs, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  constexpr int nb = kCRMaxN, nt = nb / 16;
+  const int bi = rs.at(lb / (nt * nt)), t = lb % (nt * nt), ti = t / nt, tj = t % nt;
+  const double *X = v.A + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb;
+  const double *Y = v.Linv + (size_t)k * nb * nb + (size_t)(16 * tj) * nb;  // Linv rows 16 tj..: lower, K <= 16 (tj+1)
+  const d4 acc = tile_xyt(X, v.n, Y, nb, 16 * (tj + 1));
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  double *o = v.L + (size_t)(bi * nb + 16 * ti) * v.n + (size_t)k * nb + 16 * tj;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[(size_t)(k4 + 4 * j) * v.n + r16] = acc[j];
+}
+
+// A_ij -= L_ik L_jk^T for k < j <= i (diagonal blocks: lower tiles only).
+// The same update with one wavefront per 16x16 tile and operands straight
+// from L2 / HBM: more parallelism per pair, used when there are few pairs (the
+// block-arrow band steps), where one workgroup per pair is latency-bound.
+struct RowSet;
+__global__ __launch_bounds__(64) void k_dchol_update_tiles(DenseView v, int k, RowSet rs, int total);
+
 // A_ij -= L_ik L_jk^T for one 112x112 block pair (bi, bj), bi >= bj > k, per
 // workgroup of 8 waves: the two 112 x 16 K-slices of L are staged in LDS (16-
 // byte loads, double-buffered), waves 0..6 each accumulate one row of 16x16
@@ -747,7 +787,7 @@ __global__ __launch_bounds__(64) void k_dchol_update(DenseView v, int k, int tot
 // update runs on the matrix cores instead of the L2 (the one-wave-per-tile
 // k_dchol_update re-reads both 16 x 112 slices for every tile).
 constexpr int kUpdKC = 16, kUpdLd = kUpdKC + 2;  // row stride: 16-byte aligned, spreads the 16 rows over banks
-__global__ __launch_bounds__(512) void k_dchol_update_blk(DenseView v, int k, int npairs) {
+__global__ __launch_bounds__(512) void k_dchol_update_blk(DenseView v, int k, RowSet rs, int npairs) {
   constexpr int nb = kCRMaxN, nt = nb / 16, nkc = nb / kUpdKC;
   __shared__ __attribute__((aligned(16))) double Xs[2][nb * kUpdLd];
   __shared__ __attribute__((aligned(16))) double Ys[2][nb * kUpdLd];
@@ -755,7 +795,7 @@ __global__ __launch_bounds__(512) void k_dchol_update_blk(DenseView v, int k, in
   if (lb >= npairs) return;
   int ii = 0, rem = lb;
   while (rem > ii) { rem -= ii + 1; ++ii; }
-  const int bi = k + 1 + ii, bj = k + 1 + rem;
+  const int bi = rs.at(ii), bj = rs.at(rem);
   const bool diag = bi == bj;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r16 = lane & 15, k4 = lane >> 4;
   const double *X = v.L + (size_t)bi * nb * v.n + (size_t)k * nb;
@@ -830,11 +870,12 @@ __global__ __launch_bounds__(512) void k_dtrsv_fwd_diag(DenseView v, int k) {
   if (t < nb) v.x[(size_t)k * nb + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
 }
 
-// one wavefront per row below block k: r_i -= L_i,k-block . y_k
-__global__ __launch_bounds__(256) void k_dtrsv_fwd_update(DenseView v, int k) {
+// one wavefront per row of the block rows rs below block k: r_i -= L_i,k-block . y_k
+__global__ __launch_bounds__(256) void k_dtrsv_fwd_update(DenseView v, int k, RowSet rs) {
   constexpr int nb = kCRMaxN;
-  const int row = (k + 1) * nb + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= v.n) return;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (q >= rs.count() * nb) return;
+  const int row = rs.at(q / nb) * nb + q % nb;
   const double *Lr = v.L + (size_t)row * v.n + (size_t)k * nb, *y = v.x + (size_t)k * nb;
   double s = 0.0;
   for (int m = lane; m < nb; m += 64) s += Lr[m] * y[m];
@@ -863,9 +904,10 @@ __global__ __launch_bounds__(512) void k_dtrsv_bwd_diag(DenseView v, int k) {
   if (t < nb) v.x[(size_t)k * nb + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
 }
 
-__global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k) {
+// columns [c0 nb, k nb) left of block k whose L_kj can be nonzero
+__global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k, int c0) {
   constexpr int nb = kCRMaxN;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = c0 * nb + blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= k * nb) return;
   const double *Lk = v.L + (size_t)k * nb * v.n + c, *xk = v.x + (size_t)k * nb;
   double s[4] = {0.0, 0.0, 0.0, 0.0};
@@ -875,30 +917,38 @@ __global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k) {
 }
 
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
-                           hipStream_t st) {
+                           hipStream_t st, int band) {
   constexpr int nb = kCRMaxN, nt = nb / 16;
   if (n <= 0 || n % nb) return -1;
   const int nblk = n / nb;
+  band = std::max(0, std::min(band, nblk));
   DenseView v{n, nblk, A, L, Linv, r, x, flags};
   const size_t lds = cr_factor_lds(nb);
+  // factor + forward substitution in one sweep: block k's diagonal kernel also
+  // forms y_k = Linv_kk r_k, then the panel, the trailing update and
+  // r_i -= L_ik y_k for the rows below
   for (int k = 0; k < nblk; ++k) {
     hipLaunchKernelGGL(k_dchol_diag, dim3(1), dim3(512), lds, st, v, k);
-    const int m = nblk - 1 - k;
-    if (m == 0) break;
+    const RowSet rs = rows_below(k, nblk, band);
+    const int m = rs.count();
+    if (m == 0) continue;
     const int np = m * nt * nt, npairs = m * (m + 1) / 2;
-    hipLaunchKernelGGL(k_dchol_panel, dim3(xcd_grid(np)), dim3(64), 0, st, v, k, np);
-    hipLaunchKernelGGL(k_dchol_update_blk, dim3(xcd_grid(npairs)), dim3(512), 0, st, v, k, npairs);
-  }
-  for (int k = 0; k < nblk; ++k) {
-    hipLaunchKernelGGL(k_dtrsv_fwd_diag, dim3(1), dim3(512), 0, st, v, k);
-    const int rows = n - (k + 1) * nb;
-    if (rows > 0) hipLaunchKernelGGL(k_dtrsv_fwd_update, dim3((rows + 3) / 4), dim3(256), 0, st, v, k);
+    hipLaunchKernelGGL(k_dchol_panel, dim3(xcd_grid(np)), dim3(64), 0, st, v, k, rs, np);
+    if (npairs < 128)  // few pairs: one wave per tile keeps every CU busy
+      hipLaunchKernelGGL(k_dchol_update_tiles, dim3(xcd_grid(npairs * nt * nt)), dim3(64), 0, st, v, k, rs,
+                         npairs * nt * nt);
+    else
+      hipLaunchKernelGGL(k_dchol_update_blk, dim3(xcd_grid(npairs)), dim3(512), 0, st, v, k, rs, npairs);
+    hipLaunchKernelGGL(k_dtrsv_fwd_update, dim3((m * nb + 3) / 4), dim3(256), 0, st, v, k, rs);
   }
   // y (in x) becomes the right-hand side of the backward pass
   if (hipMemcpyAsync(r, x, sizeof(double) * n, hipMemcpyDeviceToDevice, st) != hipSuccess) return -2;
   for (int k = nblk - 1; k >= 0; --k) {
     hipLaunchKernelGGL(k_dtrsv_bwd_diag, dim3(1), dim3(512), 0, st, v, k);
-    if (k > 0) hipLaunchKernelGGL(k_dtrsv_bwd_update, dim3((k * nb + 255) / 256), dim3(256), 0, st, v, k);
+    // L_kj != 0: j = k - 1 for a band block, every j < k for a border block
+    const int c0 = k < band ? std::max(k - 1, 0) : 0;
+    if (k > c0)
+      hipLaunchKernelGGL(k_dtrsv_bwd_update, dim3(((k - c0) * nb + 255) / 256), dim3(256), 0, st, v, k, c0);
   }
   return 0;
 }
