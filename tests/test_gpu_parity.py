@@ -165,3 +165,21 @@ def test_dense_solve_path(gpu_ctx, oracle, n_kf, k_min, k_max):
     assert ng == nr
     _compare_stats(sg, sr)
     _compare_state(gpu_ctx, ref)
+
+
+def test_config4_full_size_two_iterations(gpu_ctx, oracle):
+    """BASELINE config 4 at full size (5k poses, 500k landmarks, 5M observations,
+    278 CR superblocks, 9 levels): two LM iterations match the oracle's —
+    same decisions, chi2 trace and estimates within 1e-6 (the oracle needs
+    ~3 s per iteration on one core, so two iterations keep the test short)."""
+    prob = synth.config4(seed=4)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.global_ba(2)
+    gpu_ctx.set_problem(prob)
+    ng, sg = gpu_ctx.global_ba(2)
+    assert ng == nr == 2
+    _compare_stats(sg, sr)
+    _compare_state(gpu_ctx, ref)
+    # size-independent properties of the full run: chi2 falls, every edge active
+    assert sg["trace_chi2"][1] < sg["trace_chi2"][0] < sg["chi2_begin"]
+    assert sg["n_active_edges"] == prob.n_obs
