@@ -8,10 +8,12 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <limits>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/sqrtlm.h"
@@ -244,6 +246,15 @@ inline bool stopped(const volatile uint8_t *s) { return s && *s; }
 // camera CSR and the upper block pattern of the reduced camera system.
 int prepare(sqlm_ctx *c, int level) {
   DevProblem &d = c->d;
+  // SQLM_PREP_TIMING=1: host phase times of this setup on stderr
+  const bool ptime = std::getenv("SQLM_PREP_TIMING") != nullptr;
+  auto pt0 = std::chrono::steady_clock::now();
+  auto phase = [&](const char *what) {
+    if (!ptime) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "prepare %-12s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - pt0).count());
+    pt0 = now;
+  };
   std::vector<uint8_t> pose_act(c->n_pose, 0), pt_act(c->n_pt, 0);
   std::vector<int> kcount(c->n_pt, 0);
   int64_t n_ae = 0;
@@ -282,15 +293,27 @@ int prepare(sqlm_ctx *c, int level) {
     span_lo[l] = std::min(span_lo[l], pp);
     span_hi[l] = std::max(span_hi[l], pp);
   }
-  for (int l = 0; l < c->n_pt; ++l)
-    if (pt_act[l]) pts.push_back(l);
-  std::stable_sort(pts.begin(), pts.end(), [&](int a, int b) {
-    const int wa = seg_width(kcount[a]), wb = seg_width(kcount[b]);
-    if (wa != wb) return wa < wb;
-    if (span_lo[a] != span_lo[b]) return span_lo[a] < span_lo[b];
-    return span_hi[a] < span_hi[b];
-  });
+  // (segment width, first pose) buckets by a counting sort, then last pose
+  // inside a bucket; ties keep id order (the order a stable sort would give)
+  {
+    auto wl = [](int k) { int w = seg_width(k), b = 0; while ((2 << b) < w) ++b; return b; };  // log2(W) - 1
+    const int64_t nb = 7 * (int64_t)c->n_pose + 1;
+    std::vector<int> bcnt(nb + 1, 0);
+    std::vector<int> key(c->n_pt, -1);
+    for (int l = 0; l < c->n_pt; ++l)
+      if (pt_act[l]) { key[l] = (int)(wl(kcount[l]) * (int64_t)c->n_pose + span_lo[l]); ++bcnt[key[l] + 1]; }
+    for (int64_t b = 0; b < nb; ++b) bcnt[b + 1] += bcnt[b];
+    pts.assign(bcnt[nb], 0);
+    std::vector<int> f(bcnt.begin(), bcnt.end() - 1);
+    for (int l = 0; l < c->n_pt; ++l)
+      if (key[l] >= 0) pts[f[key[l]]++] = l;
+    for (int64_t b = 0; b < nb; ++b)
+      if (bcnt[b + 1] - bcnt[b] > 1)
+        std::stable_sort(pts.begin() + bcnt[b], pts.begin() + bcnt[b + 1],
+                         [&](int a, int bb) { return span_hi[a] < span_hi[bb]; });
+  }
   const int nL = (int)pts.size();
+  phase("active+sort");
   if (nP + nL == 0) return SQLM_ERR_STATE;  // "0 vertices to optimize"
   std::vector<int> pt_slot(c->n_pt, -1);
   for (int s = 0; s < nL; ++s) pt_slot[pts[s]] = s;
@@ -343,24 +366,34 @@ int prepare(sqlm_ctx *c, int level) {
     for (int64_t o = 0; o < nE; ++o)
       if (obs_camh[o] >= 0) cam_obs[f[obs_camh[o]]++] = (int)o;
   }
+  phase("obs+camcsr");
   // reduced-camera-system pattern (upper, diagonal first)
   std::vector<int> s_row(nP + 1, 0), s_col;
   {
-    std::vector<int> mark(nP, -1), row;
     std::vector<std::vector<int>> rows(nP);
-    for (int i = 0; i < nP; ++i) {
-      row.clear();
-      row.push_back(i);
-      mark[i] = i;
-      for (int t = cam_ptr[i]; t < cam_ptr[i + 1]; ++t) {
-        const int s = obs_lm[cam_obs[t]];
-        for (int o = lm_begin[s]; o < lm_begin[s + 1]; ++o) {
-          const int j = obs_camh[o];
-          if (j > i && mark[j] != i) { mark[j] = i; row.push_back(j); }
+    {  // rows are independent: a few host threads, each with its own marks
+      const int nth = std::max(1, std::min(8, (int)std::thread::hardware_concurrency()));
+      auto work = [&](int t0) {
+        std::vector<int> mark(nP, -1), row;
+        for (int i = t0; i < nP; i += nth) {
+          row.clear();
+          row.push_back(i);
+          mark[i] = i;
+          for (int t = cam_ptr[i]; t < cam_ptr[i + 1]; ++t) {
+            const int s = obs_lm[cam_obs[t]];
+            for (int o = lm_begin[s]; o < lm_begin[s + 1]; ++o) {
+              const int j = obs_camh[o];
+              if (j > i && mark[j] != i) { mark[j] = i; row.push_back(j); }
+            }
+          }
+          std::sort(row.begin() + 1, row.end());
+          rows[i] = row;
         }
-      }
-      std::sort(row.begin() + 1, row.end());
-      rows[i] = row;
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < nth; ++t) th.emplace_back(work, t);
+      work(0);
+      for (auto &t : th) t.join();
     }
     if (sharded) {
       // a common pattern for the S all-reduce: the band of the widest shard
@@ -400,7 +433,9 @@ int prepare(sqlm_ctx *c, int level) {
   // tiles still cover every CU twice (a local-BA window of 5k landmarks would
   // otherwise run ~40 long tiles on 256 CUs)
   const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
+  phase("S pattern");
   build_tiles(nP, nL, lm_begin, obs_camh, s_row, s_col, lm_cap, tp);
+  phase("tiles");
   c->use_tiles = nP > 0 && tp.max_cp <= kTileHardCams;
   c->tile_max_cp = tp.max_cp;
   c->tile_max_k = 0;
@@ -426,6 +461,7 @@ int prepare(sqlm_ctx *c, int level) {
       }
     }
   }
+  phase("lidar");
   // ---------------- upload ----------------
   d.n_pose = c->n_pose;
   d.sharded = c->comm.enabled() ? 1 : 0;
@@ -505,33 +541,20 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_OBSERR, 2 * (size_t)nE, d.obs_err);
   UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
   UP(B_CAMOBS, cam_obs, d.cam_obs);
-  {  // camera-ordered copies of the camera pass inputs (one coalesced stream + the X gather)
-    std::vector<int> cslot(cam_obs.size());
-    std::vector<double> cuv(4 * cam_obs.size());
-    for (size_t t = 0; t < cam_obs.size(); ++t) {
-      const int o = cam_obs[t];
-      cslot[t] = obs_lm[o];
-      cuv[4 * t] = obs_uv[2 * o];
-      cuv[4 * t + 1] = obs_uv[2 * o + 1];
-      cuv[4 * t + 2] = obs_info[o];
-      cuv[4 * t + 3] = obs_delta[o];
-    }
-    UP(B_CAMSLOT, cslot, d.cam_slot);
-    UP(B_CAMUV, cuv, d.cam_uv);
-    if (c->has_stereo) {
-      std::vector<double> cur(cam_obs.size());
-      for (size_t t = 0; t < cam_obs.size(); ++t) cur[t] = obs_ur[cam_obs[t]];
-      UP(B_CAMUR, cur, d.cam_ur);
-    }
-  }
   d.has_stereo = c->has_stereo ? 1 : 0;
   if (c->has_stereo) {
     UP(B_OBSUR, obs_ur, d.obs_ur);
     UP(B_POSEBF, c->pose_bf, d.pose_bf);
     AL(B_OBSERR3, (size_t)nE, d.obs_err3);
+    AL(B_CAMUR, cam_obs.size(), d.cam_ur);
   } else {
     d.obs_ur = d.obs_err3 = d.pose_bf = d.cam_ur = nullptr;
   }
+  // camera-ordered copies of the camera pass inputs (one coalesced stream +
+  // the X gather), gathered on the device from the slot-ordered arrays
+  AL(B_CAMSLOT, cam_obs.size(), d.cam_slot);
+  AL(B_CAMUV, 4 * cam_obs.size(), d.cam_uv);
+  launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
   UP(B_LIDPTR, lid_ptr, d.lid_cam_ptr);
@@ -616,6 +639,7 @@ int prepare(sqlm_ctx *c, int level) {
   HIP_OK(hipMemsetAsync(d.obs_err, 0, sizeof(double) * 2 * std::max<int64_t>(nE, 1), c->stream));
   if (d.obs_err3) HIP_OK(hipMemsetAsync(d.obs_err3, 0, sizeof(double) * std::max<int64_t>(nE, 1), c->stream));
   launch_pose_prep(d, 0, c->stream);
+  phase("upload");
   return SQLM_OK;
 }
 

@@ -144,6 +144,7 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
 void launch_camera_pass(const DevProblem &d, hipStream_t st);
 void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
 void launch_pose_diag(const DevProblem &d, hipStream_t st);
+void launch_cam_gather(const DevProblem &d, int64_t n_cam_obs, hipStream_t st);
 // rank 0 of a sharded run: destination / source ranges of the gathered rows
 constexpr int kMaxRanks = 16;
 struct GatherTab {

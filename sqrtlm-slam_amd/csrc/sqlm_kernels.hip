@@ -517,6 +517,25 @@ __global__ __launch_bounds__(256) void k_pose_maxdiag(DevProblem d) {
   if (threadIdx.x == 0) atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
 }
 
+// setup: camera-ordered copies of the camera pass inputs, gathered from the
+// slot-ordered observation arrays (saves uploading them a second time)
+__global__ __launch_bounds__(256) void k_cam_gather(DevProblem d, int64_t n) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int o = d.cam_obs[t];
+  d.cam_slot[t] = d.obs_lm[o];
+  double *u = d.cam_uv + 4 * t;
+  u[0] = d.obs_uv[2 * (int64_t)o];
+  u[1] = d.obs_uv[2 * (int64_t)o + 1];
+  u[2] = d.obs_info[o];
+  u[3] = d.obs_delta[o];
+  if (d.cam_ur) d.cam_ur[t] = d.obs_ur[o];
+}
+
+void launch_cam_gather(const DevProblem &d, int64_t n, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_cam_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, d, n);
+}
+
 void launch_pose_diag(const DevProblem &d, hipStream_t st) {
   if (d.nP == 0) return;
   hipLaunchKernelGGL(k_pose_diag, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d);
