@@ -93,6 +93,19 @@ struct sqlm_ctx {
   // (independent inputs and outputs); fork / join through two events
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // speculative linearization: every trial's k_landmark_update also linearizes
+  // at the trial state (into the *_nx buffers) and the camera pass for that
+  // state runs on the side stream; an accepted trial swaps them in, so the next
+  // iteration starts without a linearization pass (g2o linearizes at exactly
+  // that state: same device code, same bits). SQLM_NO_SPEC=1 turns it off.
+  bool spec = false;
+  bool lin_valid = false;          // the current buffers hold the linearization at the current state
+  bool spec_outstanding = false;   // a speculative camera pass may still run on the side stream
+  hipEvent_t ev_spec_fork = nullptr, ev_spec_join = nullptr;
+  hipEvent_t ev_cam[2][2] = {};    // timing of the speculative camera passes (ping-pong)
+  bool cam_pending[2] = {false, false};
+  int cam_par = 0;
+  int lin_timers = 2;               // timers the last linearize() recorded
   bool timing = false;
   double kernel_ms_acc[SQLM_NKERNEL_TIMERS] = {};
   int kernel_ms_n = 0;
@@ -136,7 +149,8 @@ enum BufId {
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
-  B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX
+  B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
+  B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -557,6 +571,24 @@ int prepare(sqlm_ctx *c, int level) {
   launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
+  {
+    const bool no_spec = getenv("SQLM_NO_SPEC") && atoi(getenv("SQLM_NO_SPEC")) != 0;
+    c->spec = c->use_tiles && d.obs_P == nullptr && !no_spec;
+  }
+  c->lin_valid = false;
+  d.pc_lm = kPartChiCurLm;
+  d.pc_lid = kPartChiCurLid;
+  d.px_lm = kPartChiCurLm2;
+  d.px_lid = kPartChiCurLid2;
+  if (c->spec) {
+    AL(B_LMR_NX, 8 * (size_t)nL, d.lm_R_nx);
+    AL(B_LMB_NX, 4 * (size_t)nL, d.lm_b_nx);
+    AL(B_OBSS_NX, (size_t)nE, d.obs_s_nx);
+    AL(B_HPP_NX, 36 * (size_t)nP, d.Hpp_nx);
+    AL(B_BP_NX, 8 * (size_t)nP, d.bp_nx);
+  } else {
+    d.lm_R_nx = d.lm_b_nx = d.obs_s_nx = d.Hpp_nx = d.bp_nx = nullptr;
+  }
   UP(B_LIDPTR, lid_ptr, d.lid_cam_ptr);
   UP(B_LIDDATA, lid_data, d.lid_data);
   UP(B_LIDPOSE, lid_pose, d.lid_pose);
@@ -684,6 +716,13 @@ void acc_events(sqlm_ctx *c, int i0, int i1) {
 // computeActiveErrors + buildSystem for the current state.
 int linearize(sqlm_ctx *c) {
   DevProblem &d = c->d;
+  c->lin_timers = 1;
+  if (c->spec && c->lin_valid) {  // the accepted trial already linearized at this state
+    tmark(c, 0, false);
+    tmark(c, 0, true);
+    return SQLM_OK;
+  }
+  c->lin_timers = 2;  // + the camera pass on the side stream
   // the camera pass (H_pp, b_p, LiDAR) reads only the state, like the landmark
   // QR: fork it onto the side stream and join before anything consumes H_pp
   HIP_OK(hipEventRecord(c->ev_fork, c->stream));
@@ -736,6 +775,10 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   else launch_rcs(d, lambda, c->max_row_blocks, c->stream);
   tmark(c, 3, true);
   tmark(c, 8, false);
+  if (c->spec_outstanding) {  // H_pp / b_p (if swapped in) and the trial state buffers it reads
+    HIP_OK(hipStreamWaitEvent(c->stream, c->ev_spec_join, 0));
+    c->spec_outstanding = false;
+  }
   if (c->use_tiles) {
     if (d.cr_direct) {  // the reduce assembles the CR superblocks itself
       const size_t blkbytes = (size_t)c->cr.p * c->cr.n * c->cr.n * sizeof(double);
@@ -780,9 +823,27 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   tmark(c, 5, true);
   tmark(c, 6, false);
   for (size_t b = 0; b < c->buckets.size(); ++b)
-    launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream);
+    launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream, c->spec);
   launch_lidar_chi2(d, c->stream);
   tmark(c, 6, true);
+  if (c->spec) {  // camera pass at the trial state, overlapped with the host's decision and the next trial
+    HIP_OK(hipEventRecord(c->ev_spec_fork, c->stream));
+    HIP_OK(hipStreamWaitEvent(c->side, c->ev_spec_fork, 0));
+    const int p = c->cam_par;
+    if (c->timing && c->cam_pending[p]) {  // the pass two trials back is long complete
+      float ms = 0.f;
+      if (hipEventSynchronize(c->ev_cam[p][1]) == hipSuccess &&
+          hipEventElapsedTime(&ms, c->ev_cam[p][0], c->ev_cam[p][1]) == hipSuccess)
+        c->kernel_ms_acc[1] += ms;
+      c->cam_pending[p] = false;
+    }
+    if (c->timing) HIP_OK(hipEventRecord(c->ev_cam[p][0], c->side));
+    launch_camera_pass(d, c->side, true);
+    if (c->timing) { HIP_OK(hipEventRecord(c->ev_cam[p][1], c->side)); c->cam_pending[p] = true; }
+    c->cam_par ^= 1;
+    HIP_OK(hipEventRecord(c->ev_spec_join, c->side));
+    c->spec_outstanding = true;
+  }
   tmark(c, 7, false);
   s = reduce_and_fetch(c, o);
   tmark(c, 7, true);
@@ -791,9 +852,32 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
 }
 
 void swap_state(sqlm_ctx *c) {
-  std::swap(c->d.pose_qt[0], c->d.pose_qt[1]);
-  std::swap(c->d.pose_rt[0], c->d.pose_rt[1]);
-  std::swap(c->d.X[0], c->d.X[1]);
+  DevProblem &d = c->d;
+  std::swap(d.pose_qt[0], d.pose_qt[1]);
+  std::swap(d.pose_rt[0], d.pose_rt[1]);
+  std::swap(d.X[0], d.X[1]);
+  c->lin_valid = c->spec;
+  if (c->spec) {  // the speculative linearization at the accepted state becomes current
+    std::swap(d.lm_R, d.lm_R_nx);
+    std::swap(d.lm_b, d.lm_b_nx);
+    std::swap(d.obs_s, d.obs_s_nx);
+    std::swap(d.Hpp, d.Hpp_nx);
+    std::swap(d.bp, d.bp_nx);
+    std::swap(d.pc_lm, d.px_lm);
+    std::swap(d.pc_lid, d.px_lid);
+  }
+}
+
+// Timing of speculative camera passes not yet added (end of an LM run).
+void flush_cam_timers(sqlm_ctx *c) {
+  for (int p = 0; p < 2; ++p) {
+    if (!c->cam_pending[p]) continue;
+    float ms = 0.f;
+    if (hipEventSynchronize(c->ev_cam[p][1]) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev_cam[p][0], c->ev_cam[p][1]) == hipSuccess)
+      c->kernel_ms_acc[1] += ms;
+    c->cam_pending[p] = false;
+  }
 }
 
 // The Levenberg–Marquardt loop of g2o (levenberg.cpp:61-164 inside
@@ -807,6 +891,7 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
   st->n_active_edges = c->n_active_edges;
   double lambda = -1., ni = 2.;
   int nbad = 0, its = 0, result = 0;
+  c->lin_valid = false;  // iteration 0 linearizes in full (lambda_0 needs max diag H)
   Timer tt;
   for (int it = 0; it < iterations && !stopped(stop) && (result == 0 || bench); ++it) {
     Timer tl;
@@ -834,7 +919,7 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
       s = trial(c, lambda, o);
       if (s) return s;
       if (qmax == 0 && it > 0) { currentChi = o.chi_cur; iniChi = currentChi; }
-      if (qmax == 0) acc_events(c, 0, 2);
+      if (qmax == 0) acc_events(c, 0, c->lin_timers);
       tempChi = o.chi_new;
       if (!o.ok) tempChi = std::numeric_limits<double>::max();
       rho = (currentChi - tempChi);
@@ -874,6 +959,11 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
     st->lambda_end = lambda;
     ++its;
   }
+  if (c->spec_outstanding) {  // nothing of a speculative pass outlives the run
+    HIP_OK(hipStreamWaitEvent(c->stream, c->ev_spec_join, 0));
+    c->spec_outstanding = false;
+  }
+  flush_cam_timers(c);
   st->iterations = its;
   st->result = result;
   st->ms_total = tt.ms();
@@ -971,9 +1061,13 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   // timing-only events: no system-scope fence, which would flush caches and
   // leave a ~10 us bubble between the kernels they separate
   for (auto &e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  for (auto &pr : c->ev_cam)
+    for (auto &e : pr) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_spec_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_spec_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
     sqlm_ctx_destroy(c);
     return SQLM_ERR_HIP;
   }
@@ -995,6 +1089,11 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->ev_spec_fork) (void)hipEventDestroy(c->ev_spec_fork);
+  if (c->ev_spec_join) (void)hipEventDestroy(c->ev_spec_join);
+  for (auto &pr : c->ev_cam)
+    for (auto &e : pr)
+      if (e) (void)hipEventDestroy(e);
   if (c->side) (void)hipStreamDestroy(c->side);
   (void)hipStreamDestroy(c->stream);
   delete c;

@@ -29,6 +29,9 @@ struct DevProblem {
   int *lm_begin = nullptr;                  // [nL+1]
   double *lm_R = nullptr;                   // [nL][8]  R upper (6) of QR(J_l)
   double *lm_b = nullptr;                   // [nL][4]  b_l = -J_l^T W r
+  // speculative linearization at the trial state (k_landmark_update<SPEC>),
+  // swapped with lm_R / lm_b / obs_s / Hpp / bp when the trial is accepted
+  double *lm_R_nx = nullptr, *lm_b_nx = nullptr, *obs_s_nx = nullptr, *Hpp_nx = nullptr, *bp_nx = nullptr;
   double *lm_M = nullptr;                   // [nL][8]  (H_ll + lambda I)^-1, sym (6)
   double *lm_v = nullptr;                   // [nL][4]  M b_l
   double *lm_Rp = nullptr;                  // [nL][12] R'^-1 of the damped factor (6), w = R'^-T b_l (3)
@@ -104,6 +107,8 @@ struct DevProblem {
   int cr_B = 0, cr_n = 0, cr_p = 0;
   // reductions
   double *partials = nullptr;               // [kMaxPartials]
+  int pc_lm = 0, pc_lid = 0;                // chi2 partial regions of the current linearization
+  int px_lm = 0, px_lid = 0;                //   ... and of the speculative one (swapped on accept)
   double *scalars = nullptr;                // [8] see Scalar
   unsigned long long *maxdiag = nullptr;    // bit pattern of a non-negative double
   int *flags = nullptr;                     // [4] solve_ok ...
@@ -119,7 +124,9 @@ enum PartialRegion {
   kPartChiNewLid = 163840,   // lidar chi2 at trial state blocks (<= 16384)
   kPartScaleCam = 180224,    // pose part of computeScale blocks (<= 16384)
   kPartScaleLm = 196608,     // landmark part                   (<= 16384)
-  kPartEnd = 212992
+  kPartChiCurLm2 = 212992,   // second chi-cur landmark region (speculative linearization)
+  kPartChiCurLid2 = 229376,  // second chi-cur camera region
+  kPartEnd = 360448
 };
 constexpr int kMaxPartials = kPartEnd;
 constexpr int kMaxFreePoses = 131072;
@@ -141,7 +148,7 @@ struct Bucket {
 // kernel launchers (sqlm_kernels.hip). All asynchronous on `st`.
 void launch_pose_prep(const DevProblem &d, int buf, hipStream_t st);
 void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStream_t st);
-void launch_camera_pass(const DevProblem &d, hipStream_t st);
+void launch_camera_pass(const DevProblem &d, hipStream_t st, bool spec = false);
 void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
 void launch_pose_diag(const DevProblem &d, hipStream_t st);
 void launch_cam_gather(const DevProblem &d, int64_t n_cam_obs, hipStream_t st);
@@ -176,8 +183,8 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
                            hipStream_t st, int band = 0);
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
-void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off,
-                            hipStream_t st);
+void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st,
+                            bool spec = false);
 void launch_lidar_chi2(const DevProblem &d, hipStream_t st);
 void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts,
                    int n_lid_parts, hipStream_t st);

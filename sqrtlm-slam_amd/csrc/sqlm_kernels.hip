@@ -246,6 +246,31 @@ __device__ __forceinline__ void store2(double *p, double a, double b) {
   *reinterpret_cast<double2 *>(p) = make_double2(a, b);
 }
 
+// The per-observation inputs of one edge, loaded up front: every lane of a
+// segment owns at most two observations (W >= k / 2, seg_width), so both are
+// requested before any of them is used and their latencies overlap.
+struct ObsIn {
+  int cam, camh;
+  double u, v, info, delta, ur, s;
+};
+
+template <bool ST, bool WANT_S>
+__device__ __forceinline__ ObsIn load_obs(const DevProblem &d, int e, bool ok) {
+  ObsIn o{0, -1, 0.0, 0.0, 0.0, 0.0, -1.0, 0.0};
+  if (ok) {
+    o.cam = d.obs_cam[e];
+    o.camh = d.obs_camh[e];
+    const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
+    o.u = uv.x;
+    o.v = uv.y;
+    o.info = d.obs_info[e];
+    o.delta = d.obs_delta[e];
+    if (ST) o.ur = d.obs_ur[e];
+    if (WANT_S) o.s = d.obs_s[e];
+  }
+  return o;
+}
+
 // ---------------------------------------------------------------- pose prep
 
 __global__ void k_pose_prep(const double *__restrict__ qt, const double *__restrict__ intr,
@@ -266,6 +291,80 @@ void launch_pose_prep(const DevProblem &d, int buf, hipStream_t st) {
   if (d.n_pose == 0) return;
   hipLaunchKernelGGL(k_pose_prep, dim3((d.n_pose + 255) / 256), dim3(256), 0, st, d.pose_qt[buf], d.intr,
                      d.pose_rt[buf], d.n_pose);
+}
+
+// One edge of the landmark linearization at the state (prt_all, X): residual
+// and robust weight (to obs_err / s_out), the weighted Jacobian rows folded into
+// the landmark's R by Givens rotations, b_l, the Hessian diagonal g, chi2.
+// k_linearize and the speculative pass of k_landmark_update call it in the same
+// order, so both produce the same bits.
+template <bool ST>
+__device__ __forceinline__ void lin_edge(const DevProblem &d, const ObsIn &o, int e, const double *prt_all, double X0,
+                                         double X1, double X2, double *s_out, bool want_P, double R[6], double &b0,
+                                         double &b1, double &b2, double &g0, double &g1, double &g2, double &chi) {
+  const int cam = o.cam;
+  const double *prt = prt_all + 16 * cam;
+  MonoEval m;
+  const double bf = ST ? d.pose_bf[cam] : 0.0;
+  const bool st = ST && o.ur >= 0.0;
+  if (st) stereo_error(prt, X0, X1, X2, o.u, o.v, o.ur, bf, o.info, o.delta, m);
+  else mono_error(prt, X0, X1, X2, o.u, o.v, o.info, o.delta, m);
+  store2(d.obs_err + 2 * e, m.e0, m.e1);
+  if (ST) d.obs_err3[e] = st ? m.e2 : 0.0;
+  s_out[e] = m.s;
+  chi += m.chi_rob;
+  double jl[6], jp[12], jl3[3] = {0, 0, 0}, jp3[6] = {0, 0, 0, 0, 0, 0};
+  mono_jac(prt, m, jl, jp);
+  const double r0 = m.s * m.e0, r1 = m.s * m.e1;
+  b0 -= jl[0] * r0 + jl[3] * r1;
+  b1 -= jl[1] * r0 + jl[4] * r1;
+  b2 -= jl[2] * r0 + jl[5] * r1;
+  g0 += jl[0] * jl[0] + jl[3] * jl[3];
+  g1 += jl[1] * jl[1] + jl[4] * jl[4];
+  g2 += jl[2] * jl[2] + jl[5] * jl[5];
+  givens_add_row(R, jl[0], jl[1], jl[2]);
+  givens_add_row(R, jl[3], jl[4], jl[5]);
+  if (st) {
+    stereo_row(prt, m, bf, jl, jp, jl3, jp3);
+    const double r2 = m.s * m.e2;
+    b0 -= jl3[0] * r2; b1 -= jl3[1] * r2; b2 -= jl3[2] * r2;
+    g0 += jl3[0] * jl3[0]; g1 += jl3[1] * jl3[1]; g2 += jl3[2] * jl3[2];
+    givens_add_row(R, jl3[0], jl3[1], jl3[2]);
+  }
+  if (want_P && d.obs_P && o.camh >= 0) {
+    // row-kernel fallback only: H_lp block jl^T jp (3x6), SoA, entry (a,c) at P[(6a+c) nE + e]
+    double *P = d.obs_P + e;
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        P[(6 * a + c) * d.nE] = jl[a] * jp[c] + jl[3 + a] * jp[6 + c] + (st ? jl3[a] * jp3[c] : 0.0);
+  }
+}
+
+// TSQR butterfly inside a W-lane segment (canonical: the lower lane's R absorbs
+// the upper's rows), with the sums of b, g and chi2.
+template <int W>
+__device__ __forceinline__ void lin_butterfly(int lane, double R[6], double &b0, double &b1, double &b2, double &g0,
+                                              double &g1, double &g2, double &chi) {
+#pragma unroll
+  for (int off = 1; off < W; off <<= 1) {
+    double o[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) o[i] = __shfl_xor(R[i], off, 64);
+    const bool lo = (lane & off) == 0;
+    double A[6], B[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { A[i] = lo ? R[i] : o[i]; B[i] = lo ? o[i] : R[i]; }
+    givens_add_row(A, B[0], B[1], B[2]);
+    givens_add_row(A, 0.0, B[3], B[4]);
+    givens_add_row(A, 0.0, 0.0, B[5]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) R[i] = A[i];
+    b0 += __shfl_xor(b0, off, 64); b1 += __shfl_xor(b1, off, 64); b2 += __shfl_xor(b2, off, 64);
+    g0 += __shfl_xor(g0, off, 64); g1 += __shfl_xor(g1, off, 64); g2 += __shfl_xor(g2, off, 64);
+    chi += __shfl_xor(chi, off, 64);
+  }
 }
 
 // ---------------------------------------------------------------- linearize
@@ -302,68 +401,15 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
     if (valid) {
       const double X0 = d.X[0][4 * slot], X1 = d.X[0][4 * slot + 1], X2 = d.X[0][4 * slot + 2];
       const int beg = d.lm_begin[slot], end = d.lm_begin[slot + 1];
-      for (int e = beg + lane; e < end; e += W) {
-        const int cam = d.obs_cam[e];
-        const double *prt = prt_all + 16 * cam;
-        const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
-        MonoEval m;
-        double ur = -1.0, bf = 0.0;
-        if (ST) { ur = d.obs_ur[e]; bf = d.pose_bf[cam]; }
-        const bool st = ST && ur >= 0.0;
-        if (st) stereo_error(prt, X0, X1, X2, uv.x, uv.y, ur, bf, d.obs_info[e], d.obs_delta[e], m);
-        else mono_error(prt, X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
-        store2(d.obs_err + 2 * e, m.e0, m.e1);
-        if (ST) d.obs_err3[e] = st ? m.e2 : 0.0;
-        d.obs_s[e] = m.s;
-        chi += m.chi_rob;
-        double jl[6], jp[12], jl3[3] = {0, 0, 0}, jp3[6] = {0, 0, 0, 0, 0, 0};
-        mono_jac(prt, m, jl, jp);
-        const double r0 = m.s * m.e0, r1 = m.s * m.e1;
-        b0 -= jl[0] * r0 + jl[3] * r1;
-        b1 -= jl[1] * r0 + jl[4] * r1;
-        b2 -= jl[2] * r0 + jl[5] * r1;
-        g0 += jl[0] * jl[0] + jl[3] * jl[3];
-        g1 += jl[1] * jl[1] + jl[4] * jl[4];
-        g2 += jl[2] * jl[2] + jl[5] * jl[5];
-        givens_add_row(R, jl[0], jl[1], jl[2]);
-        givens_add_row(R, jl[3], jl[4], jl[5]);
-        if (st) {
-          stereo_row(prt, m, bf, jl, jp, jl3, jp3);
-          const double r2 = m.s * m.e2;
-          b0 -= jl3[0] * r2; b1 -= jl3[1] * r2; b2 -= jl3[2] * r2;
-          g0 += jl3[0] * jl3[0]; g1 += jl3[1] * jl3[1]; g2 += jl3[2] * jl3[2];
-          givens_add_row(R, jl3[0], jl3[1], jl3[2]);
-        }
-        if (d.obs_P && d.obs_camh[e] >= 0) {
-          // row-kernel fallback only: H_lp block jl^T jp (3x6), SoA, entry (a,c) at P[(6a+c) nE + e]
-          double *P = d.obs_P + e;
-#pragma unroll
-          for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int c = 0; c < 6; ++c)
-              P[(6 * a + c) * d.nE] = jl[a] * jp[c] + jl[3 + a] * jp[6 + c] + (st ? jl3[a] * jp3[c] : 0.0);
-        }
-      }
+      const int ea = beg + lane, eb = ea + W;
+      const ObsIn oa = load_obs<ST, false>(d, ea, ea < end), ob = load_obs<ST, false>(d, eb, eb < end);
+      if (ea < end) lin_edge<ST>(d, oa, ea, prt_all, X0, X1, X2, d.obs_s, true, R, b0, b1, b2, g0, g1, g2, chi);
+      if (eb < end) lin_edge<ST>(d, ob, eb, prt_all, X0, X1, X2, d.obs_s, true, R, b0, b1, b2, g0, g1, g2, chi);
+      for (int e = eb + W; e < end; e += W)  // tracks > 128 only
+        lin_edge<ST>(d, load_obs<ST, false>(d, e, true), e, prt_all, X0, X1, X2, d.obs_s, true, R, b0, b1, b2, g0, g1,
+                     g2, chi);
     }
-    // TSQR butterfly inside the segment (canonical: lower lane's R absorbs the upper's rows)
-#pragma unroll
-    for (int off = 1; off < W; off <<= 1) {
-      double o[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) o[i] = __shfl_xor(R[i], off, 64);
-      const bool lo = (lane & off) == 0;
-      double A[6], B[6];
-#pragma unroll
-      for (int i = 0; i < 6; ++i) { A[i] = lo ? R[i] : o[i]; B[i] = lo ? o[i] : R[i]; }
-      givens_add_row(A, B[0], B[1], B[2]);
-      givens_add_row(A, 0.0, B[3], B[4]);
-      givens_add_row(A, 0.0, 0.0, B[5]);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) R[i] = A[i];
-      b0 += __shfl_xor(b0, off, 64); b1 += __shfl_xor(b1, off, 64); b2 += __shfl_xor(b2, off, 64);
-      g0 += __shfl_xor(g0, off, 64); g1 += __shfl_xor(g1, off, 64); g2 += __shfl_xor(g2, off, 64);
-      chi += __shfl_xor(chi, off, 64);
-    }
+    lin_butterfly<W>(lane, R, b0, b1, b2, g0, g1, g2, chi);
     if (valid && lane == 0) {
       double *Ro = d.lm_R + 8 * slot;
       store2(Ro, R[0], R[1]); store2(Ro + 2, R[2], R[3]); store2(Ro + 4, R[4], R[5]);
@@ -376,7 +422,7 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
   const double s = block_sum(chi_acc, red);
   const double mx = block_max(dmax, red);
   if (threadIdx.x == 0) {
-    d.partials[kPartChiCurLm + part_off + blockIdx.x] = s;
+    d.partials[d.pc_lm + part_off + blockIdx.x] = s;
     atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
   }
 }
@@ -406,9 +452,12 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
 // weighted pose Jacobian recomputed from the inputs (the same device code as
 // k_linearize, so bit-identical), plus the camera's LiDAR unary edges
 // (numeric Jacobian, base_unary_edge.hpp:82-122).
+// spec: the speculative pass at the trial state (pose / landmark buffers 1)
+// into Hpp_nx / bp_nx, launched after k_landmark_update<SPEC>.
 template <bool ST>
-__global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
+__global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int sb = spec ? 1 : 0;
   const int i = blockIdx.x * 4 + wave;
   double H[21], b[6], chi = 0.0;
 #pragma unroll
@@ -416,10 +465,10 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
 #pragma unroll
   for (int k = 0; k < 6; ++k) b[k] = 0.0;
   if (i < d.nP) {
-    const double *prt = d.pose_rt[0] + 16 * d.hidx_pose[i];
+    const double *prt = d.pose_rt[sb] + 16 * d.hidx_pose[i];
     const double bf = ST ? d.pose_bf[d.hidx_pose[i]] : 0.0;
     for (int t = d.cam_obs_ptr[i] + lane; t < d.cam_obs_ptr[i + 1]; t += 64) {
-      const double *X = d.X[0] + 4 * d.cam_slot[t];
+      const double *X = d.X[sb] + 4 * d.cam_slot[t];
       const double2 uv = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t);
       const double2 id = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t + 2);
       const double ur = ST ? d.cam_ur[t] : -1.0;
@@ -453,7 +502,7 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
     }
     if (d.nLid > 0) {
       const int p = d.hidx_pose[i];
-      const double *qt = d.pose_qt[0] + 8 * p;
+      const double *qt = d.pose_qt[sb] + 8 * p;
       const double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t3[3] = {qt[4], qt[5], qt[6]};
       for (int t = d.lid_cam_ptr[i] + lane; t < d.lid_cam_ptr[i + 1]; t += 64) {
         const double *L = d.lid_data + 12 * t;
@@ -479,7 +528,7 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
   for (int k = 0; k < 6; ++k) b[k] = wave_sum(b[k]);
   chi = wave_sum(chi);
   if (i < d.nP && lane == 0) {
-    double *Ho = d.Hpp + 36 * i;
+    double *Ho = (spec ? d.Hpp_nx : d.Hpp) + 36 * i;
     int k = 0;
     double mx = 0.0;
     for (int r = 0; r < 6; ++r)
@@ -489,16 +538,17 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d) {
         if (r == c) mx = fmax(mx, fabs(H[k]));
         ++k;
       }
-    for (int r = 0; r < 6; ++r) d.bp[8 * i + r] = b[r];
-    d.partials[kPartChiCurLid + i] = chi;
-    if (!d.sharded) atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
+    double *bo = spec ? d.bp_nx : d.bp;
+    for (int r = 0; r < 6; ++r) bo[8 * i + r] = b[r];
+    d.partials[(spec ? d.px_lid : d.pc_lid) + i] = chi;
+    if (!d.sharded && !spec) atomicMax(d.maxdiag, (unsigned long long)__double_as_longlong(mx));
   }
 }
 
-void launch_camera_pass(const DevProblem &d, hipStream_t st) {
+void launch_camera_pass(const DevProblem &d, hipStream_t st, bool spec) {
   if (d.nP == 0) return;
-  if (d.has_stereo) hipLaunchKernelGGL(k_camera_pass<true>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d);
-  else hipLaunchKernelGGL(k_camera_pass<false>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d);
+  if (d.has_stereo) hipLaunchKernelGGL(k_camera_pass<true>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d, (int)spec);
+  else hipLaunchKernelGGL(k_camera_pass<false>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d, (int)spec);
 }
 
 // Sharded runs, iteration 0: the pose Hessian diagonals of this rank (summed
@@ -1172,7 +1222,7 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st) {
 
 // Back-substitution dl = M (b_l - sum_i H_lp,i dx_i), X' = X + dl, then the
 // residuals of the landmark's edges at the trial state (computeActiveErrors).
-template <int W, bool ST>
+template <int W, bool ST, bool SPEC>
 __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
                                                          double lambda, int part_off) {
   __shared__ double red[4];
@@ -1187,45 +1237,49 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
     const bool valid = seg < nseg;
     double a0 = 0, a1 = 0, a2 = 0;
     int beg = 0, end = 0;
-    if (valid) {
-      beg = d.lm_begin[slot]; end = d.lm_begin[slot + 1];
-      // H_lp dx_cam = jl^T (jp dx_cam), Jacobians recomputed at the linearization point
-      const double L0 = d.X[0][4 * slot], L1 = d.X[0][4 * slot + 1], L2 = d.X[0][4 * slot + 2];
-      const double *prt_lin = d.pose_rt[0];
-      for (int e = beg + lane; e < end; e += W) {
-        const int h = d.obs_camh[e];
-        if (h < 0) continue;
-        const double *prt = prt_lin + 16 * d.obs_cam[e], *dx = d.dx + 6 * h;
-        double x[6];
+    if (valid) { beg = d.lm_begin[slot]; end = d.lm_begin[slot + 1]; }
+    const int ea = beg + lane, eb = ea + W;
+    const ObsIn oa = load_obs<ST, true>(d, ea, ea < end), ob = load_obs<ST, true>(d, eb, eb < end);
+    double L0 = 0.0, L1 = 0.0, L2 = 0.0;
+    if (valid) { L0 = d.X[0][4 * slot]; L1 = d.X[0][4 * slot + 1]; L2 = d.X[0][4 * slot + 2]; }
+    // H_lp dx_cam = jl^T (jp dx_cam), Jacobians recomputed at the linearization point
+    auto hlp_dx = [&](const ObsIn &o) {
+      if (o.camh < 0) return;
+      const double *prt = d.pose_rt[0] + 16 * o.cam, *dx = d.dx + 6 * o.camh;
+      double x[6];
 #pragma unroll
-        for (int k = 0; k < 6; ++k) x[k] = dx[k];
-        MonoEval m;
-        m.x = prt[0] * L0 + prt[1] * L1 + prt[2] * L2 + prt[9];
-        m.y = prt[3] * L0 + prt[4] * L1 + prt[5] * L2 + prt[10];
-        m.z = prt[6] * L0 + prt[7] * L1 + prt[8] * L2 + prt[11];
-        m.s = d.obs_s[e];
-        double jl[6], jp[12];
-        mono_jac(prt, m, jl, jp);
-        const double t0 = jp[0] * x[0] + jp[1] * x[1] + jp[2] * x[2] + jp[3] * x[3] + jp[5] * x[5];
-        const double t1 = jp[6] * x[0] + jp[7] * x[1] + jp[8] * x[2] + jp[10] * x[4] + jp[11] * x[5];
-        a0 += jl[0] * t0 + jl[3] * t1;
-        a1 += jl[1] * t0 + jl[4] * t1;
-        a2 += jl[2] * t0 + jl[5] * t1;
-        if (ST && d.obs_ur[e] >= 0.0) {
-          double jl3[3], jp3[6];
-          stereo_row(prt, m, d.pose_bf[d.obs_cam[e]], jl, jp, jl3, jp3);
-          const double t2 = jp3[0] * x[0] + jp3[1] * x[1] + jp3[2] * x[2] + jp3[3] * x[3] + jp3[5] * x[5];
-          a0 += jl3[0] * t2;
-          a1 += jl3[1] * t2;
-          a2 += jl3[2] * t2;
-        }
+      for (int k = 0; k < 6; ++k) x[k] = dx[k];
+      MonoEval m;
+      m.x = prt[0] * L0 + prt[1] * L1 + prt[2] * L2 + prt[9];
+      m.y = prt[3] * L0 + prt[4] * L1 + prt[5] * L2 + prt[10];
+      m.z = prt[6] * L0 + prt[7] * L1 + prt[8] * L2 + prt[11];
+      m.s = o.s;
+      double jl[6], jp[12];
+      mono_jac(prt, m, jl, jp);
+      const double t0 = jp[0] * x[0] + jp[1] * x[1] + jp[2] * x[2] + jp[3] * x[3] + jp[5] * x[5];
+      const double t1 = jp[6] * x[0] + jp[7] * x[1] + jp[8] * x[2] + jp[10] * x[4] + jp[11] * x[5];
+      a0 += jl[0] * t0 + jl[3] * t1;
+      a1 += jl[1] * t0 + jl[4] * t1;
+      a2 += jl[2] * t0 + jl[5] * t1;
+      if (ST && o.ur >= 0.0) {
+        double jl3[3], jp3[6];
+        stereo_row(prt, m, d.pose_bf[o.cam], jl, jp, jl3, jp3);
+        const double t2 = jp3[0] * x[0] + jp3[1] * x[1] + jp3[2] * x[2] + jp3[3] * x[3] + jp3[5] * x[5];
+        a0 += jl3[0] * t2;
+        a1 += jl3[1] * t2;
+        a2 += jl3[2] * t2;
       }
-    }
+    };
+    hlp_dx(oa);
+    hlp_dx(ob);
+    for (int e = eb + W; e < end; e += W) hlp_dx(load_obs<ST, true>(d, e, true));  // tracks > 128 only
 #pragma unroll
     for (int off = 1; off < W; off <<= 1) {
       a0 += __shfl_xor(a0, off, 64); a1 += __shfl_xor(a1, off, 64); a2 += __shfl_xor(a2, off, 64);
     }
     double chi = 0.0;
+    double R[6] = {0, 0, 0, 0, 0, 0};  // SPEC: QR of the landmark's rows at the trial state
+    double b0 = 0, b1 = 0, b2 = 0, g0 = 0, g1 = 0, g2 = 0;
     if (valid) {
       // dl = (H_ll + lambda I)^-1 c = R'^-1 (R'^-T c), R'^-1 upper (i00 i01 i02 i11 i12 i22)
       const double *Ri = d.lm_Rp + 12 * slot, *bl = d.lm_b + 4 * slot;
@@ -1234,31 +1288,46 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
       const double dl0 = Ri[0] * y0 + Ri[1] * y1 + Ri[2] * y2;
       const double dl1 = Ri[3] * y1 + Ri[4] * y2;
       const double dl2 = Ri[5] * y2;
-      const double *X = d.X[0] + 4 * slot;
-      const double X0 = X[0] + dl0, X1 = X[1] + dl1, X2 = X[2] + dl2;
+      const double X0 = L0 + dl0, X1 = L1 + dl1, X2 = L2 + dl2;
       if (lane == 0) {
         double *Xo = d.X[1] + 4 * slot;
         store2(Xo, X0, X1); store2(Xo + 2, X2, 0.0);
         sc_acc += dl0 * (lambda * dl0 + bl[0]) + dl1 * (lambda * dl1 + bl[1]) + dl2 * (lambda * dl2 + bl[2]);
       }
       const double *prt_all = d.pose_rt[1];
-      for (int e = beg + lane; e < end; e += W) {
-        const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
-        const int cam = d.obs_cam[e];
-        MonoEval m;
-        const double ur = ST ? d.obs_ur[e] : -1.0;
-        if (ST && ur >= 0.0)
-          stereo_error(prt_all + 16 * cam, X0, X1, X2, uv.x, uv.y, ur, d.pose_bf[cam], d.obs_info[e], d.obs_delta[e],
-                       m);
-        else
-          mono_error(prt_all + 16 * cam, X0, X1, X2, uv.x, uv.y, d.obs_info[e], d.obs_delta[e], m);
-        store2(d.obs_err + 2 * e, m.e0, m.e1);
-        if (ST) d.obs_err3[e] = ur >= 0.0 ? m.e2 : 0.0;
-        chi += m.chi_rob;
+      if (SPEC) {  // the next linearization at the trial state (used if the trial is accepted)
+        if (ea < end) lin_edge<ST>(d, oa, ea, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
+        if (eb < end) lin_edge<ST>(d, ob, eb, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
+        for (int e = eb + W; e < end; e += W)
+          lin_edge<ST>(d, load_obs<ST, true>(d, e, true), e, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2,
+                       g0, g1, g2, chi);
+      } else {
+        auto trial_err = [&](const ObsIn &o, int e) {
+          MonoEval m;
+          const double *prt = prt_all + 16 * o.cam;
+          if (ST && o.ur >= 0.0) stereo_error(prt, X0, X1, X2, o.u, o.v, o.ur, d.pose_bf[o.cam], o.info, o.delta, m);
+          else mono_error(prt, X0, X1, X2, o.u, o.v, o.info, o.delta, m);
+          store2(d.obs_err + 2 * e, m.e0, m.e1);
+          if (ST) d.obs_err3[e] = o.ur >= 0.0 ? m.e2 : 0.0;
+          chi += m.chi_rob;
+        };
+        if (ea < end) trial_err(oa, ea);
+        if (eb < end) trial_err(ob, eb);
+        for (int e = eb + W; e < end; e += W) trial_err(load_obs<ST, true>(d, e, true), e);
       }
     }
+    if (SPEC) {
+      lin_butterfly<W>(lane, R, b0, b1, b2, g0, g1, g2, chi);
+      if (valid && lane == 0) {
+        double *Ro = d.lm_R_nx + 8 * slot;
+        store2(Ro, R[0], R[1]); store2(Ro + 2, R[2], R[3]); store2(Ro + 4, R[4], R[5]);
+        double *bo = d.lm_b_nx + 4 * slot;
+        store2(bo, b0, b1); store2(bo + 2, b2, 0.0);
+      }
+    } else {
 #pragma unroll
-    for (int off = 1; off < W; off <<= 1) chi += __shfl_xor(chi, off, 64);
+      for (int off = 1; off < W; off <<= 1) chi += __shfl_xor(chi, off, 64);
+    }
     if (valid && lane == 0) chi_acc += chi;
   }
   const double s1 = block_sum(chi_acc, red);
@@ -1266,26 +1335,33 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
   if (threadIdx.x == 0) {
     d.partials[kPartChiNewLm + part_off + blockIdx.x] = s1;
     d.partials[kPartScaleLm + part_off + blockIdx.x] = s2;
+    if (SPEC) d.partials[d.px_lm + part_off + blockIdx.x] = s1;  // chi2 of the next linearization
   }
 }
 
-void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st) {
+void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st,
+                            bool spec) {
   const int nb = linearize_blocks(b);
   if (nb <= 0) return;
-  switch (b.W) {
-#define SQLM_CASE(WW)                                                                                    \
-  case WW:                                                                                               \
-    if (d.has_stereo)                                                                                    \
-      hipLaunchKernelGGL((k_landmark_update<WW, true>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin,  \
-                         b.slot_end, lambda, part_off);                                                  \
-    else                                                                                                 \
-      hipLaunchKernelGGL((k_landmark_update<WW, false>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, \
-                         b.slot_end, lambda, part_off);                                                  \
+#define SQLM_LAUNCH(WW, STT, SP) \
+  hipLaunchKernelGGL((k_landmark_update<WW, STT, SP>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, \
+                     lambda, part_off)
+#define SQLM_CASE(WW)                                   \
+  case WW:                                              \
+    if (d.has_stereo) {                                 \
+      if (spec) SQLM_LAUNCH(WW, true, true);            \
+      else SQLM_LAUNCH(WW, true, false);                \
+    } else {                                            \
+      if (spec) SQLM_LAUNCH(WW, false, true);           \
+      else SQLM_LAUNCH(WW, false, false);               \
+    }                                                   \
     break;
+  switch (b.W) {
     SQLM_CASE(2) SQLM_CASE(4) SQLM_CASE(8) SQLM_CASE(16) SQLM_CASE(32) SQLM_CASE(64)
-#undef SQLM_CASE
     default: break;
   }
+#undef SQLM_CASE
+#undef SQLM_LAUNCH
 }
 
 __global__ __launch_bounds__(256) void k_lidar_chi2(DevProblem d) {
@@ -1318,8 +1394,8 @@ __global__ __launch_bounds__(384) void k_reduce(DevProblem d, int n_lm_cur, int 
   const double *p = d.partials;
   int n = 0;
   switch (wave) {
-    case 0: p += kPartChiCurLm; n = n_lm_cur; break;
-    case 1: p += kPartChiCurLid; n = d.nP; break;
+    case 0: p += d.pc_lm; n = n_lm_cur; break;
+    case 1: p += d.pc_lid; n = d.nP; break;
     case 2: p += kPartChiNewLm; n = n_lm_new; break;
     case 3: p += kPartChiNewLid; n = n_lid; break;
     case 4: p += kPartScaleCam; n = n_cam; break;

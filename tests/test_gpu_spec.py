@@ -1,0 +1,71 @@
+"""Speculative linearization: every trial's
+k_landmark_update also linearizes at the trial state and the camera pass for
+that state runs on the side stream; an accepted trial swaps the results in and
+the next iteration skips its linearization pass. g2o linearizes at exactly that
+state with the same device code, so the run must be bit-identical to the plain
+schedule (SQLM_NO_SPEC=1): poses, points, edge chi2 and the whole LM trace
+compared with ==, including a problem with rejected trials (the speculative
+results of a rejected trial are discarded) and the three-pass local-BA
+schedule."""
+import numpy as np
+import pytest
+
+from sqrtlm import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ctx, prob, kind, monkeypatch, spec):
+    if spec:
+        monkeypatch.delenv("SQLM_NO_SPEC", raising=False)
+    else:
+        monkeypatch.setenv("SQLM_NO_SPEC", "1")
+    ctx.set_problem(prob)
+    if kind == "global":
+        n, st = ctx.global_ba(12)
+        out = (n, st)
+    elif kind == "local":
+        ran, tags, sts = ctx.local_ba()
+        out = (ran, tags.tolist(), sts)
+    else:
+        n, st = ctx.optimize(0, 20)
+        out = (n, st)
+    q, t = ctx.poses()
+    return out, q.copy(), t.copy(), ctx.points().copy(), ctx.edge_chi2().copy()
+
+
+def _strip(st):
+    """The LM decisions and values of a stats dict (timings removed)."""
+    drop = {"ms_total", "ms_setup", "ms_linearize", "ms_trials"}
+    if isinstance(st, dict):
+        return {k: v for k, v in st.items() if k not in drop}
+    return [_strip(s) for s in st]
+
+
+CASES = {
+    "config4_small": ("global", lambda: synth.config4(scale=0.02, seed=3)),
+    # an iteration with a rejected trial (oracle trace: [.., 2, ..])
+    "window_outliers": ("opt", lambda: synth.make_problem(30, 1500, seed=5, robust=True, outlier_frac=0.1)),
+    "stereo_lidar": ("opt", lambda: synth.add_lidar_flat(
+        synth.add_stereo(synth.make_problem(30, 1500, seed=6, robust=True), 0.5, seed=1), 29, 200, seed=2)),
+    "local_ba_schedule": ("local", lambda: synth.config2(seed=2)),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_speculative_bitwise_equal(gpu_ctx, monkeypatch, name):
+    kind, make = CASES[name]
+    prob = make()
+    a = _run(gpu_ctx, prob, kind, monkeypatch, True)
+    b = _run(gpu_ctx, prob, kind, monkeypatch, False)
+    if kind == "local":
+        assert a[0][0] == b[0][0] and a[0][1] == b[0][1]
+        assert _strip(a[0][2]) == _strip(b[0][2])
+    else:
+        assert a[0][0] == b[0][0]
+        assert _strip(a[0][1]) == _strip(b[0][1])
+    for x, y in zip(a[1:], b[1:]):
+        assert np.array_equal(x, y)
+    if name == "window_outliers":
+        assert max(a[0][1]["trace_trials"]) > 1  # the rejected-trial path ran
+
