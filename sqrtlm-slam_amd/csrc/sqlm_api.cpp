@@ -199,12 +199,12 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
         const int i = cur[u], j = cur[v];
         const int *b0 = s_col.data() + s_row[i], *b1 = s_col.data() + s_row[i + 1];
         const int sidx = (int)(std::lower_bound(b0, b1, j) - s_col.data());
-        red.push_back({sidx, t, (u << 8) | v});
+        red.push_back({sidx, t, tile_blk(u, v, cp)});
       }
     for (int u = 0; u < cp; ++u) gred.push_back({cur[u], t, u});
     const int ld = (6 * cp + 15) / 16 * 16;
     tp.ld.push_back(ld);
-    tp.part_ptr.push_back(tp.part_ptr.back() + (int64_t)ld * ld);
+    tp.part_ptr.push_back(tp.part_ptr.back() + 36 * (int64_t)(cp * (cp + 1) / 2));
     tp.gpart_ptr.push_back(tp.gpart_ptr.back() + ld);
     tp.cams.insert(tp.cams.end(), cur.begin(), cur.end());
     tp.cam_ptr.push_back(tp.cam_ptr.back() + cp);

@@ -139,6 +139,11 @@ struct CRPlan {
 };
 constexpr int kCRMaxN = 112;  // LDS: L (n x n+1) + Dinv (16n) + W (16n) <= 160 KiB
 
+// Tile partials are stored block-major: the upper 6x6 camera blocks (u <= w)
+// of a tile's cp cameras, packed row by row, 36 contiguous doubles each (the
+// reduction reads every contribution as one 288-byte run).
+__host__ __device__ inline int tile_blk(int u, int w, int cp) { return u * (2 * cp - u + 1) / 2 + (w - u); }
+
 struct Bucket {
   int W;            // segment width
   int slot_begin;   // first landmark slot

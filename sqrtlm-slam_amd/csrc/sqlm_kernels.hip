@@ -853,7 +853,7 @@ __device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int t
 }
 
 template <int NT, bool ST>
-__global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
+__global__ __launch_bounds__(kTileThreads, 3) void k_rcs_tile(DevProblem d) {
   // wave w owns the accumulator tiles q with q % kTileWaves == w
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
   constexpr int NC = NT * 16, NG = (NC + TH - 1) / TH;
@@ -869,7 +869,7 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
   __shared__ double Lbf[ST ? kTileMaxCams : 1];   // window cameras: bf (stereo edges)
   const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
-  const int ncol = 6 * cp, nt = (ncol + 15) >> 4, ld = nt * 16;
+  const int ncol = 6 * cp, nt = (ncol + 15) >> 4;
   const int r16 = lane & 15, k4 = lane >> 4;
   d4v acc[NQW];
 #pragma unroll
@@ -1027,17 +1027,29 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
     TP(6);
   }
   TP_STORE;
-  // write -G_t (upper tiles) as the tile's partial, ld = 16 nt
+  // write -G_t as the tile's partial, block-major (tile_blk): element (R, C) of
+  // an upper 16x16 tile goes to block (R/6, C/6) if that block is upper; a
+  // diagonal block straddling two tiles also gets the mirror of the elements
+  // whose transpose falls in the (never computed) lower tile
   double *out = d.part + d.tile_part_ptr[t];
+  const int n6 = 6 * cp;
   int q = 0;
 #pragma unroll
   for (int ti = 0; ti < NT; ++ti)
 #pragma unroll
     for (int tj = ti; tj < NT; ++tj, ++q) {
       if (q % kTileWaves == wave && tj < nt) {
+        const int C = tj * 16 + r16, w = C / 6, c = C - 6 * w;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          out[(size_t)(ti * 16 + k4 + 4 * j) * ld + tj * 16 + r16] = -acc[q / kTileWaves][j];
+        for (int j = 0; j < 4; ++j) {
+          const int R = ti * 16 + k4 + 4 * j, u = R / 6, r = R - 6 * u;
+          if (R < n6 && C < n6 && u <= w) {
+            double *blk = out + 36 * tile_blk(u, w, cp);
+            const double v = -acc[q / kTileWaves][j];
+            blk[6 * r + c] = v;
+            if (u == w && ti < tj) blk[6 * c + r] = v;
+          }
+        }
       }
     }
   double *go = d.gpart + d.tile_gpart_ptr[t];
@@ -1049,8 +1061,8 @@ __global__ __launch_bounds__(kTileThreads, 2) void k_rcs_tile(DevProblem d) {
 }
 
 // S block s = sum of its tile partials (tile order) + H_pp + lambda I on the
-// diagonal; g row i likewise. Partials are symmetric: entries that fall in a
-// lower 16x16 tile are read from their transpose. With cr_direct the sums go
+// diagonal; g row i likewise. Each contribution is one 36-double block of a
+// tile's block-major partial (tile_blk). With cr_direct the sums go
 // straight into the block-tridiagonal superblocks of the CR solver (D_I and
 // its mirror, E_I = S(I, I+1), g_I, identity on padded rows), replacing the
 // BSR copy and its scatter.
@@ -1061,12 +1073,8 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
     const int s = (int)(gid / 36), e = (int)(gid % 36), r = e / 6, c = e % 6;
     double v = 0.0;
     for (int k = d.red_ptr[s]; k < d.red_ptr[s + 1]; ++k) {
-      const int2 ct = d.red_idx[k];
-      const int u = ct.y >> 8, w = ct.y & 255;
-      const int ld = d.tile_ld[ct.x];
-      int R = 6 * u + r, C = 6 * w + c;
-      if ((R >> 4) > (C >> 4)) { const int tmp = R; R = C; C = tmp; }
-      v += d.part[d.tile_part_ptr[ct.x] + (int64_t)R * ld + C];
+      const int2 ct = d.red_idx[k];  // (tile, block index in the tile's partial)
+      v += d.part[d.tile_part_ptr[ct.x] + 36 * (int64_t)ct.y + e];
     }
     const int j = d.s_col[s];
     if (s == d.s_row_ptr[j]) {  // diagonal block (first block of row j); sharded: this rank's share
