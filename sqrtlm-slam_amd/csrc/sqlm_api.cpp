@@ -516,7 +516,6 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_LMB, 4 * (size_t)nL, d.lm_b);
   AL(B_LMM, 8 * (size_t)nL, d.lm_M);
   AL(B_LMV, 4 * (size_t)nL, d.lm_v);
-  AL(B_LMRP, 12 * (size_t)nL, d.lm_Rp);
   d.n_tiles = c->use_tiles ? (int)tp.lm_ptr.size() - 1 : 0;
   d.tile_dups = tp.dups ? 1 : 0;
   {

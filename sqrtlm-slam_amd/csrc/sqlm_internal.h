@@ -34,7 +34,6 @@ struct DevProblem {
   double *lm_R_nx = nullptr, *lm_b_nx = nullptr, *obs_s_nx = nullptr, *Hpp_nx = nullptr, *bp_nx = nullptr;
   double *lm_M = nullptr;                   // [nL][8]  (H_ll + lambda I)^-1, sym (6)
   double *lm_v = nullptr;                   // [nL][4]  M b_l
-  double *lm_Rp = nullptr;                  // [nL][12] R'^-1 of the damped factor (6), w = R'^-T b_l (3)
   // observations
   int *obs_lm = nullptr;                    // [nE] landmark slot
   int *obs_cam = nullptr;                   // [nE] pose id

@@ -633,11 +633,12 @@ void launch_flag_pack(const DevProblem &d, bool unpack, hipStream_t st) {
 
 // ---------------------------------------------------------------- damping
 
-// R' = QR([R; sqrt(lambda) I]) by three Givens sweeps; M = R'^-1 R'^-T.
-__global__ void k_damp(DevProblem d, double lambda) {
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= d.nL) return;
-  const double *Rl = d.lm_R + 8 * l;
+// Damped landmark factor: R' = QR([R; sqrt(lambda) I]) by three Givens
+// sweeps, its inverse R'^-1 (upper: i00 i01 i02 i11 i12 i22) and
+// w = R'^-T b_l. Computed where it is consumed (the RCS tile staging and the
+// landmark update, same code => same bits), not stored per trial.
+__device__ __forceinline__ void damp_factor(const double *__restrict__ Rl, const double *__restrict__ bl,
+                                            double lambda, double Ri[6], double w[3]) {
   double R[6] = {Rl[0], Rl[1], Rl[2], Rl[3], Rl[4], Rl[5]};
   const double sl = sqrt(lambda);
   givens_add_row(R, sl, 0.0, 0.0);
@@ -647,35 +648,37 @@ __global__ void k_damp(DevProblem d, double lambda) {
   const double i01 = -(R[1] * i11) * i00;
   const double i12 = -(R[4] * i22) * i11;
   const double i02 = -(R[1] * i12 + R[2] * i22) * i00;
+  Ri[0] = i00; Ri[1] = i01; Ri[2] = i02; Ri[3] = i11; Ri[4] = i12; Ri[5] = i22;
+  w[0] = i00 * bl[0];
+  w[1] = i01 * bl[0] + i11 * bl[1];
+  w[2] = i02 * bl[0] + i12 * bl[1] + i22 * bl[2];
+}
+
+// Row-kernel RCS fallback only: M = (R'^T R')^-1 = R'^-1 R'^-T and M b_l.
+__global__ void k_damp(DevProblem d, double lambda) {
+  const int l = blockIdx.x * blockDim.x + threadIdx.x;
+  if (l >= d.nL) return;
+  double Ri[6], w[3];
+  const double *bl = d.lm_b + 4 * l;
+  damp_factor(d.lm_R + 8 * l, bl, lambda, Ri, w);
+  const double i00 = Ri[0], i01 = Ri[1], i02 = Ri[2], i11 = Ri[3], i12 = Ri[4], i22 = Ri[5];
   const double m00 = i00 * i00 + i01 * i01 + i02 * i02;
   const double m01 = i01 * i11 + i02 * i12;
   const double m02 = i02 * i22;
   const double m11 = i11 * i11 + i12 * i12;
   const double m12 = i12 * i22;
   const double m22 = i22 * i22;
-  if (d.obs_P) {  // row-kernel RCS fallback only: M = (R'^T R')^-1 and M b_l
-    double *M = d.lm_M + 8 * l;
-    store2(M, m00, m01); store2(M + 2, m02, m11); store2(M + 4, m12, m22);
-  }
-  const double *bl = d.lm_b + 4 * l;
-  // R'^-1 (upper) and w = R'^-T b_l; the RCS tiles stage Y = R'^-T P as (R'^-1)^T P
-  const double w0 = i00 * bl[0];
-  const double w1 = i01 * bl[0] + i11 * bl[1];
-  const double w2 = i02 * bl[0] + i12 * bl[1] + i22 * bl[2];
-  double *Rp = d.lm_Rp + 12 * l;
-  store2(Rp, i00, i01); store2(Rp + 2, i02, i11); store2(Rp + 4, i12, i22);
-  store2(Rp + 6, w0, w1); store2(Rp + 8, w2, 0.0);
-  if (d.obs_P) {
-    const double v0 = m00 * bl[0] + m01 * bl[1] + m02 * bl[2];
-    const double v1 = m01 * bl[0] + m11 * bl[1] + m12 * bl[2];
-    const double v2 = m02 * bl[0] + m12 * bl[1] + m22 * bl[2];
-    double *v = d.lm_v + 4 * l;
-    store2(v, v0, v1); store2(v + 2, v2, 0.0);
-  }
+  double *M = d.lm_M + 8 * l;
+  store2(M, m00, m01); store2(M + 2, m02, m11); store2(M + 4, m12, m22);
+  const double v0 = m00 * bl[0] + m01 * bl[1] + m02 * bl[2];
+  const double v1 = m01 * bl[0] + m11 * bl[1] + m12 * bl[2];
+  const double v2 = m02 * bl[0] + m12 * bl[1] + m22 * bl[2];
+  double *v = d.lm_v + 4 * l;
+  store2(v, v0, v1); store2(v + 2, v2, 0.0);
 }
 
 void launch_damp(const DevProblem &d, double lambda, hipStream_t st) {
-  if (d.nL == 0) return;
+  if (d.nL == 0 || !d.obs_P) return;  // the tiled path damps where it consumes
   hipLaunchKernelGGL(k_damp, dim3((d.nL + 255) / 256), dim3(256), 0, st, d, lambda);
 }
 
@@ -853,8 +856,9 @@ __device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int t
 }
 
 template <int NT, bool ST>
-__global__ __launch_bounds__(kTileThreads, 3) void k_rcs_tile(DevProblem d) {
-  // wave w owns the accumulator tiles q with q % kTileWaves == w
+__global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProblem d, double lambda) {
+  // wave w owns the accumulator tiles q with q % kTileWaves == w; 3 waves per SIMD
+  // for mono problems (167 VGPRs), 2 with the stereo row (spill-free)
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
   constexpr int NC = NT * 16, NG = (NC + TH - 1) / TH;
   constexpr int BL = kTileBL;
@@ -883,11 +887,7 @@ __global__ __launch_bounds__(kTileThreads, 3) void k_rcs_tile(DevProblem d) {
   const bool slow = d.tile_dups || d.tile_maxk > kTileFastK;
   for (int k = tid; k <= ntl; k += TH) Lb[k] = d.lm_begin[l0 + k];
   for (int k = tid; k < ntl; k += TH) Lu[k] = d.lm_urange[l0 + k];
-  for (int k = tid; k < 9 * ntl; k += TH) {
-    const int li = k / 9, c = k - 9 * li;
-    const double v = d.lm_Rp[12 * (l0 + li) + c];
-    if (c < 6) Lr[li][c] = v; else Lw[li][c - 6] = v;
-  }
+  for (int li = tid; li < ntl; li += TH) damp_factor(d.lm_R + 8 * (l0 + li), d.lm_b + 4 * (l0 + li), lambda, Lr[li], Lw[li]);
   for (int k = tid; k < 3 * ntl; k += TH) {
     const int li = k / 3, c = k - 3 * li;
     Lx[li][c] = d.X[0][4 * (l0 + li) + c];
@@ -1127,8 +1127,8 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
   if (d.n_tiles > 0) {
 #define SQLM_TILE(NTT)                                                                            \
   do {                                                                                            \
-    if (d.has_stereo) hipLaunchKernelGGL((k_rcs_tile<NTT, true>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d); \
-    else hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d);            \
+    if (d.has_stereo) hipLaunchKernelGGL((k_rcs_tile<NTT, true>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d, lambda); \
+    else hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d, lambda);    \
   } while (0)
     if (nt <= 3) SQLM_TILE(3);
     else if (nt <= 5) SQLM_TILE(5);
@@ -1290,7 +1290,9 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
     double b0 = 0, b1 = 0, b2 = 0, g0 = 0, g1 = 0, g2 = 0;
     if (valid) {
       // dl = (H_ll + lambda I)^-1 c = R'^-1 (R'^-T c), R'^-1 upper (i00 i01 i02 i11 i12 i22)
-      const double *Ri = d.lm_Rp + 12 * slot, *bl = d.lm_b + 4 * slot;
+      const double *bl = d.lm_b + 4 * slot;
+      double Ri[6], wl[3];
+      damp_factor(d.lm_R + 8 * slot, bl, lambda, Ri, wl);
       const double c0 = bl[0] - a0, c1 = bl[1] - a1, c2 = bl[2] - a2;
       const double y0 = Ri[0] * c0, y1 = Ri[1] * c0 + Ri[3] * c1, y2 = Ri[2] * c0 + Ri[4] * c1 + Ri[5] * c2;
       const double dl0 = Ri[0] * y0 + Ri[1] * y1 + Ri[2] * y2;
@@ -1396,30 +1398,49 @@ void launch_lidar_chi2(const DevProblem &d, hipStream_t st) {
 // ---------------------------------------------------------------- reductions
 
 // The six partial regions, one wavefront each (fixed order: bitwise deterministic).
-__global__ __launch_bounds__(384) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam, int n_lid) {
-  __shared__ double part[6];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// The six partial regions folded into the trial scalars by one 1024-thread
+// block: every thread loads its strided share of all regions with the loads
+// of four strides in flight together (one memory latency per 4096 partials,
+// not one per 64), then fixed-order wave and block sums (deterministic).
+constexpr int kReduceThreads = 1024;
+__global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam,
+                                                          int n_lid) {
+  __shared__ double red[6][kReduceThreads / 64];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const double *p = d.partials;
-  int n = 0;
-  switch (wave) {
-    case 0: p += d.pc_lm; n = n_lm_cur; break;
-    case 1: p += d.pc_lid; n = d.nP; break;
-    case 2: p += kPartChiNewLm; n = n_lm_new; break;
-    case 3: p += kPartChiNewLid; n = n_lid; break;
-    case 4: p += kPartScaleCam; n = n_cam; break;
-    default: p += kPartScaleLm; n = n_lm_new; break;
+  const double *base[6] = {p + d.pc_lm, p + d.pc_lid, p + kPartChiNewLm, p + kPartChiNewLid, p + kPartScaleCam,
+                           p + kPartScaleLm};
+  const int n[6] = {n_lm_cur, d.nP, n_lm_new, n_lid, n_cam, n_lm_new};
+  int nmax = 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) nmax = max(nmax, n[r]);
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int k0 = tid; k0 < nmax; k0 += 4 * kReduceThreads) {
+    double v[4][6];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const int k = k0 + u * kReduceThreads;
+        v[u][r] = k < n[r] ? base[r][k] : 0.0;
+      }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) acc[r] += (v[0][r] + v[1][r]) + (v[2][r] + v[3][r]);
   }
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  for (int k = lane; k < n; k += 256) {
-    a0 += p[k];
-    if (k + 64 < n) a1 += p[k + 64];
-    if (k + 128 < n) a2 += p[k + 128];
-    if (k + 192 < n) a3 += p[k + 192];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const double w = wave_sum(acc[r]);
+    if (lane == 0) red[r][wave] = w;
   }
-  const double v = wave_sum((a0 + a1) + (a2 + a3));
-  if (lane == 0) part[wave] = v;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
+    double part[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      double t = 0.0;
+      for (int w = 0; w < kReduceThreads / 64; ++w) t += red[r][w];
+      part[r] = t;
+    }
     d.scalars[kChiCur] = part[0] + part[1];
     d.scalars[kChiNew] = part[2] + part[3];
     d.scalars[kScale] = part[4] + part[5];
@@ -1431,7 +1452,7 @@ __global__ __launch_bounds__(384) void k_reduce(DevProblem d, int n_lm_cur, int 
 
 void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts, int n_lid_parts,
                    hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(384), 0, st, d, n_lm_parts_cur, n_lm_parts_new, n_cam_parts,
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, st, d, n_lm_parts_cur, n_lm_parts_new, n_cam_parts,
                      n_lid_parts);
 }
 
