@@ -9,8 +9,9 @@ synthetic local BA, 50 KF x 5k landmarks x 200 obs/KF) instead.
 A "step" is one Levenberg–Marquardt outer iteration exactly as g2o runs it
 (relinearise, then damped trials until one is accepted), with every array
 already resident in HBM. Multi-GPU: landmarks are sharded over ranks (one
-process per GPU), the reduced camera system is summed over RCCL, every rank
-factorises it; total work is fixed => strong scaling.
+process per GPU); every rank assembles the S / g rows of its landmarks, rank 0
+gathers them over RCCL point-to-point, solves, and broadcasts the step; total
+work is fixed => strong scaling.
 
 Prints ONE JSON line on rank 0.
 """
@@ -62,6 +63,17 @@ def algorithmic_bytes_linearize(p) -> float:
     L2-resident) excluded."""
     E, L = p.n_obs, p.n_pt
     return E * (40 + 16 + 8) + L * (24 + 4 + 48 + 24)
+
+
+def algorithmic_bytes_update(p) -> float:
+    """Bytes k_landmark_update<SPEC> must move per trial (DESIGN.md §2 steps
+    6-7): per observation it reads cam id, free-camera id, uv, info, delta and
+    the linearization-point weight s (48 B) and writes the trial error (16 B)
+    and the trial-state weight (8 B); per landmark it reads the offset, X, R
+    and b_l (100 B) and writes X' and the trial-state R, b_l (96 B). Pose and
+    dx reads (<1 MB, L2-resident) excluded."""
+    E, L = p.n_obs, p.n_pt
+    return E * (48 + 16 + 8) + L * (100 + 96)
 
 
 def algorithmic_flops_rcs(p) -> float:
@@ -374,10 +386,14 @@ def main():
         flops = algorithmic_flops_rcs(local)
         ach_tf = flops / (t_rcs * 1e-3) / 1e12 if t_rcs > 0 else 0.0
         traffic, tsrc = pmc_traffic("k_rcs_tile", args.config, local.n_obs) if world == 1 else (None, None)
-        t_lin = kms["k_linearize"]
-        alg = algorithmic_bytes_linearize(local)
+        # the landmark linearization runs inside k_landmark_update (speculative,
+        # DESIGN.md §2 step 7) unless SQLM_NO_SPEC=1 puts it back in k_linearize
+        spec = os.environ.get("SQLM_NO_SPEC", "0") in ("", "0")
+        lin_kernel = "k_landmark_update" if spec else "k_linearize"
+        t_lin = kms[lin_kernel] / (launches if spec else 1.0)
+        alg = algorithmic_bytes_update(local) if spec else algorithmic_bytes_linearize(local)
         achieved = alg / (t_lin * 1e-3) / 1e9 if t_lin > 0 else 0.0
-        lin_traffic, _ = pmc_traffic("k_linearize", args.config, local.n_obs) if world == 1 else (None, None)
+        lin_traffic, _ = pmc_traffic(lin_kernel, args.config, local.n_obs) if world == 1 else (None, None)
         out = {
             "metric": "LM iterations/sec (synthetic KITTI-00-scale BA)",
             "value": 1000.0 / ms,
@@ -401,11 +417,11 @@ def main():
                          "peak": MFMA_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach_tf / MFMA_F64_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": tsrc, "algorithmic_flops": flops,
                          "launch_ms": t_rcs},
-            "roofline_secondary": {"bound": "hbm", "kernel": "k_linearize (all buckets)", "achieved": achieved,
+            "roofline_secondary": {"bound": "hbm", "kernel": f"{lin_kernel} (all buckets)", "achieved": achieved,
                                    "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                                    "traffic": lin_traffic, "algorithmic_bytes": alg, "launch_ms": t_lin,
                                    "survey_basis_GBps": survey_bytes_linearize(local) / (t_lin * 1e-3) / 1e9
-                                   if t_lin else None},
+                                   if t_lin and not spec else None},
         }
         out["final_rmse_px"] = float(np.sqrt(sse / max(1.0, nres)))
         if e2e is not None:
