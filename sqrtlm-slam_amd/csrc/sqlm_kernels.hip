@@ -342,17 +342,40 @@ __device__ __forceinline__ void lin_edge(const DevProblem &d, const ObsIn &o, in
   }
 }
 
+// Exchange with the partner group of a segment butterfly level OFF. Within a
+// row of 16 lanes this is a DPP move (quad_perm for 1 and 2, half-row / row
+// mirror for 4 and 8: after the lower levels every lane of a group holds the
+// same value, so the mirror partner is as good as lane ^ OFF), else ds_bpermute.
+template <int OFF>
+__device__ __forceinline__ double seg_xor(double v) {
+  if constexpr (OFF <= 8) {
+    constexpr int ctrl = OFF == 1 ? 0xB1 : OFF == 2 ? 0x4E : OFF == 4 ? 0x141 : 0x140;
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), ctrl, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+  } else {
+    return __shfl_xor(v, OFF, 64);
+  }
+}
+
+// Sum over a W-lane segment, the same tree in every lane (bitwise equal results).
+template <int W, int OFF = 1>
+__device__ __forceinline__ double seg_sum(double v) {
+  if constexpr (OFF < W) return seg_sum<W, 2 * OFF>(v + seg_xor<OFF>(v));
+  else return v;
+}
+
 // TSQR butterfly inside a W-lane segment (canonical: the lower lane's R absorbs
 // the upper's rows), with the sums of b, g and chi2.
-template <int W>
+template <int W, int OFF = 1>
 __device__ __forceinline__ void lin_butterfly(int lane, double R[6], double &b0, double &b1, double &b2, double &g0,
                                               double &g1, double &g2, double &chi) {
-#pragma unroll
-  for (int off = 1; off < W; off <<= 1) {
+  if constexpr (OFF < W) {
     double o[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) o[i] = __shfl_xor(R[i], off, 64);
-    const bool lo = (lane & off) == 0;
+    for (int i = 0; i < 6; ++i) o[i] = seg_xor<OFF>(R[i]);
+    const bool lo = (lane & OFF) == 0;
     double A[6], B[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) { A[i] = lo ? R[i] : o[i]; B[i] = lo ? o[i] : R[i]; }
@@ -361,9 +384,10 @@ __device__ __forceinline__ void lin_butterfly(int lane, double R[6], double &b0,
     givens_add_row(A, 0.0, 0.0, B[5]);
 #pragma unroll
     for (int i = 0; i < 6; ++i) R[i] = A[i];
-    b0 += __shfl_xor(b0, off, 64); b1 += __shfl_xor(b1, off, 64); b2 += __shfl_xor(b2, off, 64);
-    g0 += __shfl_xor(g0, off, 64); g1 += __shfl_xor(g1, off, 64); g2 += __shfl_xor(g2, off, 64);
-    chi += __shfl_xor(chi, off, 64);
+    b0 += seg_xor<OFF>(b0); b1 += seg_xor<OFF>(b1); b2 += seg_xor<OFF>(b2);
+    g0 += seg_xor<OFF>(g0); g1 += seg_xor<OFF>(g1); g2 += seg_xor<OFF>(g2);
+    chi += seg_xor<OFF>(chi);
+    lin_butterfly<W, 2 * OFF>(lane, R, b0, b1, b2, g0, g1, g2, chi);
   }
 }
 
@@ -1281,10 +1305,7 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
     hlp_dx(oa);
     hlp_dx(ob);
     for (int e = eb + W; e < end; e += W) hlp_dx(load_obs<ST, true>(d, e, true));  // tracks > 128 only
-#pragma unroll
-    for (int off = 1; off < W; off <<= 1) {
-      a0 += __shfl_xor(a0, off, 64); a1 += __shfl_xor(a1, off, 64); a2 += __shfl_xor(a2, off, 64);
-    }
+    a0 = seg_sum<W>(a0); a1 = seg_sum<W>(a1); a2 = seg_sum<W>(a2);
     double chi = 0.0;
     double R[6] = {0, 0, 0, 0, 0, 0};  // SPEC: QR of the landmark's rows at the trial state
     double b0 = 0, b1 = 0, b2 = 0, g0 = 0, g1 = 0, g2 = 0;
@@ -1335,8 +1356,7 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
         store2(bo, b0, b1); store2(bo + 2, b2, 0.0);
       }
     } else {
-#pragma unroll
-      for (int off = 1; off < W; off <<= 1) chi += __shfl_xor(chi, off, 64);
+      chi = seg_sum<W>(chi);
     }
     if (valid && lane == 0) chi_acc += chi;
   }
