@@ -244,12 +244,11 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
   csr(gred, nP, tp.gred_ptr, tp.gred_idx);
 }
 
-// Lanes per landmark segment in the per-landmark kernels: up to two
-// observations per lane (a serial pair of Givens rows is cheaper than one
-// more butterfly round), at least 2 lanes.
+// Lanes per landmark segment in the per-landmark kernels: up to kObsPerLane
+// observations per lane, at least 2 lanes.
 inline int seg_width(int k) {
   int w = 2;
-  while (2 * w < k && w < 64) w <<= 1;
+  while (kObsPerLane * w < k && w < 64) w <<= 1;
   return w;
 }
 

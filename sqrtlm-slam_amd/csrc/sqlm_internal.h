@@ -143,6 +143,20 @@ constexpr int kCRMaxN = 112;  // LDS: L (n x n+1) + Dinv (16n) + W (16n) <= 160 
 // reduction reads every contribution as one 288-byte run).
 __host__ __device__ inline int tile_blk(int u, int w, int cp) { return u * (2 * cp - u + 1) / 2 + (w - u); }
 
+// Observations per lane in the per-landmark kernels (k_linearize,
+// k_landmark_update): a segment of W lanes serves tracks of up to
+// kObsPerLane * W observations. A serial chain of Givens rows per lane is
+// cheaper than more lanes and butterfly rounds (config 4: 1 / 2 / 3 / 4 per
+// lane -> 0.43 / 0.33 / 0.30 / 0.31 ms for the speculative landmark update,
+// two of them preloaded).
+#ifndef SQLM_OBS_PER_LANE
+#define SQLM_OBS_PER_LANE 3
+#endif
+constexpr int kObsPerLane = SQLM_OBS_PER_LANE;
+// loaded up front (the rest of a lane's observations stream in a loop): 3
+// would push the speculative landmark update to 130 VGPRs, 3 waves per SIMD
+constexpr int kObsPreload = 2;
+
 struct Bucket {
   int W;            // segment width
   int slot_begin;   // first landmark slot

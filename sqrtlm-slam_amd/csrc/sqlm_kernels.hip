@@ -247,8 +247,8 @@ __device__ __forceinline__ void store2(double *p, double a, double b) {
 }
 
 // The per-observation inputs of one edge, loaded up front: every lane of a
-// segment owns at most two observations (W >= k / 2, seg_width), so both are
-// requested before any of them is used and their latencies overlap.
+// segment owns at most kObsPerLane observations (W >= k / kObsPerLane,
+// seg_width); the first kObsPreload of them are requested before any is used.
 struct ObsIn {
   int cam, camh;
   double u, v, info, delta, ur, s;
@@ -425,11 +425,15 @@ __global__ __launch_bounds__(256) void k_linearize(DevProblem d, int slot_begin,
     if (valid) {
       const double X0 = d.X[0][4 * slot], X1 = d.X[0][4 * slot + 1], X2 = d.X[0][4 * slot + 2];
       const int beg = d.lm_begin[slot], end = d.lm_begin[slot + 1];
-      const int ea = beg + lane, eb = ea + W;
-      const ObsIn oa = load_obs<ST, false>(d, ea, ea < end), ob = load_obs<ST, false>(d, eb, eb < end);
-      if (ea < end) lin_edge<ST>(d, oa, ea, prt_all, X0, X1, X2, d.obs_s, true, R, b0, b1, b2, g0, g1, g2, chi);
-      if (eb < end) lin_edge<ST>(d, ob, eb, prt_all, X0, X1, X2, d.obs_s, true, R, b0, b1, b2, g0, g1, g2, chi);
-      for (int e = eb + W; e < end; e += W)  // tracks > 128 only
+      ObsIn o[kObsPreload];
+#pragma unroll
+      for (int i = 0; i < kObsPreload; ++i) o[i] = load_obs<ST, false>(d, beg + lane + i * W, beg + lane + i * W < end);
+#pragma unroll
+      for (int i = 0; i < kObsPreload; ++i) {
+        const int e = beg + lane + i * W;
+        if (e < end) lin_edge<ST>(d, o[i], e, prt_all, X0, X1, X2, d.obs_s, true, R, b0, b1, b2, g0, g1, g2, chi);
+      }
+      for (int e = beg + lane + kObsPreload * W; e < end; e += W)  // the rest of the lane's observations
         lin_edge<ST>(d, load_obs<ST, false>(d, e, true), e, prt_all, X0, X1, X2, d.obs_s, true, R, b0, b1, b2, g0, g1,
                      g2, chi);
     }
@@ -1270,8 +1274,9 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
     double a0 = 0, a1 = 0, a2 = 0;
     int beg = 0, end = 0;
     if (valid) { beg = d.lm_begin[slot]; end = d.lm_begin[slot + 1]; }
-    const int ea = beg + lane, eb = ea + W;
-    const ObsIn oa = load_obs<ST, true>(d, ea, ea < end), ob = load_obs<ST, true>(d, eb, eb < end);
+    ObsIn o[kObsPreload];
+#pragma unroll
+    for (int i = 0; i < kObsPreload; ++i) o[i] = load_obs<ST, true>(d, beg + lane + i * W, beg + lane + i * W < end);
     double L0 = 0.0, L1 = 0.0, L2 = 0.0;
     if (valid) { L0 = d.X[0][4 * slot]; L1 = d.X[0][4 * slot + 1]; L2 = d.X[0][4 * slot + 2]; }
     // H_lp dx_cam = jl^T (jp dx_cam), Jacobians recomputed at the linearization point
@@ -1302,9 +1307,9 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
         a2 += jl3[2] * t2;
       }
     };
-    hlp_dx(oa);
-    hlp_dx(ob);
-    for (int e = eb + W; e < end; e += W) hlp_dx(load_obs<ST, true>(d, e, true));  // tracks > 128 only
+#pragma unroll
+    for (int i = 0; i < kObsPreload; ++i) hlp_dx(o[i]);  // camh = -1 for lanes past the track
+    for (int e = beg + lane + kObsPreload * W; e < end; e += W) hlp_dx(load_obs<ST, true>(d, e, true));
     a0 = seg_sum<W>(a0); a1 = seg_sum<W>(a1); a2 = seg_sum<W>(a2);
     double chi = 0.0;
     double R[6] = {0, 0, 0, 0, 0, 0};  // SPEC: QR of the landmark's rows at the trial state
@@ -1327,9 +1332,12 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
       }
       const double *prt_all = d.pose_rt[1];
       if (SPEC) {  // the next linearization at the trial state (used if the trial is accepted)
-        if (ea < end) lin_edge<ST>(d, oa, ea, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
-        if (eb < end) lin_edge<ST>(d, ob, eb, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
-        for (int e = eb + W; e < end; e += W)
+#pragma unroll
+        for (int i = 0; i < kObsPreload; ++i) {
+          const int e = beg + lane + i * W;
+          if (e < end) lin_edge<ST>(d, o[i], e, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
+        }
+        for (int e = beg + lane + kObsPreload * W; e < end; e += W)
           lin_edge<ST>(d, load_obs<ST, true>(d, e, true), e, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2,
                        g0, g1, g2, chi);
       } else {
@@ -1342,9 +1350,10 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
           if (ST) d.obs_err3[e] = o.ur >= 0.0 ? m.e2 : 0.0;
           chi += m.chi_rob;
         };
-        if (ea < end) trial_err(oa, ea);
-        if (eb < end) trial_err(ob, eb);
-        for (int e = eb + W; e < end; e += W) trial_err(load_obs<ST, true>(d, e, true), e);
+#pragma unroll
+        for (int i = 0; i < kObsPreload; ++i)
+          if (beg + lane + i * W < end) trial_err(o[i], beg + lane + i * W);
+        for (int e = beg + lane + kObsPreload * W; e < end; e += W) trial_err(load_obs<ST, true>(d, e, true), e);
       }
     }
     if (SPEC) {
