@@ -283,6 +283,98 @@ __global__ __launch_bounds__(256) void k_eg_reduce(EGDev d, int n_err_parts, int
   if (threadIdx.x == 0 && flags) d.scalars[4] = (double)flags[0];
 }
 
+// ---- band + border solve of the block-arrow layout (cyclic reduction) -------
+// The band (p blocks of n = kCRMaxN rows) is block-tridiagonal and the border
+// couples to any band block, so [B F^T; F G] [x_b; x_c] = [r_b; r_c] is solved as
+//   B [Y | y] = [F^T | r_b]     cyclic reduction, R = nb + 1 right-hand sides
+//   (G - F Y) x_c = r_c - F y   dense Cholesky of the nb x nb border system
+//   x_b = y - Y x_c,
+// i.e. log2(p) levels of 112-row block factorizations instead of p sequential
+// block steps of the arrow Cholesky.
+struct EGCR {
+  int p = 0, n = 0, R = 0, nb = 0, nc = 0;
+  double *D = nullptr, *E = nullptr, *A = nullptr, *Cm = nullptr, *gs = nullptr, *xs = nullptr;
+  double *G = nullptr, *Go = nullptr, *Z = nullptr, *X = nullptr, *P = nullptr;
+  double *Sc = nullptr, *ScL = nullptr, *ScLinv = nullptr, *rc = nullptr, *xc = nullptr;
+};
+
+// D_I / E_I / G_I (and its copy Go) from the assembled lower H0 with lambda on
+// the diagonal of the problem rows (identity on padding rows), the border
+// system S_c = G + lambda I and r_c.
+__global__ __launch_bounds__(256) void k_egcr_gather(EGDev d, EGCR c, double lambda) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = c.n, R = c.R;
+  const int64_t np = d.n_pad, nn = (int64_t)n * n, nD = (int64_t)c.p * nn, nG = (int64_t)c.p * n * R;
+  const int64_t nS = (int64_t)c.nc * c.nc;
+  const int vb = 7 * d.band_slots, b0 = 7 * d.border0;
+  const double *H = d.H0;
+  if (g < nD) {
+    const int I = (int)(g / nn), rem = (int)(g - I * nn), r = rem / n, cc = rem - r * n;
+    const int gr = I * n + r, gc = I * n + cc;
+    double v;
+    if (gr < vb && gc < vb) {
+      v = cc <= r ? H[gr * np + gc] : H[gc * np + gr];
+      if (r == cc) v += lambda;
+    } else {
+      v = r == cc ? 1.0 : 0.0;
+    }
+    c.D[g] = v;
+    const int gc2 = gc + n;
+    c.E[g] = (I + 1 < c.p && gr < vb && gc2 < vb) ? H[gc2 * np + gr] : 0.0;
+  } else if (g < nD + nG) {
+    const int64_t g2 = g - nD;
+    const int I = (int)(g2 / ((int64_t)n * R)), rem = (int)(g2 - (int64_t)I * n * R), r = rem / R, l = rem - r * R;
+    const int gr = I * n + r;
+    double v = 0.0;
+    if (gr < vb) {
+      if (l < c.nb) v = H[(b0 + l) * np + gr];
+      else if (l == c.nb) v = d.b[gr];
+    }
+    c.G[g2] = v;
+    c.Go[g2] = v;
+  } else if (g < nD + nG + nS) {
+    const int64_t g3 = g - nD - nG;
+    const int k = (int)(g3 / c.nc), l = (int)(g3 - (int64_t)k * c.nc);
+    double v;
+    if (k < c.nb && l < c.nb) {
+      v = l <= k ? H[(b0 + k) * np + b0 + l] : H[(b0 + l) * np + b0 + k];
+      if (k == l) v += lambda;
+    } else {
+      v = k == l ? 1.0 : 0.0;
+    }
+    c.Sc[g3] = v;
+    if (l == 0) c.rc[k] = k < c.nb ? d.b[b0 + k] : 0.0;
+  }
+}
+
+// S_c -= F Y, r_c -= F y from the per-block products P_I = Go_I^T X_I, summed
+// in block order (deterministic).
+__global__ __launch_bounds__(256) void k_egcr_schur(EGCR c) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= c.nb * (c.nb + 1)) return;
+  const int k = g / (c.nb + 1), l = g - k * (c.nb + 1);
+  double s = 0.0;
+  for (int I = 0; I < c.p; ++I) s += c.P[((size_t)I * c.R + k) * c.R + l];
+  if (l < c.nb) c.Sc[(size_t)k * c.nc + l] -= s;
+  else c.rc[k] -= s;
+}
+
+// x in the EG row layout: band rows y - Y x_c, border rows x_c, padding 0.
+__global__ __launch_bounds__(256) void k_egcr_final(EGDev d, EGCR c, double *x) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d.n_pad) return;
+  const int vb = 7 * d.band_slots, b0 = 7 * d.border0;
+  double v = 0.0;
+  if (j < vb) {
+    const double *Xr = c.X + (size_t)j * c.R;  // band row j = block j / n, row j % n
+    v = Xr[c.nb];
+    for (int l = 0; l < c.nb; ++l) v -= Xr[l] * c.xc[l];
+  } else if (j >= b0 && j < b0 + c.nb) {
+    v = c.xc[j - b0];
+  }
+  x[j] = v;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- host driver
@@ -450,8 +542,37 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
   d.jt = alloc<double>(161 * A_);
   const size_t nn = (size_t)n_pad * n_pad;
   d.H0 = alloc<double>(nn);
-  double *A = alloc<double>(nn), *L = alloc<double>(nn);
-  double *Linv = alloc<double>((size_t)(n_pad / kCRMaxN) * kCRMaxN * kCRMaxN);
+  // arrow layout: the band by cyclic reduction with the border columns as extra
+  // right-hand sides (EGCR) unless SQLM_EG_CR=0; else the arrow / dense Cholesky
+  const int nbr = 7 * nborder;
+  const char *cr_env = std::getenv("SQLM_EG_CR");
+  const bool use_cr = arrow && band_blk >= 1 && nbr + 1 <= 512 && !(cr_env && std::atoi(cr_env) == 0);
+  double *A = nullptr, *L = nullptr, *Linv = nullptr;
+  EGCR c;
+  if (use_cr) {
+    c.p = band_blk;
+    c.n = kCRMaxN;
+    c.nb = nbr;
+    c.R = (nbr + 1 + 15) / 16 * 16;
+    c.nc = nbr > 0 ? (nbr + kCRMaxN - 1) / kCRMaxN * kCRMaxN : kCRMaxN;
+    const size_t pnn = (size_t)c.p * c.n * c.n, pnr = (size_t)c.p * c.n * c.R, ncc = (size_t)c.nc * c.nc;
+    c.D = alloc<double>(pnn); c.E = alloc<double>(pnn); c.A = alloc<double>(pnn); c.Cm = alloc<double>(pnn);
+    c.gs = alloc<double>((size_t)c.p * c.n); c.xs = alloc<double>((size_t)c.p * c.n);
+    c.G = alloc<double>(pnr); c.Go = alloc<double>(pnr); c.Z = alloc<double>(pnr); c.X = alloc<double>(pnr);
+    c.P = alloc<double>((size_t)c.p * c.R * c.R);
+    c.Sc = alloc<double>(ncc); c.ScL = alloc<double>(ncc);
+    c.ScLinv = alloc<double>((size_t)(c.nc / kCRMaxN) * kCRMaxN * kCRMaxN);
+    c.rc = alloc<double>(c.nc); c.xc = alloc<double>(c.nc);
+    if (!c.D || !c.E || !c.A || !c.Cm || !c.gs || !c.xs || !c.G || !c.Go || !c.Z || !c.X || !c.P || !c.Sc || !c.ScL ||
+        !c.ScLinv || !c.rc || !c.xc)
+      return SQLM_ERR_OOM;
+    // the scratch right-hand side of the reused single-RHS kernels: finite values
+    if (hipMemsetAsync(c.gs, 0, sizeof(double) * c.p * c.n, st) != hipSuccess) return SQLM_ERR_HIP;
+  } else {
+    A = alloc<double>(nn);
+    L = alloc<double>(nn);
+    Linv = alloc<double>((size_t)(n_pad / kCRMaxN) * kCRMaxN * kCRMaxN);
+  }
   d.b = alloc<double>(n_pad);
   double *r = alloc<double>(n_pad), *x = alloc<double>(n_pad);
   int *d_dst = upload(dst), *d_sptr = upload(sptr), *d_src = upload(src);
@@ -459,7 +580,7 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
   d.scalars = alloc<double>(8);
   int *flags = alloc<int>(4);
   if (!d_act || !d_ei || !d_ej || !d_hid || !d_C || (!info.empty() && !d_info) || !Sd[0] || !Sd[1] || !d.err ||
-      !d.jt || !d.H0 || !A || !L || !Linv || !d.b || !r || !x || !d_dst || !d_sptr || !d_src || !d.partials ||
+      !d.jt || !d.H0 || (!use_cr && (!A || !L || !Linv)) || !d.b || !r || !x || !d_dst || !d_sptr || !d_src || !d.partials ||
       !d.scalars || !flags)
     return SQLM_ERR_OOM;
   d.act = d_act; d.ei = d_ei; d.ej = d_ej; d.hid = d_hid; d.C = d_C; d.info = d_info;
@@ -496,10 +617,23 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
     int qmax = 0;
     do {
       if (hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(flags), 1, 1, st) != hipSuccess) return SQLM_ERR_HIP;
-      hipLaunchKernelGGL(k_eg_damp, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, st, d, A, lambda);
-      if (hipMemcpyAsync(r, d.b, sizeof(double) * n_pad, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return SQLM_ERR_HIP;
-      if (launch_dense_spd_solve(A, L, Linv, r, x, flags, n_pad, st, arrow ? band_blk : 0)) return SQLM_ERR_HIP;
+      if (use_cr) {
+        const int64_t tot = (int64_t)c.p * c.n * c.n + (int64_t)c.p * c.n * c.R + (int64_t)c.nc * c.nc;
+        hipLaunchKernelGGL(k_egcr_gather, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, d, c, lambda);
+        if (launch_cr_multi(c.D, c.E, c.A, c.Cm, c.gs, c.xs, c.G, c.Z, c.X, flags, c.p, c.n, c.R, st))
+          return SQLM_ERR_HIP;
+        if (c.nb > 0) {
+          if (launch_batched_atb(c.Go, c.X, c.P, c.p, c.n, c.R, st)) return SQLM_ERR_HIP;
+          hipLaunchKernelGGL(k_egcr_schur, dim3((c.nb * (c.nb + 1) + 255) / 256), dim3(256), 0, st, c);
+          if (launch_dense_spd_solve(c.Sc, c.ScL, c.ScLinv, c.rc, c.xc, flags, c.nc, st, 0)) return SQLM_ERR_HIP;
+        }
+        hipLaunchKernelGGL(k_egcr_final, dim3((n_pad + 255) / 256), dim3(256), 0, st, d, c, x);
+      } else {
+        hipLaunchKernelGGL(k_eg_damp, dim3((unsigned)((nn + 255) / 256)), dim3(256), 0, st, d, A, lambda);
+        if (hipMemcpyAsync(r, d.b, sizeof(double) * n_pad, hipMemcpyDeviceToDevice, st) != hipSuccess)
+          return SQLM_ERR_HIP;
+        if (launch_dense_spd_solve(A, L, Linv, r, x, flags, n_pad, st, arrow ? band_blk : 0)) return SQLM_ERR_HIP;
+      }
       hipLaunchKernelGGL(k_eg_update, dim3((nK + 255) / 256), dim3(256), 0, st, d, Sd[0], Sd[1], x);
       hipLaunchKernelGGL(k_eg_errors, dim3(eb), dim3(kEGBlock), 0, st, d, Sd[1], 1);
       hipLaunchKernelGGL(k_eg_scale, dim3(sb), dim3(kEGBlock), 0, st, d, x, lambda);

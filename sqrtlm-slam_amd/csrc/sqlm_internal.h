@@ -200,6 +200,15 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
 // touched (band = 0: fully dense).
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
                            hipStream_t st, int band = 0);
+// Block-tridiagonal SPD solve with R right-hand sides by cyclic reduction:
+// D / E [p][n][n] (D_I lower, E_I = S(I, I+1)), G [p][n][R] right-hand sides
+// (overwritten), X [p][n][R] solution; A, C, Z scratch of the same shapes, gs /
+// xs [p][n] scratch. n <= kCRMaxN, n and R multiples of 16. flags[0] = 0 if a
+// pivot is not positive.
+int launch_cr_multi(double *D, double *E, double *A, double *C, double *gs, double *xs, double *G, double *Z,
+                    double *X, int *flags, int p, int n, int R, hipStream_t st);
+// P_I = A_I^T B_I for I < p, A_I / B_I [n][R] row-major, P_I [R][R] (R % 16 == 0).
+int launch_batched_atb(const double *A, const double *B, double *P, int p, int n, int R, hipStream_t st);
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st,
                             bool spec = false);

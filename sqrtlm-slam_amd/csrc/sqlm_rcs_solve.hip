@@ -405,10 +405,9 @@ __device__ __forceinline__ void cr_factor_block(const CRView &v, int I, double *
 
 // Level h, step 1: every odd superblock I (I = h, 3h, 5h, ...) is factored:
 // D_I <- Linv_I = chol(D_I)^-1 (lower block triangle, zero above), g_I <- z_I = Linv_I g_I.
-__global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  __shared__ int fail;
-  const int I = h + 2 * h * blockIdx.x, n = v.n, ld = n + 1, nt = n >> 4;
+__device__ __forceinline__ void cr_factor_store(const CRView &v, int I, double *lds, int *fail_p) {
+  int &fail = *fail_p;
+  const int n = v.n, ld = n + 1, nt = n >> 4;
   const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
   cr_factor_block(v, I, lds, &fail);
   const double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n;
@@ -430,6 +429,12 @@ __global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
     const double s = linv_gemv(L, ld, Dinv, tmp, wave);
     if (k4 == 0) v.g[(size_t)I * n + 16 * wave + r16] = s;
   }
+}
+
+__global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int fail;
+  cr_factor_store(v, h + 2 * h * blockIdx.x, lds, &fail);
 }
 
 // One wavefront computes one 16x16 tile acc = op(A) op(B) over K = n,
@@ -951,6 +956,153 @@ int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double
       hipLaunchKernelGGL(k_dtrsv_bwd_update, dim3(((k - c0) * nb + 255) / 256), dim3(256), 0, st, v, k, c0);
   }
   return 0;
+}
+
+// ---- block-tridiagonal solve with many right-hand sides (essential graph) ----
+// The elimination of launch_cr_core (k_cr_factor, k_cr_elim_gemm,
+// k_cr_update_gemm on D / E; their single right-hand side runs on a scratch
+// vector), with R right-hand sides G [p][n][R] carried by MFMA tile GEMMs
+// (one wavefront per 16x16 tile):
+//   odd I at level h:  Z_I = Linv_I G_I
+//   even J:            G_J -= A_{J+h}^T Z_{J+h} + C_{J-h}^T Z_{J-h}
+//   top (block 0):     X_0 = Linv_0^T (Linv_0 G_0)
+//   back, odd I:       X_I = Linv_I^T (Z_I - A_I X_{I-h} - C_I X_{I+h}).
+struct CRMView {
+  int p, n, R;
+  const double *D, *A, *C;  // D_I = Linv_I (lower) once block I is factored
+  double *G, *Z, *X;        // [p][n][R]
+};
+
+// acc = op(A)[16 ti .. +16][k0 .. k1) B[k0 .. k1)[16 tj .. +16] (row-major;
+// op(A) = A or A^T), k1 - k0 <= kCRMaxN; every operand load is issued before
+// the first MFMA (clamped index, zero weight past k1).
+template <bool TA>
+__device__ __forceinline__ d4 mm_tile(const double *A, int lda, const double *B, int ldb, int ti, int tj, int k0,
+                                      int k1) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+  const int ar = 16 * ti + r16, bc = 16 * tj + r16;
+  constexpr int S = kCRMaxN / 4;
+  double a[S], b[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int k = k0 + 4 * s + k4, kc = k < k1 ? k : k1 - 1;
+    a[s] = TA ? A[(size_t)kc * lda + ar] : A[(size_t)ar * lda + kc];
+    b[s] = k < k1 ? B[(size_t)kc * ldb + bc] : 0.0;
+  }
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (k0 + 4 * s < k1) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ void mm_store(double *C, int ldc, int ti, int tj, const d4 &acc, double alpha, bool add) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double *c = C + (size_t)(16 * ti + k4 + 4 * j) * ldc + 16 * tj + r16;
+    *c = add ? *c + alpha * acc[j] : alpha * acc[j];
+  }
+}
+
+// Z_I = Linv_I G_I for I = I0 + stride q (Linv lower: K up to the tile row)
+__global__ __launch_bounds__(64) void k_crm_fwd(CRMView v, int I0, int stride, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int nt = v.n >> 4, rt = v.R >> 4, per = nt * rt;
+  const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, I = I0 + stride * q;
+  const size_t nn = (size_t)v.n * v.n, nr = (size_t)v.n * v.R;
+  const d4 acc = mm_tile<false>(v.D + I * nn, v.n, v.G + I * nr, v.R, ti, tj, 0, 16 * (ti + 1));
+  mm_store(v.Z + I * nr, v.R, ti, tj, acc, 1.0, false);
+}
+
+// even J = 2 h q: G_J -= A_{J+h}^T Z_{J+h} + C_{J-h}^T Z_{J-h}
+__global__ __launch_bounds__(64) void k_crm_upd(CRMView v, int h, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int n = v.n, nt = n >> 4, rt = v.R >> 4, per = nt * rt;
+  const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, J = 2 * h * q;
+  const size_t nn = (size_t)n * n, nr = (size_t)n * v.R;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  const bool right = J + h < v.p, left = J >= h;
+  if (right) acc = mm_tile<true>(v.A + (J + h) * nn, n, v.Z + (J + h) * nr, v.R, ti, tj, 0, n);
+  if (left) acc += mm_tile<true>(v.C + (J - h) * nn, n, v.Z + (J - h) * nr, v.R, ti, tj, 0, n);
+  if (right || left) mm_store(v.G + J * nr, v.R, ti, tj, acc, -1.0, true);
+}
+
+// odd I = h + 2 h q: Z_I -= A_I X_{I-h} + C_I X_{I+h} (in place, tile by tile)
+__global__ __launch_bounds__(64) void k_crm_back_rhs(CRMView v, int h, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int n = v.n, nt = n >> 4, rt = v.R >> 4, per = nt * rt;
+  const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, I = h + 2 * h * q;
+  const size_t nn = (size_t)n * n, nr = (size_t)n * v.R;
+  d4 acc = mm_tile<false>(v.A + I * nn, n, v.X + (I - h) * nr, v.R, ti, tj, 0, n);
+  if (I + h < v.p) acc += mm_tile<false>(v.C + I * nn, n, v.X + (I + h) * nr, v.R, ti, tj, 0, n);
+  mm_store(v.Z + I * nr, v.R, ti, tj, acc, -1.0, true);
+}
+
+// X_I = Linv_I^T Z_I for I = I0 + stride q (Linv^T upper: K from the tile row)
+__global__ __launch_bounds__(64) void k_crm_bwd(CRMView v, int I0, int stride, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int nt = v.n >> 4, rt = v.R >> 4, per = nt * rt;
+  const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, I = I0 + stride * q;
+  const size_t nn = (size_t)v.n * v.n, nr = (size_t)v.n * v.R;
+  const d4 acc = mm_tile<true>(v.D + I * nn, v.n, v.Z + I * nr, v.R, ti, tj, 16 * ti, v.n);
+  mm_store(v.X + I * nr, v.R, ti, tj, acc, 1.0, false);
+}
+
+// P_I = A_I^T B_I for p blocks of [n][R] (R x R results, one tile per wavefront)
+__global__ __launch_bounds__(64) void k_batched_atb(const double *A, const double *B, double *P, int n, int R,
+                                                    int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int rt = R >> 4, per = rt * rt, I = lb / per, t = lb - I * per, ti = t / rt, tj = t - ti * rt;
+  const size_t nr = (size_t)n * R;
+  const d4 acc = mm_tile<true>(A + I * nr, R, B + I * nr, R, ti, tj, 0, n);
+  mm_store(P + (size_t)I * R * R, R, ti, tj, acc, 1.0, false);
+}
+
+int launch_batched_atb(const double *A, const double *B, double *P, int p, int n, int R, hipStream_t st) {
+  if (p <= 0 || n % 4 || R % 16) return -1;
+  const int total = p * (R / 16) * (R / 16);
+  hipLaunchKernelGGL(k_batched_atb, dim3(xcd_grid(total)), dim3(64), 0, st, A, B, P, n, R, total);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+__global__ __launch_bounds__(512) void k_cr_factor_at(CRView v, int I) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int fail;
+  cr_factor_store(v, I, lds, &fail);
+}
+
+int launch_cr_multi(double *D, double *E, double *A, double *C, double *gs, double *xs, double *G, double *Z,
+                    double *X, int *flags, int p, int n, int R, hipStream_t st) {
+  if (p <= 0 || n % 16 || n > kCRMaxN || R <= 0 || R % 16) return -1;
+  CRView v{p, n, 0, 0, D, E, A, C, gs, xs, flags};
+  CRMView m{p, n, R, D, A, C, G, Z, X};
+  const size_t lds = cr_factor_lds(n);
+  const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt, rhs = nt * (R / 16);
+  int h = 1;
+  for (; h < p; h *= 2) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
+    const int n_even = (p + 2 * h - 1) / (2 * h);
+    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
+    hipLaunchKernelGGL(k_crm_fwd, dim3(xcd_grid(n_odd * rhs)), dim3(64), 0, st, m, h, 2 * h, n_odd * rhs);
+    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
+    hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
+    hipLaunchKernelGGL(k_crm_upd, dim3(xcd_grid(n_even * rhs)), dim3(64), 0, st, m, h, n_even * rhs);
+  }
+  hipLaunchKernelGGL(k_cr_factor_at, dim3(1), dim3(512), lds, st, v, 0);
+  hipLaunchKernelGGL(k_crm_fwd, dim3(xcd_grid(rhs)), dim3(64), 0, st, m, 0, 1, rhs);
+  hipLaunchKernelGGL(k_crm_bwd, dim3(xcd_grid(rhs)), dim3(64), 0, st, m, 0, 1, rhs);
+  for (h /= 2; h >= 1; h /= 2) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
+    hipLaunchKernelGGL(k_crm_back_rhs, dim3(xcd_grid(n_odd * rhs)), dim3(64), 0, st, m, h, n_odd * rhs);
+    hipLaunchKernelGGL(k_crm_bwd, dim3(xcd_grid(n_odd * rhs)), dim3(64), 0, st, m, h, 2 * h, n_odd * rhs);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 __global__ void k_cr_gather(DevProblem d, CRView v) {

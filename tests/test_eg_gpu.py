@@ -105,6 +105,47 @@ def test_eg_layouts_match(gpu_ctx, oracle, monkeypatch, dense):
     assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-9
 
 
+def _eg_solve_once(gpu_ctx, pg, iters, env, monkeypatch):
+    for k in ("SQLM_EG_CR", "SQLM_EG_DENSE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    gpu_ctx.eg_set_problem(pg)
+    n, st = gpu_ctx.eg_optimize(iters, 1e-16)
+    return st, gpu_ctx.eg_poses().copy()
+
+
+@pytest.mark.parametrize("n_kf,n_loops", [(12, 0), (300, 0), (500, 12), (1500, 20)])
+def test_eg_cyclic_reduction_matches(gpu_ctx, oracle, monkeypatch, n_kf, n_loops):
+    """Block-arrow band by cyclic reduction with the border columns as extra
+    right-hand sides (the default) against the arrow Cholesky (SQLM_EG_CR=0)
+    and the oracle: one band block (12 KF), no border (0 loops), borders of
+    ~12 and ~20 vertices. First step within 1e-9 of the Cholesky (a different
+    elimination order of the same SPD system) and within the north-star 1e-6
+    of the oracle; chi2 within 1e-8."""
+    pg = synth.make_pose_graph(n_kf, window=6, n_loops=n_loops, seed=9, fix_scale=True, rot_noise=3e-4,
+                               trans_noise=5e-4)
+    ref = oracle.OracleEG(pg)
+    nr, sr = ref.optimize(1, 1e-16)
+    s_cr, p_cr = _eg_solve_once(gpu_ctx, pg, 1, {}, monkeypatch)
+    s_ch, p_ch = _eg_solve_once(gpu_ctx, pg, 1, {"SQLM_EG_CR": "0"}, monkeypatch)
+    assert s_cr["trace_trials"] == sr["trace_trials"]
+    assert abs(s_cr["chi2_end"] - sr["chi2_end"]) <= 1e-8 * sr["chi2_begin"]
+    assert _rel(p_cr, p_ch) < 1e-9
+    assert _rel(p_cr, ref.Siw) < 1e-6
+
+
+def test_eg_cyclic_reduction_converges(gpu_ctx, oracle, monkeypatch):
+    """20 iterations on a noise-free graph with loop edges: the same optimum as
+    the oracle within 1e-9 (the CR path end to end, trials included)."""
+    pg = synth.make_pose_graph(500, window=6, n_loops=12, seed=7, noise=False, fix_scale=True)
+    ref = oracle.OracleEG(pg)
+    ref.optimize(20, 1e-16)
+    st, poses = _eg_solve_once(gpu_ctx, pg, 20, {}, monkeypatch)
+    assert st["chi2_end"] < 1e-18
+    assert _rel(poses, ref.Siw) < 1e-9
+
+
 def test_eg_bench_size_first_iteration(gpu_ctx, oracle, monkeypatch):
     """The bench graph itself (1500 keyframes, 20 loop edges, block-arrow
     layout with a border): the first LM iteration (lambda 1e-16, i.e. a
