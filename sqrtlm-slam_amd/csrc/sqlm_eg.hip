@@ -45,7 +45,12 @@ struct EGDev {
   const double *info = nullptr;         // [nE][49] or null (identity)
   double *err = nullptr;                // [nE][7]
   double *jt = nullptr;                 // [nE][161]: Hii Hjj Hij (49 each), bi bj (7 each)
-  double *H0 = nullptr;                 // [n_pad][n_pad] assembled (lower)
+  double *H0 = nullptr;                 // [n_pad][n_pad] assembled (lower); dense / arrow-Cholesky path
+  // cyclic-reduction path: the assembled lower system straight in block form
+  // (no dense buffer): D0 [p][112][112] diagonal band blocks, E0 [p][112][112]
+  // block (I+1, I), F0 [nb][112 p] border rows x band columns, B0 [nb][nb]
+  int cr = 0, cr_p = 0, cr_nb = 0;
+  double *D0 = nullptr, *E0 = nullptr, *F0 = nullptr, *B0 = nullptr;
   double *b = nullptr;                  // [n_pad]
   const int *dst = nullptr;             // [nD] destination: block row << 16 | block col, or -(v+1) for b_v
   const int *src_ptr = nullptr;         // [nD+1]
@@ -56,6 +61,20 @@ struct EGDev {
 
 __device__ __forceinline__ bool row_valid(const EGDev &d, int r) {
   return r < 7 * d.band_slots || (r >= 7 * d.border0 && r < 7 * (d.border0 + d.border_slots));
+}
+
+// Entry (R, C), R >= C block-wise (the assembled lower part), of the system.
+__device__ __forceinline__ double *h0_at(const EGDev &d, int R, int C) {
+  if (!d.cr) return d.H0 + (size_t)R * d.n_pad + C;
+  constexpr int n = kCRMaxN;
+  const int vb = 7 * d.band_slots, b0 = 7 * d.border0;
+  if (R < vb) {  // band row, band column in the same or the previous block
+    const int I = R / n, J = C / n;
+    double *blk = (I == J ? d.D0 + (size_t)I * n * n : d.E0 + (size_t)J * n * n);
+    return blk + (size_t)(R - I * n) * n + (C - J * n);
+  }
+  const int k = R - b0;
+  return C < vb ? d.F0 + (size_t)k * d.cr_p * n + C : d.B0 + (size_t)k * d.cr_nb + (C - b0);
 }
 
 __device__ __forceinline__ double info_at(const EGDev &d, int64_t k, int r, int c) {
@@ -205,7 +224,7 @@ __global__ __launch_bounds__(64) void k_eg_assemble(EGDev d, int nD) {
       const double *blk = d.jt + 161 * (int64_t)(s >> 2);
       v += kind == 0 ? blk[lane] : kind == 1 ? blk[49 + lane] : kind == 2 ? blk[98 + lane] : blk[98 + 7 * c + r];
     }
-    d.H0[(size_t)(7 * br + r) * d.n_pad + 7 * bc + c] = v;
+    *h0_at(d, 7 * br + r, 7 * bc + c) = v;
   } else {
     if (lane >= 7) return;
     const int hv = -dst - 1;
@@ -236,7 +255,7 @@ __global__ __launch_bounds__(256) void k_eg_maxdiag(EGDev d) {
   __shared__ double red[4];
   double m = 0.0;
   for (int j = threadIdx.x; j < d.n_pad; j += blockDim.x)
-    if (row_valid(d, j)) m = fmax(m, fabs(d.H0[(size_t)j * d.n_pad + j]));
+    if (row_valid(d, j)) m = fmax(m, fabs(*h0_at(d, j, j)));
 #pragma unroll
   for (int s = 32; s >= 1; s >>= 1) m = fmax(m, __shfl_xor(m, s, 64));
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
@@ -304,30 +323,30 @@ struct EGCR {
 __global__ __launch_bounds__(256) void k_egcr_gather(EGDev d, EGCR c, double lambda) {
   const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int n = c.n, R = c.R;
-  const int64_t np = d.n_pad, nn = (int64_t)n * n, nD = (int64_t)c.p * nn, nG = (int64_t)c.p * n * R;
+  const int64_t nn = (int64_t)n * n, nD = (int64_t)c.p * nn, nG = (int64_t)c.p * n * R;
   const int64_t nS = (int64_t)c.nc * c.nc;
   const int vb = 7 * d.band_slots, b0 = 7 * d.border0;
-  const double *H = d.H0;
   if (g < nD) {
     const int I = (int)(g / nn), rem = (int)(g - I * nn), r = rem / n, cc = rem - r * n;
     const int gr = I * n + r, gc = I * n + cc;
+    const double *D0 = d.D0 + I * nn;
     double v;
     if (gr < vb && gc < vb) {
-      v = cc <= r ? H[gr * np + gc] : H[gc * np + gr];
+      v = cc <= r ? D0[r * n + cc] : D0[cc * n + r];
       if (r == cc) v += lambda;
     } else {
       v = r == cc ? 1.0 : 0.0;
     }
     c.D[g] = v;
-    const int gc2 = gc + n;
-    c.E[g] = (I + 1 < c.p && gr < vb && gc2 < vb) ? H[gc2 * np + gr] : 0.0;
+    // E_I(r, cc) = S(I n + r, (I+1) n + cc), assembled as block (I+1, I) entry (cc, r)
+    c.E[g] = (I + 1 < c.p && gr < vb && gc + n < vb) ? d.E0[I * nn + (int64_t)cc * n + r] : 0.0;
   } else if (g < nD + nG) {
     const int64_t g2 = g - nD;
     const int I = (int)(g2 / ((int64_t)n * R)), rem = (int)(g2 - (int64_t)I * n * R), r = rem / R, l = rem - r * R;
     const int gr = I * n + r;
     double v = 0.0;
     if (gr < vb) {
-      if (l < c.nb) v = H[(b0 + l) * np + gr];
+      if (l < c.nb) v = d.F0[(size_t)l * c.p * n + gr];
       else if (l == c.nb) v = d.b[gr];
     }
     c.G[g2] = v;
@@ -337,7 +356,7 @@ __global__ __launch_bounds__(256) void k_egcr_gather(EGDev d, EGCR c, double lam
     const int k = (int)(g3 / c.nc), l = (int)(g3 - (int64_t)k * c.nc);
     double v;
     if (k < c.nb && l < c.nb) {
-      v = l <= k ? H[(b0 + k) * np + b0 + l] : H[(b0 + l) * np + b0 + k];
+      v = l <= k ? d.B0[(size_t)k * c.nb + l] : d.B0[(size_t)l * c.nb + k];
       if (k == l) v += lambda;
     } else {
       v = k == l ? 1.0 : 0.0;
@@ -541,7 +560,6 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
   d.err = alloc<double>(7 * A_);
   d.jt = alloc<double>(161 * A_);
   const size_t nn = (size_t)n_pad * n_pad;
-  d.H0 = alloc<double>(nn);
   // arrow layout: the band by cyclic reduction with the border columns as extra
   // right-hand sides (EGCR) unless SQLM_EG_CR=0; else the arrow / dense Cholesky
   const int nbr = 7 * nborder;
@@ -549,6 +567,17 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
   const bool use_cr = arrow && band_blk >= 1 && nbr + 1 <= 512 && !(cr_env && std::atoi(cr_env) == 0);
   double *A = nullptr, *L = nullptr, *Linv = nullptr;
   EGCR c;
+  size_t asm_n = nn;  // doubles of the assembly buffer (cleared every iteration)
+  if (use_cr) {
+    const size_t pnn = (size_t)band_blk * kCRMaxN * kCRMaxN;
+    asm_n = 2 * pnn + (size_t)nbr * band_blk * kCRMaxN + (size_t)nbr * nbr;
+    d.H0 = alloc<double>(asm_n);
+    if (!d.H0) return SQLM_ERR_OOM;
+    d.cr = 1; d.cr_p = band_blk; d.cr_nb = nbr;
+    d.D0 = d.H0; d.E0 = d.D0 + pnn; d.F0 = d.E0 + pnn; d.B0 = d.F0 + (size_t)nbr * band_blk * kCRMaxN;
+  } else {
+    d.H0 = alloc<double>(nn);
+  }
   if (use_cr) {
     c.p = band_blk;
     c.n = kCRMaxN;
@@ -601,7 +630,7 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
     hipLaunchKernelGGL(k_eg_errors, dim3(eb), dim3(kEGBlock), 0, st, d, Sd[0], 0);
     hipLaunchKernelGGL(k_eg_reduce, dim3(1), dim3(256), 0, st, d, eb, 0, 1, (const int *)nullptr);
     hipLaunchKernelGGL(k_eg_linearize, dim3((unsigned)((A_ + 3) / 4)), dim3(256), 0, st, d, Sd[0]);
-    if (hipMemsetAsync(d.H0, 0, nn * sizeof(double), st) != hipSuccess) return SQLM_ERR_HIP;
+    if (hipMemsetAsync(d.H0, 0, asm_n * sizeof(double), st) != hipSuccess) return SQLM_ERR_HIP;
     hipLaunchKernelGGL(k_eg_assemble, dim3(nD), dim3(64), 0, st, d, nD);
     if (it == 0) hipLaunchKernelGGL(k_eg_maxdiag, dim3(1), dim3(256), 0, st, d);
     if (fetch()) return SQLM_ERR_HIP;
