@@ -164,43 +164,101 @@ struct TilePlan {
   bool dups = false;
 };
 
+// fn(t) for t = 0 .. nth-1 on nth host threads (t = 0 on the caller's)
+template <class F>
+void run_threads(int nth, F &&fn) {
+  std::vector<std::thread> th;
+  for (int t = 1; t < nth; ++t) th.emplace_back(fn, t);
+  fn(0);
+  for (auto &t : th) t.join();
+}
+
+inline int host_threads() { return std::max(1, std::min(16, (int)std::thread::hardware_concurrency())); }
+
 void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::vector<int> &obs_camh,
                  const std::vector<int> &s_row, const std::vector<int> &s_col, int lm_cap, TilePlan &tp) {
   const int64_t nE = lm_begin[nL];
   tp.obs_local.assign(nE, -1);
   tp.urange.assign(nL, int2{-1, -1});
-  std::vector<int> stamp(nP, -1), lidx(nP, -1), lmst(nP, -1), cur, lcams;
-  std::vector<uint8_t> pst;
-  struct Red { int key, tile, code; };
-  std::vector<Red> red, gred;
-  int t = 0, cur_lm = 0, tile_start = 0;
-  auto close_tile = [&](int s_end) {
-    std::sort(cur.begin(), cur.end());
-    const int cp = (int)cur.size();
-    for (int u = 0; u < cp; ++u) lidx[cur[u]] = u;
-    pst.assign((size_t)cp * cp, 0);
-    for (int sl = tile_start; sl < s_end; ++sl) {
-      lcams.clear();
+  // pass 1 (sequential, greedy): tile boundaries — a tile closes before the
+  // landmark that would push its window past kTileMaxCams cameras or lm_cap
+  std::vector<int> tstart{0};
+  {
+    std::vector<int> stamp(nP, -1), lmst(nP, -1);
+    int t = 0, ncur = 0, cur_lm = 0;
+    for (int sl = 0; sl < nL; ++sl) {
+      int nnew = 0;
       for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
         const int h = obs_camh[o];
-        tp.obs_local[o] = h >= 0 ? lidx[h] : -1;
-        if (h >= 0) lcams.push_back(lidx[h]);
+        if (h < 0) continue;
+        if (lmst[h] == sl) { tp.dups = true; continue; }
+        lmst[h] = sl;
+        if (stamp[h] != t) ++nnew;
       }
-      if (lcams.empty()) continue;
-      std::sort(lcams.begin(), lcams.end());
-      lcams.erase(std::unique(lcams.begin(), lcams.end()), lcams.end());
-      tp.urange[sl] = int2{lcams.front(), lcams.back()};
-      for (size_t a = 0; a < lcams.size(); ++a)
-        for (size_t b = a; b < lcams.size(); ++b) pst[(size_t)lcams[a] * cp + lcams[b]] = 1;
+      if (cur_lm > 0 && (ncur + nnew > kTileMaxCams || cur_lm >= lm_cap)) {
+        tstart.push_back(sl);
+        ++t;
+        ncur = 0;
+        cur_lm = 0;
+      }
+      for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+        const int h = obs_camh[o];
+        if (h >= 0 && stamp[h] != t) { stamp[h] = t; ++ncur; }
+      }
+      ++cur_lm;
     }
-    for (int u = 0; u < cp; ++u)
-      for (int v = u; v < cp; ++v) {
-        if (!pst[(size_t)u * cp + v]) continue;
-        const int i = cur[u], j = cur[v];
-        const int *b0 = s_col.data() + s_row[i], *b1 = s_col.data() + s_row[i + 1];
-        const int sidx = (int)(std::lower_bound(b0, b1, j) - s_col.data());
-        red.push_back({sidx, t, tile_blk(u, v, cp)});
+    if (cur_lm > 0) tstart.push_back(nL);
+  }
+  const int nt = (int)tstart.size() - 1;
+  // pass 2 (tiles on host threads): window cameras, local camera of every
+  // observation, landmark spans, and the S blocks each tile contributes to
+  struct Red { int key, tile, code; };
+  struct TileOut { std::vector<int> cams; std::vector<Red> red; };
+  std::vector<TileOut> out(nt);
+  const int nth = host_threads();
+  run_threads(nth, [&](int th) {
+    std::vector<int> lidx(nP, -1), lcams;
+    std::vector<uint8_t> pst;
+    for (int t = th; t < nt; t += nth) {
+      std::vector<int> &cur = out[t].cams;
+      for (int o = lm_begin[tstart[t]]; o < lm_begin[tstart[t + 1]]; ++o)
+        if (obs_camh[o] >= 0) cur.push_back(obs_camh[o]);
+      std::sort(cur.begin(), cur.end());
+      cur.erase(std::unique(cur.begin(), cur.end()), cur.end());
+      const int cp = (int)cur.size();
+      for (int u = 0; u < cp; ++u) lidx[cur[u]] = u;
+      pst.assign((size_t)cp * cp, 0);
+      for (int sl = tstart[t]; sl < tstart[t + 1]; ++sl) {
+        lcams.clear();
+        for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+          const int h = obs_camh[o];
+          tp.obs_local[o] = h >= 0 ? lidx[h] : -1;
+          if (h >= 0) lcams.push_back(lidx[h]);
+        }
+        if (lcams.empty()) continue;
+        std::sort(lcams.begin(), lcams.end());
+        lcams.erase(std::unique(lcams.begin(), lcams.end()), lcams.end());
+        tp.urange[sl] = int2{lcams.front(), lcams.back()};
+        for (size_t a = 0; a < lcams.size(); ++a)
+          for (size_t b = a; b < lcams.size(); ++b) pst[(size_t)lcams[a] * cp + lcams[b]] = 1;
       }
+      for (int u = 0; u < cp; ++u)
+        for (int v = u; v < cp; ++v) {
+          if (!pst[(size_t)u * cp + v]) continue;
+          const int i = cur[u], j = cur[v];
+          const int *b0 = s_col.data() + s_row[i], *b1 = s_col.data() + s_row[i + 1];
+          const int sidx = (int)(std::lower_bound(b0, b1, j) - s_col.data());
+          out[t].red.push_back({sidx, t, tile_blk(u, v, cp)});
+        }
+      for (int u = 0; u < cp; ++u) lidx[cur[u]] = -1;
+    }
+  });
+  // pass 3 (tile order): offsets, camera lists, the reduction lists
+  std::vector<Red> red, gred;
+  for (int t = 0; t < nt; ++t) {
+    const std::vector<int> &cur = out[t].cams;
+    const int cp = (int)cur.size();
+    red.insert(red.end(), out[t].red.begin(), out[t].red.end());
     for (int u = 0; u < cp; ++u) gred.push_back({cur[u], t, u});
     const int ld = (6 * cp + 15) / 16 * 16;
     tp.ld.push_back(ld);
@@ -208,30 +266,9 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
     tp.gpart_ptr.push_back(tp.gpart_ptr.back() + ld);
     tp.cams.insert(tp.cams.end(), cur.begin(), cur.end());
     tp.cam_ptr.push_back(tp.cam_ptr.back() + cp);
-    tp.lm_ptr.push_back(s_end);
+    tp.lm_ptr.push_back(tstart[t + 1]);
     tp.max_cp = std::max(tp.max_cp, cp);
-    ++t;
-    cur.clear();
-    cur_lm = 0;
-    tile_start = s_end;
-  };
-  for (int sl = 0; sl < nL; ++sl) {
-    int nnew = 0;
-    for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
-      const int h = obs_camh[o];
-      if (h < 0) continue;
-      if (lmst[h] == sl) { tp.dups = true; continue; }
-      lmst[h] = sl;
-      if (stamp[h] != t) ++nnew;
-    }
-    if (cur_lm > 0 && ((int)cur.size() + nnew > kTileMaxCams || cur_lm >= lm_cap)) close_tile(sl);
-    for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
-      const int h = obs_camh[o];
-      if (h >= 0 && stamp[h] != t) { stamp[h] = t; cur.push_back(h); }
-    }
-    ++cur_lm;
   }
-  if (cur_lm > 0) close_tile(nL);
   auto csr = [](const std::vector<Red> &v, int nkeys, std::vector<int> &ptr, std::vector<int2> &idx) {
     ptr.assign(nkeys + 1, 0);
     for (auto &r : v) ptr[r.key + 1]++;
@@ -350,34 +387,72 @@ int prepare(sqlm_ctx *c, int level) {
   for (int s = 0; s < nL; ++s) lm_begin[s + 1] = lm_begin[s] + kcount[pts[s]];
   const int64_t nE = lm_begin[nL];
   if (nE > (int64_t)std::numeric_limits<int>::max()) return SQLM_ERR_UNSUPPORTED;
-  std::vector<int> fill(lm_begin.begin(), lm_begin.end() - 1);
   c->dev_edge.assign(nE, 0);
   std::vector<int> obs_lm(nE), obs_cam(nE), obs_camh(nE);
   std::vector<double> obs_uv(2 * nE), obs_info(nE), obs_delta(nE), obs_ur(c->has_stereo ? nE : 0);
-  for (int64_t e = 0; e < c->n_obs; ++e) {
-    if (c->obs_level[e] != level) continue;
-    const int s = pt_slot[c->obs_pt[e]];
-    const int o = fill[s]++;
-    c->dev_edge[o] = e;
-    obs_lm[o] = s;
-    obs_cam[o] = c->obs_pose[e];
-    obs_camh[o] = phidx[c->obs_pose[e]];
-    obs_uv[2 * o] = c->obs_uv[2 * e];
-    obs_uv[2 * o + 1] = c->obs_uv[2 * e + 1];
-    obs_info[o] = c->obs_info[e];
-    obs_delta[o] = c->obs_delta[e];
-    if (c->has_stereo) obs_ur[o] = c->obs_ur[e];
-  }
-  // camera CSR (device obs in slot order)
-  std::vector<int> cam_ptr(nP + 1, 0), cam_obs;
-  for (int64_t o = 0; o < nE; ++o)
-    if (obs_camh[o] >= 0) cam_ptr[obs_camh[o] + 1]++;
-  for (int i = 0; i < nP; ++i) cam_ptr[i + 1] += cam_ptr[i];
-  cam_obs.resize(cam_ptr[nP]);
+  // Stable scatter of the observations into slot order on a few host threads:
+  // chunk t of the edge range counts its edges per slot, the per-(chunk, slot)
+  // bases follow by a prefix over chunks (edge-id order inside a landmark is
+  // kept), then every chunk scatters its edges; the camera CSR likewise.
+  const int nth = host_threads();
+  auto par = [&](auto &&fn) { run_threads(nth, fn); };
   {
-    std::vector<int> f(cam_ptr.begin(), cam_ptr.end() - 1);
-    for (int64_t o = 0; o < nE; ++o)
-      if (obs_camh[o] >= 0) cam_obs[f[obs_camh[o]]++] = (int)o;
+    auto ebeg = [&](int t) { return c->n_obs * t / nth; };
+    std::vector<std::vector<int>> base(nth);
+    par([&](int t) {
+      std::vector<int> &cnt = base[t];
+      cnt.assign(nL, 0);
+      for (int64_t e = ebeg(t); e < ebeg(t + 1); ++e)
+        if (c->obs_level[e] == level) ++cnt[pt_slot[c->obs_pt[e]]];
+    });
+    par([&](int t) {  // per-slot prefix over the chunks, slots split across threads
+      const int s0 = (int)((int64_t)nL * t / nth), s1 = (int)((int64_t)nL * (t + 1) / nth);
+      for (int sl = s0; sl < s1; ++sl) {
+        int b = lm_begin[sl];
+        for (int u = 0; u < nth; ++u) { const int k = base[u][sl]; base[u][sl] = b; b += k; }
+      }
+    });
+    par([&](int t) {
+      std::vector<int> &fill = base[t];
+      for (int64_t e = ebeg(t); e < ebeg(t + 1); ++e) {
+        if (c->obs_level[e] != level) continue;
+        const int sl = pt_slot[c->obs_pt[e]];
+        const int o = fill[sl]++;
+        c->dev_edge[o] = e;
+        obs_lm[o] = sl;
+        obs_cam[o] = c->obs_pose[e];
+        obs_camh[o] = phidx[c->obs_pose[e]];
+        obs_uv[2 * o] = c->obs_uv[2 * e];
+        obs_uv[2 * o + 1] = c->obs_uv[2 * e + 1];
+        obs_info[o] = c->obs_info[e];
+        obs_delta[o] = c->obs_delta[e];
+        if (c->has_stereo) obs_ur[o] = c->obs_ur[e];
+      }
+    });
+  }
+  // camera CSR (device obs in slot order), the same chunked counting sort
+  std::vector<int> cam_ptr(nP + 1, 0), cam_obs;
+  {
+    auto obeg = [&](int t) { return nE * t / nth; };
+    std::vector<std::vector<int>> base(nth);
+    par([&](int t) {
+      base[t].assign(nP, 0);
+      for (int64_t o = obeg(t); o < obeg(t + 1); ++o)
+        if (obs_camh[o] >= 0) ++base[t][obs_camh[o]];
+    });
+    for (int i = 0; i < nP; ++i)
+      for (int u = 0; u < nth; ++u) cam_ptr[i + 1] += base[u][i];
+    for (int i = 0; i < nP; ++i) cam_ptr[i + 1] += cam_ptr[i];
+    for (int i = 0; i < nP; ++i) {
+      int b = cam_ptr[i];
+      for (int u = 0; u < nth; ++u) { const int k = base[u][i]; base[u][i] = b; b += k; }
+    }
+    cam_obs.resize(cam_ptr[nP]);
+    par([&](int t) {
+      std::vector<int> &fill = base[t];
+      for (int64_t o = obeg(t); o < obeg(t + 1); ++o)
+        if (obs_camh[o] >= 0) cam_obs[fill[obs_camh[o]]++] = (int)o;
+    });
   }
   phase("obs+camcsr");
   // reduced-camera-system pattern (upper, diagonal first)
