@@ -158,7 +158,8 @@ enum BufId {
 // lists that sum each S block / g row from its tiles in tile order.
 struct TilePlan {
   std::vector<int> lm_ptr{0}, cam_ptr{0}, cams, obs_local, ld, red_ptr, gred_ptr;
-  std::vector<int2> urange, red_idx, gred_idx;
+  std::vector<int2> urange, gred_idx;
+  std::vector<int64_t> red_off;  // absolute offset (doubles) of each contribution's 6x6 block in part
   std::vector<int64_t> part_ptr{0}, gpart_ptr{0};
   int max_cp = 0;
   bool dups = false;
@@ -277,7 +278,10 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
     std::vector<int> f(ptr.begin(), ptr.end() - 1);
     for (auto &r : v) idx[f[r.key]++] = int2{r.tile, r.code};
   };
-  csr(red, s_row[nP], tp.red_ptr, tp.red_idx);
+  std::vector<int2> red_idx;
+  csr(red, s_row[nP], tp.red_ptr, red_idx);
+  tp.red_off.resize(red_idx.size());
+  for (size_t k = 0; k < red_idx.size(); ++k) tp.red_off[k] = tp.part_ptr[red_idx[k].x] + 36 * (int64_t)red_idx[k].y;
   csr(gred, nP, tp.gred_ptr, tp.gred_idx);
 }
 
@@ -609,7 +613,7 @@ int prepare(sqlm_ctx *c, int level) {
     AL(B_PART2, (size_t)tp.part_ptr.back(), d.part);
     AL(B_GPART, (size_t)tp.gpart_ptr.back(), d.gpart);
     UP(B_REDP, tp.red_ptr, d.red_ptr);
-    UP(B_REDI, tp.red_idx, d.red_idx);
+    UP(B_REDI, tp.red_off, d.red_off);
     UP(B_GREDP, tp.gred_ptr, d.gred_ptr);
     UP(B_GREDI, tp.gred_idx, d.gred_idx);
   }

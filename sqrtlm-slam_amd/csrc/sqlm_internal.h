@@ -93,7 +93,7 @@ struct DevProblem {
   double *part = nullptr;                   // tile partial Gram matrices
   double *gpart = nullptr;                  // tile partial g
   int *red_ptr = nullptr;                   // [nnzb+1] S block -> contributions
-  int2 *red_idx = nullptr;                  //   (tile, u << 8 | v)
+  int64_t *red_off = nullptr;               //   offset in part of the contribution's 36-double block
   int *gred_ptr = nullptr;                  // [nP+1] camera -> contributions
   int2 *gred_idx = nullptr;                 //   (tile, u)
   int tile_dups = 0;                        // some landmark observed twice by one camera

@@ -1100,9 +1100,13 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
   if (gid < d.nnzb * 36) {
     const int s = (int)(gid / 36), e = (int)(gid % 36), r = e / 6, c = e % 6;
     double v = 0.0;
-    for (int k = d.red_ptr[s]; k < d.red_ptr[s + 1]; ++k) {
-      const int2 ct = d.red_idx[k];  // (tile, block index in the tile's partial)
-      v += d.part[d.tile_part_ptr[ct.x] + 36 * (int64_t)ct.y + e];
+    const int k0 = d.red_ptr[s], k1 = d.red_ptr[s + 1];
+    for (int k = k0; k < k1; k += 4) {  // four contributions' loads in flight, summed in list order
+      double p4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) p4[u] = k + u < k1 ? d.part[d.red_off[k + u] + e] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v += p4[u];
     }
     const int j = d.s_col[s];
     if (s == d.s_row_ptr[j]) {  // diagonal block (first block of row j); sharded: this rank's share
