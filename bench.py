@@ -299,6 +299,21 @@ def bench_orb(args, world):
             dist.barrier()
         reps = max(50, args.steps * 10)
         ms, stages = ex.bench(img, reps)
+        # a stereo Frame extracts left and right on two threads with two
+        # ORBextractor objects (Frame.cc stereo constructor): two contexts (own
+        # HIP stream each) driven concurrently, one overlapping the other's host
+        # quadtree and synchronisations
+        import threading
+        with Context(local_rank) as ctx2:
+            ex2 = ORBextractor(2000, 1.2, 8, 20, 7, ctx=ctx2)
+            ex2(img)
+            th = [threading.Thread(target=e.bench, args=(img, reps)) for e in (ex, ex2)]
+            t0 = time.perf_counter()
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            stereo_fps = 2 * reps / (time.perf_counter() - t0)
         # algorithmic bytes of k_orb_fast per launch: every cell view it stages
         # (overlapping 30-px cells + 6-px overlap) + 4 B per candidate + 4 B count
         from oracle import orb as OB  # geometry only: the same cell loop as the reference
@@ -337,6 +352,7 @@ def bench_orb(args, world):
                "config": {"workload": "ORBextractor 1241x376, 2000 features, 8 levels", "keypoints": int(len(kps)),
                           "parallelism": f"replicas x{world}"},
                "stage_ms": dict(zip(["pyramid", "fast", "compact", "blur", "describe", "host_quadtree"], stages)),
+               "stereo_two_extractors_frames_per_s": stereo_fps,
                "roofline": {"bound": "hbm", "kernel": "k_orb_fast", "algorithmic_bytes": alg,
                             "achieved": alg / (t_fast * 1e-3) / 1e9 if t_fast > 0 else 0.0, "peak": HBM_PEAK_GBPS,
                             "unit": "GB/s", "traffic": None, "launch_ms": t_fast,
