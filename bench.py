@@ -418,6 +418,17 @@ def main():
     ms, kms, st = ctx.bench(args.warmup, args.steps)
     sse, nres = reprojection_sse(local, *ctx.poses(), ctx.points())
     e2e = None
+    if world == 1 and args.config == "lba":
+        # the drop-in LocalBundleAdjustment call: host arrays in, the three-pass
+        # schedule (5 Huber iterations, outlier tags, 10 more, + LiDAR 20), out
+        t0 = time.perf_counter()
+        ctx.set_problem(local)
+        ran, _tags, sts = ctx.local_ba()
+        ctx.poses(), ctx.points()
+        e2e = {"seconds": time.perf_counter() - t0, "passes": int(ran),
+               "lm_iterations": int(sum(x["iterations"] for x in sts)),
+               "setup_ms": float(sum(x["ms_setup"] for x in sts)), "optimize_ms": float(sum(x["ms_total"] for x in sts)),
+               "what": "sqlm_set_problem + sqlm_local_ba (3-pass schedule) + sqlm_get_poses/points, host buffers"}
     if world == 1 and args.config == "gba":
         # the drop-in call as the reference makes it (GlobalBundleAdjustemnt, 10
         # iterations): host arrays in, setup (sorting, tiles, H2D), the solve,

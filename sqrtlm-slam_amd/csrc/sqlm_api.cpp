@@ -174,7 +174,12 @@ void run_threads(int nth, F &&fn) {
   for (auto &t : th) t.join();
 }
 
-inline int host_threads() { return std::max(1, std::min(16, (int)std::thread::hardware_concurrency())); }
+// Host threads for a setup pass over `work` items: one per 128k items (thread
+// start-up costs more than small passes save; a local-BA window uses one).
+inline int host_threads(int64_t work) {
+  const int64_t want = std::max<int64_t>(1, work / 131072);
+  return (int)std::max<int64_t>(1, std::min<int64_t>({16, want, (int64_t)std::thread::hardware_concurrency()}));
+}
 
 void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::vector<int> &obs_camh,
                  const std::vector<int> &s_row, const std::vector<int> &s_col, int lm_cap, TilePlan &tp) {
@@ -216,7 +221,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
   struct Red { int key, tile, code; };
   struct TileOut { std::vector<int> cams; std::vector<Red> red; };
   std::vector<TileOut> out(nt);
-  const int nth = host_threads();
+  const int nth = host_threads(nE);
   run_threads(nth, [&](int th) {
     std::vector<int> lidx(nP, -1), lcams;
     std::vector<uint8_t> pst;
@@ -398,7 +403,7 @@ int prepare(sqlm_ctx *c, int level) {
   // chunk t of the edge range counts its edges per slot, the per-(chunk, slot)
   // bases follow by a prefix over chunks (edge-id order inside a landmark is
   // kept), then every chunk scatters its edges; the camera CSR likewise.
-  const int nth = host_threads();
+  const int nth = host_threads(c->n_obs);
   auto par = [&](auto &&fn) { run_threads(nth, fn); };
   {
     auto ebeg = [&](int t) { return c->n_obs * t / nth; };
@@ -464,7 +469,7 @@ int prepare(sqlm_ctx *c, int level) {
   {
     std::vector<std::vector<int>> rows(nP);
     {  // rows are independent: a few host threads, each with its own marks
-      const int nth = std::max(1, std::min(8, (int)std::thread::hardware_concurrency()));
+      const int nth = std::min(8, host_threads(nE));
       auto work = [&](int t0) {
         std::vector<int> mark(nP, -1), row;
         for (int i = t0; i < nP; i += nth) {
