@@ -862,7 +862,9 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
     c->spec_outstanding = false;
   }
   if (c->use_tiles) {
-    if (d.cr_direct) {  // the reduce assembles the CR superblocks itself
+    // cr_direct: the reduce assembles the CR superblocks itself; the RCS tile
+    // kernel cleared them (no memset launches) unless there were no tiles
+    if (d.cr_direct && d.n_tiles == 0) {
       const size_t blkbytes = (size_t)c->cr.p * c->cr.n * c->cr.n * sizeof(double);
       HIP_OK(hipMemsetAsync(d.cr_D, 0, blkbytes, c->stream));
       HIP_OK(hipMemsetAsync(d.cr_E, 0, blkbytes, c->stream));

@@ -1055,6 +1055,15 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
     TP(6);
   }
   TP_STORE;
+  if (d.cr_direct) {  // this tile's share of clearing the CR superblocks that k_rcs_reduce fills next
+    const int64_t tot = (int64_t)d.cr_p * d.cr_n * d.cr_n;  // doubles per array (even: n % 16 == 0)
+    const int64_t per = ((tot + d.n_tiles - 1) / d.n_tiles + 1) & ~(int64_t)1;
+    const int64_t a0 = (int64_t)t * per, a1 = min(tot, a0 + per);
+    for (int64_t k = a0 + 2 * tid; k < a1; k += 2 * TH) {
+      store2(d.cr_D + k, 0.0, 0.0);
+      store2(d.cr_E + k, 0.0, 0.0);
+    }
+  }
   // write -G_t as the tile's partial, block-major (tile_blk): element (R, C) of
   // an upper 16x16 tile goes to block (R/6, C/6) if that block is upper; a
   // diagonal block straddling two tiles also gets the mirror of the elements
