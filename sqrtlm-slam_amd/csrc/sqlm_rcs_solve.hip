@@ -489,9 +489,7 @@ __device__ __forceinline__ void tile_store(double *C, int n, int ti, int tj, con
 
 // Level h, step 2: A_I = Linv_I S(I, I-h) = Linv_I E_{I-h}^T and
 // C_I = Linv_I S(I, I+h) = Linv_I E_I, one 16x16 tile per wavefront.
-__global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h, int total) {
-  const int lb = xcd_block(total);
-  if (lb >= total) return;
+__device__ __forceinline__ void cr_elim_item(const CRView &v, int h, int lb) {
   const int n = v.n, nt = n >> 4, per = nt * nt;
   const int odd = lb / (2 * per), rem = lb - odd * 2 * per;
   const int which = rem / per, t = rem - which * per, ti = t / nt, tj = t - ti * nt;
@@ -505,13 +503,16 @@ __global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h, int total)
   }
 }
 
+__global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h, int total) {
+  const int lb = xcd_block(total);
+  if (lb < total) cr_elim_item(v, h, lb);
+}
+
 // Level h, step 3: every even superblock J absorbs its eliminated neighbours:
 // D_J -= A_{J+h}^T A_{J+h} + C_{J-h}^T C_{J-h} (lower tiles only);
 // E_J = -A_{J+h}^T C_{J+h}; g_J -= A_{J+h}^T z_{J+h} + C_{J-h}^T z_{J-h}.
 // Work items per even block: nt(nt+1)/2 D tiles, nt^2 E tiles, nt g slices.
-__global__ __launch_bounds__(64) void k_cr_update_gemm(CRView v, int h, int total) {
-  const int lb = xcd_block(total);
-  if (lb >= total) return;
+__device__ __forceinline__ void cr_update_item(const CRView &v, int h, int lb) {
   const int n = v.n, nt = n >> 4, nd = nt * (nt + 1) / 2, items = nd + nt * nt + nt;
   const int ev = lb / items, rem = lb - ev * items;
   const int J = 2 * h * ev;
@@ -557,13 +558,16 @@ __global__ __launch_bounds__(64) void k_cr_update_gemm(CRView v, int h, int tota
   }
 }
 
+__global__ __launch_bounds__(64) void k_cr_update_gemm(CRView v, int h, int total) {
+  const int lb = xcd_block(total);
+  if (lb < total) cr_update_item(v, h, lb);
+}
+
 // Last remaining superblock 0: x_0 = D_0^-1 g_0 = Linv^T (Linv g).
-__global__ __launch_bounds__(512) void k_cr_top(CRView v) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  __shared__ int fail;
+__device__ __forceinline__ void cr_top_body(const CRView &v, double *lds, int *fail) {
   const int n = v.n, ld = n + 1, nt = n >> 4;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
-  cr_factor_block(v, 0, lds, &fail);
+  cr_factor_block(v, 0, lds, fail);
   const double *L = lds;
   double *tmp = lds + n * ld, *z = tmp + n;
   const double *Dinv = tmp + 2 * n;
@@ -580,12 +584,19 @@ __global__ __launch_bounds__(512) void k_cr_top(CRView v) {
   CR_PROF(34);
 }
 
+__global__ __launch_bounds__(512) void k_cr_top(CRView v) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int fail;
+  cr_top_body(v, lds, &fail);
+}
+
 // Back substitution at level h: x_I = Linv_I^T (z_I - A_I x_{I-h} - C_I x_{I+h}).
 // One wave per 16-row slice (blockDim = 64 nt).
-__global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
-  extern __shared__ __attribute__((aligned(16))) double t[];
-  const int I = h + 2 * h * blockIdx.x, n = v.n;
+// Waves nt .. of a larger workgroup only join the barrier.
+__device__ __forceinline__ void cr_back_body(const CRView &v, int h, int I, double *t) {
+  const int n = v.n;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lo = lane & 7, hi = lane >> 3;
+  const bool act = wave < (n >> 4);
   const bool right = I + h < v.p;
   // 16-byte loads, eight lanes per 128-byte line; every global load is issued
   // before the first use (one memory round trip, 56 loads in flight).
@@ -602,6 +613,7 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
   const int r0 = 16 * wave + hi, hn = n >> 1;
   d2 a0[kCRMaxN / 16], a1[kCRMaxN / 16], c0[kCRMaxN / 16], c1[kCRMaxN / 16], vl[kCRMaxN / 16], vr[kCRMaxN / 16];
   d2 li[kCRMaxN / 8];
+  if (act) {
 #pragma unroll
   for (int u = 0; u < kCRMaxN / 16; ++u) {
     const int c = kclamp(16 * u + ca, n) >> 1;
@@ -640,7 +652,9 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
     t[r0] = v.g[(size_t)I * n + r0] - s0;
     t[r0 + 8] = v.g[(size_t)I * n + r0 + 8] - s1;
   }
+  }
   __syncthreads();
+  if (!act) return;
   double x0 = 0.0, x1 = 0.0;
 #pragma unroll
   for (int u = 0; u < kCRMaxN / 8; ++u) {
@@ -659,6 +673,12 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
     v.x[(size_t)I * n + 16 * wave + ca + 1] = x1;
   }
 }
+
+__global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
+  extern __shared__ __attribute__((aligned(16))) double t[];
+  cr_back_body(v, h, h + 2 * h * blockIdx.x, t);
+}
+
 
 // ---- dense SPD solve (essential graph) --------------------------------------
 // Blocked right-looking Cholesky of an n x n SPD matrix (n a multiple of

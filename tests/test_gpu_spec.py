@@ -69,3 +69,4 @@ def test_speculative_bitwise_equal(gpu_ctx, monkeypatch, name):
     if name == "window_outliers":
         assert max(a[0][1]["trace_trials"]) > 1  # the rejected-trial path ran
 
+
