@@ -17,6 +17,10 @@
 //     broadcasts; the panel solve is row-parallel; the trailing update runs on
 //     the FP64 matrix cores while wave 0 already factors the next diagonal
 //     block (look-ahead); the diagonal inverses are formed in parallel.
+//   * k_cr_factor_elim: the first level (>= 128 odd superblocks) runs the
+//     factor and the A_I / C_I tiles in one workgroup with Linv_I still in
+//     LDS; deeper levels, with few superblocks, keep the tile-parallel
+//     k_cr_elim_gemm, whose tiles spread over every CU (fused there: slower).
 //   * k_cr_elim_gemm / k_cr_update_gemm: one wavefront per 16x16 output tile
 //     (v_mfma_f64_16x16x4f64), workgroups remapped so that the tiles of one
 //     superblock run on one XCD and share its L2; only the lower triangle of
@@ -27,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "sqlm_internal.h"
 
@@ -506,6 +511,86 @@ __device__ __forceinline__ void cr_elim_item(const CRView &v, int h, int lb) {
 __global__ __launch_bounds__(64) void k_cr_elim_gemm(CRView v, int h, int total) {
   const int lb = xcd_block(total);
   if (lb < total) cr_elim_item(v, h, lb);
+}
+
+// One column strip of op(E) (rows 0..n, columns 16 tj .. +16) in registers, in
+// tile_gemm's K order (lane k4 holds k = 8m + 2k4 and k + 1 of pair m).
+template <bool TB>
+__device__ __forceinline__ void load_strip(const double *B, int n, int tj, double (&bx)[kCRMaxN / 8],
+                                           double (&by)[kCRMaxN / 8]) {
+  using d2 = HIP_vector_type<double, 2>;
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4, bc = tj * 16 + r16;
+#pragma unroll
+  for (int m = 0; m < kCRMaxN / 8; ++m) {
+    const int k = 8 * m + 2 * k4;
+    if (8 * m < n) {
+      if (TB) {
+        const d2 t = *reinterpret_cast<const d2 *>(B + bc * n + k);
+        bx[m] = t.x;
+        by[m] = t.y;
+      } else {
+        bx[m] = B[k * n + bc];
+        by[m] = B[(k + 1) * n + bc];
+      }
+    }
+  }
+}
+
+// Output tiles (ti, tj), ti = 0 .. nt-1, of Linv_I op(E) for one register strip,
+// Linv_I read from the factor's LDS layout (linv_at): the K order of
+// tile_gemm<false, TB, true>, so the same bits as k_cr_elim_gemm.
+__device__ __forceinline__ void strip_tiles(const double *L, int ld, const double *Dinv, const double (&bx)[kCRMaxN / 8],
+                                            const double (&by)[kCRMaxN / 8], double *out, int n, int tj) {
+  const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4, nt = n >> 4;
+  for (int ti = 0; ti < nt; ++ti) {
+    double ax[kCRMaxN / 8], ay[kCRMaxN / 8];
+#pragma unroll
+    for (int m = 0; m < kCRMaxN / 8; ++m) {
+      const int k = 8 * m + 2 * k4, kb = m >> 1;  // k and k + 1 lie in block column kb
+      if (kb <= ti) {
+        const double *a =
+            ti > kb ? L + (16 * kb + r16) * ld + 16 * ti + (k & 15) : Dinv + ti * kTile + r16 * kT + (k & 15);
+        ax[m] = a[0];
+        ay[m] = a[1];
+      }
+    }
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int m = 0; m < kCRMaxN / 8; ++m)
+      if ((m >> 1) <= ti) {
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ax[m], bx[m], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(ay[m], by[m], acc, 0, 0, 0);
+      }
+    tile_store(out, n, ti, tj, acc, 1.0, false);
+  }
+}
+
+// Level h, steps 1 + 2 in one workgroup per odd superblock: the factor of
+// k_cr_factor, then A_I = Linv_I E_{I-h}^T and C_I = Linv_I E_I with Linv_I
+// still in LDS (one launch and one global read of Linv_I less per level).
+// Wave w owns the output column strips w and w + 8 of [A_I | C_I]; both
+// E strips are loaded before the first MFMA.
+__global__ __launch_bounds__(512) void k_cr_factor_elim(CRView v, int h) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int fail;
+  const int I = h + 2 * h * blockIdx.x;
+  const int n = v.n, ld = n + 1, nt = n >> 4;
+  const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6;
+  const int jobs = (I + h < v.p ? 2 : 1) * nt;
+  const int q0 = wave, q1 = wave + nw;
+  double b0x[kCRMaxN / 8], b0y[kCRMaxN / 8], b1x[kCRMaxN / 8], b1y[kCRMaxN / 8];
+  cr_factor_store(v, I, lds, &fail);
+  const double *L = lds, *Dinv = lds + n * ld + 2 * n;
+  if (q0 < jobs) {
+    if (q0 < nt) load_strip<true>(blk(v.E, I - h, n), n, q0, b0x, b0y);
+    else load_strip<false>(blk(v.E, I, n), n, q0 - nt, b0x, b0y);
+  }
+  if (q1 < jobs) {
+    if (q1 < nt) load_strip<true>(blk(v.E, I - h, n), n, q1, b1x, b1y);
+    else load_strip<false>(blk(v.E, I, n), n, q1 - nt, b1x, b1y);
+  }
+  if (q0 < jobs) strip_tiles(L, ld, Dinv, b0x, b0y, q0 < nt ? blk(v.A, I, n) : blk(v.C, I, n), n, q0 % nt);
+  if (q1 < jobs) strip_tiles(L, ld, Dinv, b1x, b1y, q1 < nt ? blk(v.A, I, n) : blk(v.C, I, n), n, q1 % nt);
 }
 
 // Level h, step 3: every even superblock J absorbs its eliminated neighbours:
@@ -1138,12 +1223,20 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
   CRView v{p, n, 0, 0, D, E, A, C, g, x, flags};
   const size_t lds = cr_factor_lds(n);
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt;
+  // SQLM_CR_UNFUSED=1: separate factor and elimination launches (A/B only)
+  // SQLM_CR_FUSE_MIN: fewest odd superblocks for which a level runs fused
+  static const int fuse_min = std::getenv("SQLM_CR_FUSE_MIN") ? std::atoi(std::getenv("SQLM_CR_FUSE_MIN")) : 128;
+  static const bool fuse_ok = std::getenv("SQLM_CR_UNFUSED") == nullptr;
   int h = 1;
   for (; h < p; h *= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
-    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
-    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
+    if (fuse_ok && n_odd >= fuse_min) {
+      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd), dim3(512), lds, st, v, h);
+    } else {
+      hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
+      hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
+    }
     hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
   }
   hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
