@@ -1,0 +1,52 @@
+"""The CR solve's fused factor + elimination (k_cr_factor_elim) against the
+separate launches (k_cr_factor + k_cr_elim_gemm), at every level.
+
+The default fuses only levels with >= 128 odd superblocks (full-size config 4,
+covered by test_gpu_parity.py::test_config4_full_size_two_iterations); here
+SQLM_CR_FUSE_MIN=1 forces the fused kernel onto every level of a 14-superblock
+system, including the last odd block, which has no right neighbour. The two
+schedules run the same MFMA K order, so the results must be bit-identical.
+The threshold is read once per process, hence one child process per schedule.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[2], sys.argv[2] + '/sqrtlm-slam_amd']
+from sqrtlm import synth
+from sqrtlm.optimizer import Context
+prob = synth.config4(scale=0.05, seed=11)
+ctx = Context(0)
+ctx.set_problem(prob)
+n, st = ctx.global_ba(6)
+q, t = ctx.poses()
+np.savez(sys.argv[1], q=q, t=t, X=ctx.points(), chi2=np.asarray(st["trace_chi2"]), n=n)
+ctx.close()
+"""
+
+
+def _run(tmp_path, tag, env_extra):
+    out = str(tmp_path / f"{tag}.npz")
+    env = dict(os.environ)
+    env.pop("SQLM_CR_UNFUSED", None)
+    env.pop("SQLM_CR_FUSE_MIN", None)
+    env.update(env_extra)
+    subprocess.run([sys.executable, "-c", CHILD, out, ROOT], env=env, check=True, timeout=100)
+    return np.load(out)
+
+
+def test_fused_every_level_bit_identical(tmp_path):
+    a = _run(tmp_path, "fused", {"SQLM_CR_FUSE_MIN": "1"})
+    b = _run(tmp_path, "unfused", {"SQLM_CR_UNFUSED": "1"})
+    assert int(a["n"]) == int(b["n"]) > 0
+    for k in ("q", "t", "X", "chi2"):
+        assert np.array_equal(a[k], b[k]), k
