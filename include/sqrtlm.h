@@ -153,6 +153,16 @@ int sqlm_get_edge_chi2(sqlm_ctx *ctx, double *chi2);
 int sqlm_get_edge_depth_positive(sqlm_ctx *ctx, uint8_t *positive);
 int sqlm_get_edge_level(sqlm_ctx *ctx, uint8_t *level);
 
+/* Layout the last optimize() chose for the reduced camera system S (the
+ * replacement of SimplicialLDLT + AMD, linear_solver_eigen.h:60-75):
+ * out[0] = 0 none (no free camera), 1 banded (block cyclic reduction),
+ * 2 band + border (loop closure: cameras coupled far off the band eliminated
+ * last, launch_arrow_solve), 3 dense Cholesky; out[1] = cameras per
+ * superblock B, out[2] = superblocks p, out[3] = superblock rows n,
+ * out[4] = border cameras, out[5] = border rows (16-padded), out[6] = free
+ * cameras, out[7] = superblocks carrying band-border coupling. */
+int sqlm_get_rcs_layout(sqlm_ctx *ctx, int out[8]);
+
 /* Converter::toSE3Quat / toCvMat(SE3Quat) (src/utils/Converter.cc:55-79,98-109):
  * float32 row-major 4x4 T_cw <-> (q, t). */
 void sqlm_pose_from_Tcw_f32(const float T[16], double q[4], double t[3]);

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <limits>
 #include <new>
+#include <queue>
 #include <thread>
 #include <vector>
 
@@ -72,6 +73,7 @@ struct sqlm_ctx {
   int max_row_blocks = 0;
   int n_active_edges = 0;
   CRPlan cr;
+  std::vector<int> cam_pos;          // hidx -> band position or -(1 + border index)
   bool use_tiles = false;
   int tile_max_cp = 0, tile_max_k = 0;
   // ---- device memory ----
@@ -150,7 +152,8 @@ enum BufId {
   B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
-  B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX
+  B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
+  B_BDR, B_BDX
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -288,6 +291,108 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
   tp.red_off.resize(red_idx.size());
   for (size_t k = 0; k < red_idx.size(); ++k) tp.red_off[k] = tp.part_ptr[red_idx[k].x] + 36 * (int64_t)red_idx[k].y;
   csr(gred, nP, tp.gred_ptr, tp.gred_idx);
+}
+
+// Reduced-camera-system solver plan from the upper block pattern of S (hidx
+// order; SimplicialLDLT + AMD in the reference, linear_solver_eigen.h:60-75).
+// Blocks within kBandMaxCams of the diagonal form the band, solved by cyclic
+// reduction over superblocks of B = bandwidth + 1 cameras. Blocks farther off
+// (loop closures) are covered by a greedy maximum-degree vertex cover; those
+// cameras become the dense border, eliminated last (launch_arrow_solve). The
+// cyclic reduction carries the band-border coupling only in the superblocks
+// that can hold it: per level, the odd superblocks whose right-hand side is
+// nonzero form Z = Linv G, the even ones next to them take the update.
+// Returns false when S should go to the dense solver (border too large).
+bool plan_rcs(int nP, const std::vector<int> &s_row, const std::vector<int> &s_col, CRPlan &pl,
+              std::vector<int> &cam_pos) {
+  pl = CRPlan{};
+  cam_pos.resize(nP);
+  for (int i = 0; i < nP; ++i) cam_pos[i] = i;
+  if (nP == 0) return false;
+  std::vector<int> lptr(nP + 1, 0), ladj;
+  std::vector<std::pair<int, int>> longe;
+  for (int i = 0; i < nP; ++i)
+    for (int k = s_row[i]; k < s_row[i + 1]; ++k)
+      if (s_col[k] - i > kBandMaxCams) longe.emplace_back(i, s_col[k]);
+  std::vector<uint8_t> border(nP, 0);
+  int nbc = 0;
+  if (!longe.empty()) {
+    for (auto &e : longe) { ++lptr[e.first + 1]; ++lptr[e.second + 1]; }
+    for (int i = 0; i < nP; ++i) lptr[i + 1] += lptr[i];
+    ladj.resize(lptr[nP]);
+    std::vector<int> fill(lptr.begin(), lptr.end() - 1), deg(nP, 0);
+    for (auto &e : longe) { ladj[fill[e.first]++] = e.second; ladj[fill[e.second]++] = e.first; }
+    std::priority_queue<std::pair<int, int>> pq;  // (remaining long blocks, camera): ties -> higher index
+    for (int i = 0; i < nP; ++i) {
+      deg[i] = lptr[i + 1] - lptr[i];
+      if (deg[i]) pq.emplace(deg[i], i);
+    }
+    while (!pq.empty()) {
+      const auto [dg, v] = pq.top();
+      pq.pop();
+      if (border[v] || dg != deg[v] || dg == 0) continue;
+      border[v] = 1;
+      ++nbc;
+      for (int k = lptr[v]; k < lptr[v + 1]; ++k) {
+        const int u = ladj[k];
+        if (!border[u] && deg[u] > 0) pq.emplace(--deg[u], u);
+      }
+      deg[v] = 0;
+    }
+  }
+  const int nband = nP - nbc;
+  if (nbc > 0) {
+    if (nband == 0 || 3 * nbc > nP) return false;
+    int pos = 0, b = 0;
+    for (int i = 0; i < nP; ++i) cam_pos[i] = border[i] ? -1 - b++ : pos++;
+  }
+  int bw = 0;
+  for (int i = 0; i < nP; ++i)
+    for (int k = s_row[i]; k < s_row[i + 1]; ++k)
+      if (cam_pos[i] >= 0 && cam_pos[s_col[k]] >= 0) bw = std::max(bw, cam_pos[s_col[k]] - cam_pos[i]);
+  const int B = std::min(bw + 1, std::max(nband, 1));
+  const int n = (6 * B + 15) / 16 * 16;
+  if (n > kCRMaxN) return false;
+  pl.enabled = true;
+  pl.B = B;
+  pl.p = (nband + B - 1) / B;
+  pl.n = n;
+  pl.nband = nband;
+  if (nbc == 0) return true;
+  pl.nbc = nbc;
+  pl.R = (6 * nbc + 15) / 16 * 16;
+  pl.Rp = (pl.R + kCRMaxN - 1) / kCRMaxN * kCRMaxN;
+  // superblocks holding band-border blocks, then the per-level lists
+  std::vector<uint8_t> act(pl.p, 0);
+  for (int i = 0; i < nP; ++i)
+    for (int k = s_row[i]; k < s_row[i + 1]; ++k) {
+      const int a = cam_pos[i], c2 = cam_pos[s_col[k]];
+      if ((a < 0) != (c2 < 0)) act[(a >= 0 ? a : c2) / B] = 1;
+    }
+  std::vector<int> &S = pl.sched, elim;
+  pl.init_off = 0;
+  for (int I = 0; I < pl.p; ++I)
+    if (act[I]) S.push_back(I);
+  pl.init_cnt = (int)S.size();
+  for (int h = 1; h < pl.p; h *= 2) {
+    const int fo = (int)S.size();
+    for (int I = h; I < pl.p; I += 2 * h)
+      if (act[I]) { S.push_back(I); elim.push_back(I); }
+    const int uo = (int)S.size();
+    for (int J = 0; J < pl.p; J += 2 * h) {
+      const bool r = J + h < pl.p && act[J + h], l = J >= h && act[J - h];
+      if (!r && !l) continue;
+      S.push_back(J | (act[J] ? kUpdHad : 0) | (r ? kUpdRight : 0) | (l ? kUpdLeft : 0));
+      act[J] = 1;
+    }
+    pl.lvl.insert(pl.lvl.end(), {fo, uo - fo, uo, (int)S.size() - uo});
+  }
+  pl.top_active = act[0] != 0;
+  if (pl.top_active) elim.push_back(0);
+  pl.elim_off = (int)S.size();
+  pl.elim_cnt = (int)elim.size();
+  S.insert(S.end(), elim.begin(), elim.end());
+  return true;
 }
 
 // Lanes per landmark segment in the per-landmark kernels: up to kObsPerLane
@@ -511,19 +616,8 @@ int prepare(sqlm_ctx *c, int level) {
       mx = std::max(mx, (int)rows[i].size());
     }
     c->max_row_blocks = mx;
-    // block bandwidth in cameras -> superblock plan
-    int bw = 0;
-    for (int i = 0; i < nP; ++i)
-      for (int k = s_row[i]; k < s_row[i + 1]; ++k) bw = std::max(bw, s_col[k] - i);
-    c->cr = CRPlan{};
-    const int B = std::min(bw + 1, std::max(nP, 1));
-    const int n = (6 * B + 15) / 16 * 16;
-    if (n <= kCRMaxN) {
-      c->cr.enabled = true;
-      c->cr.B = B;
-      c->cr.p = (nP + B - 1) / B;
-      c->cr.n = n;
-    }
+    // band (+ border) superblock plan; the dense Cholesky otherwise
+    if (!plan_rcs(nP, s_row, s_col, c->cr, c->cam_pos)) c->cr = CRPlan{};
   }
   TilePlan tp;
   // landmarks per tile: up to kTileMaxLm, fewer on small problems so that the
@@ -573,6 +667,9 @@ int prepare(sqlm_ctx *c, int level) {
   d.cr_B = c->cr.B;
   d.cr_n = c->cr.n;
   d.cr_p = c->cr.p;
+  d.cr_nband = c->cr.nband;
+  d.arw_R = c->cr.R;
+  d.arw_Rp = c->cr.Rp;
   std::vector<double> qt(8 * (size_t)c->n_pose, 0.0), X(4 * (size_t)nL, 0.0);
   for (int p = 0; p < c->n_pose; ++p) {
     for (int k = 0; k < 4; ++k) qt[8 * p + k] = c->pose_q[4 * p + k];
@@ -686,6 +783,7 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_S, 36 * (size_t)d.nnzb, d.S);
   AL(B_G, 6 * (size_t)nP, d.g);
   AL(B_DX, 6 * (size_t)nP + 1, d.dx);
+  d.cam_pos = nullptr;
   if (c->cr.enabled) {
     const size_t nb = (size_t)c->cr.p * c->cr.n * c->cr.n;
     AL(B_CRD, nb, d.cr_D);
@@ -694,8 +792,27 @@ int prepare(sqlm_ctx *c, int level) {
     AL(B_CRC, nb, d.cr_C);
     AL(B_CRG, (size_t)c->cr.p * c->cr.n, d.cr_g);
     AL(B_CRX, (size_t)c->cr.p * c->cr.n, d.cr_x);
+    if (c->cr.R) {  // band + border layout
+      const size_t fr = (size_t)c->cr.p * c->cr.n * c->cr.R, rp = (size_t)c->cr.Rp;
+      UP(B_CAMPOS, c->cam_pos, d.cam_pos);
+      int *sd = nullptr;
+      UP(B_ARWS, c->cr.sched, sd);
+      c->cr.sched_dev = sd;
+      AL(B_ARWG, fr, d.arw_G);
+      AL(B_ARWZ, fr, d.arw_Z);
+      AL(B_BDA, rp * rp, d.bd_A);
+      AL(B_BDL, rp * rp, d.bd_L);
+      AL(B_BDLI, rp * kCRMaxN, d.bd_Linv);
+      AL(B_BDR, rp, d.bd_r);
+      AL(B_BDX, rp, d.bd_x);
+    }
   } else {  // blocked MFMA Cholesky of the dense S (sqlm_rcs_solve.hip)
     const int np_ = (6 * nP + kCRMaxN - 1) / kCRMaxN * kCRMaxN;
+    {  // two np_ x np_ matrices: refuse what the device cannot hold instead of failing mid-solve
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess && 2.0 * 8.0 * np_ * (double)np_ > 0.9 * (double)fr)
+        return SQLM_ERR_OOM;
+    }
     d.dense_n = np_;
     AL(B_DENSE, (size_t)np_ * np_, d.dense);
     AL(B_DENSEL, (size_t)np_ * np_, d.dense_L);
@@ -869,6 +986,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
       HIP_OK(hipMemsetAsync(d.cr_D, 0, blkbytes, c->stream));
       HIP_OK(hipMemsetAsync(d.cr_E, 0, blkbytes, c->stream));
     }
+    if (d.cr_direct && c->cr.R) launch_arrow_clear(d, c->cr, c->stream);
     launch_rcs_reduce(d, lambda, c->stream);
   }
   tmark(c, 8, true);
@@ -1370,6 +1488,21 @@ int sqlm_get_edge_depth_positive(sqlm_ctx *c, uint8_t *pos) {
   std::vector<uint8_t> dp;
   depth_positive_host(c, dp);
   if (c->n_obs) std::memcpy(pos, dp.data(), c->n_obs);
+  return SQLM_OK;
+}
+
+int sqlm_get_rcs_layout(sqlm_ctx *c, int out[8]) {
+  if (!c || !out) return SQLM_ERR_INVALID_ARG;
+  const CRPlan &pl = c->cr;
+  const int nP = c->d.nP;
+  out[0] = nP == 0 ? 0 : !pl.enabled ? 3 : pl.R ? 2 : 1;
+  out[1] = pl.B;
+  out[2] = pl.p;
+  out[3] = pl.n;
+  out[4] = pl.nbc;
+  out[5] = pl.R;
+  out[6] = nP;
+  out[7] = pl.init_cnt;
   return SQLM_OK;
 }
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace sqlm {
 
 constexpr int kBlock = 256;
@@ -104,6 +106,16 @@ struct DevProblem {
   double *cr_g = nullptr, *cr_x = nullptr;  // [p][n]
   int cr_direct = 0;                        // k_rcs_reduce writes D/E/g in CR layout (no BSR S)
   int cr_B = 0, cr_n = 0, cr_p = 0;
+  // band + border ("arrow") layout of a loop-closed S (CRPlan.R > 0): cameras
+  // covering every block far off the band are eliminated last as a dense
+  // border; the band cameras keep the CR superblocks in camera order
+  int cr_nband = 0;                         // band cameras (= nP without a border)
+  int arw_R = 0, arw_Rp = 0;                // border rows padded to 16 / to kCRMaxN (0 = no border)
+  int *cam_pos = nullptr;                   // [nP] band position, or -(1 + border index)
+  double *arw_G = nullptr, *arw_Z = nullptr;  // [p][n][R] band-border coupling F^T, and Linv F^T
+  double *bd_A = nullptr, *bd_L = nullptr;  // [Rp][Rp] border system (lower) / its factor
+  double *bd_Linv = nullptr;                // [Rp / kCRMaxN][kCRMaxN][kCRMaxN]
+  double *bd_r = nullptr, *bd_x = nullptr;  // [Rp]
   // reductions
   double *partials = nullptr;               // [kMaxPartials]
   int pc_lm = 0, pc_lid = 0;                // chi2 partial regions of the current linearization
@@ -132,11 +144,26 @@ constexpr int kMaxFreePoses = 131072;
 
 // Superblock plan of the reduced camera system: B cameras per superblock
 // (B = block bandwidth + 1), p superblocks of n = roundup(6B, 16) rows.
+// With a border (R > 0) the band's cyclic reduction also carries the sparse
+// right-hand sides F^T (the band-border coupling): only superblocks whose F^T
+// block can be nonzero are touched, per level (host-built lists in `sched`).
 struct CRPlan {
   bool enabled = false;
   int B = 0, p = 0, n = 0;
+  int nband = 0;                 // band cameras
+  int R = 0, Rp = 0, nbc = 0;    // border width (16-padded, kCRMaxN-padded), border cameras
+  std::vector<int> sched;        // concatenated lists (host); dev copy below
+  const int *sched_dev = nullptr;
+  // per level h = 1, 2, 4, ...: [fwd_off, fwd_cnt, upd_off, upd_cnt]
+  std::vector<int> lvl;
+  int init_off = 0, init_cnt = 0;  // superblocks with a nonzero F^T block (cleared per trial)
+  int elim_off = 0, elim_cnt = 0;  // superblocks whose Z = Linv F^T is formed (Gram, correction)
+  bool top_active = false;         // superblock 0 carries F^T after the last level
 };
 constexpr int kCRMaxN = 112;  // LDS: L (n x n+1) + Dinv (16n) + W (16n) <= 160 KiB
+constexpr int kBandMaxCams = kCRMaxN / 6 - 1;  // S blocks farther off the diagonal go to the border
+// update-list entries: superblock | flags
+constexpr int kUpdHad = 1 << 28, kUpdRight = 1 << 29, kUpdLeft = 1 << 30, kUpdMask = (1 << 28) - 1;
 
 // Tile partials are stored block-major: the upper 6x6 camera blocks (u <= w)
 // of a tile's cp cameras, packed row by row, 36 contiguous doubles each (the
@@ -189,6 +216,8 @@ int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase co
 constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);  // zeroes + scatters unless cr_direct
+// band + border layout: clear F^T / the border system before S is assembled into it
+void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st);
 // CR levels + top + back substitution on blocks already in CR layout (microbench / tests)
 void launch_cr_core(double *D, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
                     hipStream_t st);

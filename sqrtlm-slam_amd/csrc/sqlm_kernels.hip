@@ -1126,10 +1126,23 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
       d.S[gid] = v;
     } else {
       const int i = d.s_row[s], n = d.cr_n, B = d.cr_B;
-      const int I = i / B, li = i - I * B, J = j / B, lj = j - J * B;
-      double *base = (J == I ? d.cr_D : d.cr_E) + (size_t)I * n * n;
-      base[(6 * li + r) * n + 6 * lj + c] = v;
-      if (J == I && j != i) base[(6 * lj + c) * n + 6 * li + r] = v;
+      const int pi = d.cam_pos ? d.cam_pos[i] : i, pj = d.cam_pos ? d.cam_pos[j] : j;
+      if (pi >= 0 && pj >= 0) {  // band (positions ascend with the camera index)
+        const int I = pi / B, li = pi - I * B, J = pj / B, lj = pj - J * B;
+        double *base = (J == I ? d.cr_D : d.cr_E) + (size_t)I * n * n;
+        base[(6 * li + r) * n + 6 * lj + c] = v;
+        if (J == I && j != i) base[(6 * lj + c) * n + 6 * li + r] = v;
+      } else if (pi >= 0) {  // band row, border column: F^T
+        const int I = pi / B, li = pi - I * B;
+        d.arw_G[((size_t)I * n + 6 * li + r) * d.arw_R + 6 * (-1 - pj) + c] = v;
+      } else if (pj >= 0) {
+        const int J = pj / B, lj = pj - J * B;
+        d.arw_G[((size_t)J * n + 6 * lj + c) * d.arw_R + 6 * (-1 - pi) + r] = v;
+      } else {  // border system, both triangles
+        const int bi = -1 - pi, bj = -1 - pj;
+        d.bd_A[(size_t)(6 * bi + r) * d.arw_Rp + 6 * bj + c] = v;
+        d.bd_A[(size_t)(6 * bj + c) * d.arw_Rp + 6 * bi + r] = v;
+      }
     }
   }
   const int64_t g2 = gid - d.nnzb * 36;
@@ -1143,15 +1156,20 @@ __global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda)
     v += d.bp[8 * i + r];
     d.g[6 * i + r] = v;
     if (d.cr_direct) {
-      const int I = i / d.cr_B, li = i - I * d.cr_B;
-      d.cr_g[(size_t)I * d.cr_n + 6 * li + r] = v;
+      const int pi = d.cam_pos ? d.cam_pos[i] : i;
+      if (pi >= 0) {
+        const int I = pi / d.cr_B, li = pi - I * d.cr_B;
+        d.cr_g[(size_t)I * d.cr_n + 6 * li + r] = v;
+      } else {
+        d.bd_r[6 * (-1 - pi) + r] = v;
+      }
     }
   }
   if (d.cr_direct) {  // identity on the padded rows of every superblock; solve flag
     const int64_t g3 = g2 - (int64_t)d.nP * 6;
     if (g3 >= 0 && g3 < (int64_t)d.cr_p * d.cr_n) {
       const int I = (int)(g3 / d.cr_n), rr = (int)(g3 % d.cr_n);
-      const int used = min(d.cr_B, d.nP - I * d.cr_B);
+      const int used = min(d.cr_B, d.cr_nband - I * d.cr_B);
       if (rr >= 6 * used) {
         d.cr_D[((size_t)I * d.cr_n + rr) * d.cr_n + rr] = 1.0;
         d.cr_g[(size_t)I * d.cr_n + rr] = 0.0;

@@ -352,30 +352,48 @@ __device__ __forceinline__ double *blk(double *base, int I, int n) { return base
 inline size_t cr_factor_lds(int n) { return ((size_t)n * (n + 1) + 37 * (size_t)n) * sizeof(double); }
 
 // BSR (upper, 6x6 blocks) -> superblock D_I (symmetric) and E_I = S(I, I+1); g -> g_I.
+// With a border (d.cam_pos): band-border blocks -> F^T (arw_G), border-border
+// blocks -> the border system bd_A (both triangles), border g -> bd_r.
 __global__ __launch_bounds__(256) void k_cr_scatter(DevProblem d, CRView v) {
   const int i = blockIdx.x;  // free camera
-  const int I = i / v.B, li = i - I * v.B, n = v.n;
+  const int n = v.n, R = d.arw_R, Rp = d.arw_Rp;
+  const int pi = d.cam_pos ? d.cam_pos[i] : i;
+  const int I = pi >= 0 ? pi / v.B : 0, li = pi >= 0 ? pi - I * v.B : 0;
   for (int s = d.s_row_ptr[i]; s < d.s_row_ptr[i + 1]; ++s) {
     const int j = d.s_col[s];
-    const int J = j / v.B, lj = j - J * v.B;
+    const int pj = d.cam_pos ? d.cam_pos[j] : j;
+    const int J = pj >= 0 ? pj / v.B : 0, lj = pj >= 0 ? pj - J * v.B : 0;
     for (int e = threadIdx.x; e < 36; e += blockDim.x) {
       const int r = e / 6, c = e % 6;
       const double val = d.S[(size_t)s * 36 + e];
-      if (J == I) {
-        blk(v.D, I, n)[(6 * li + r) * n + 6 * lj + c] = val;
-        if (j != i) blk(v.D, I, n)[(6 * lj + c) * n + 6 * li + r] = val;
-      } else {  // J == I + 1 (block tridiagonal by construction)
-        blk(v.E, I, n)[(6 * li + r) * n + 6 * lj + c] = val;
+      if (pi >= 0 && pj >= 0) {
+        if (J == I) {
+          blk(v.D, I, n)[(6 * li + r) * n + 6 * lj + c] = val;
+          if (j != i) blk(v.D, I, n)[(6 * lj + c) * n + 6 * li + r] = val;
+        } else {  // J == I + 1 (block tridiagonal by construction)
+          blk(v.E, I, n)[(6 * li + r) * n + 6 * lj + c] = val;
+        }
+      } else if (pi >= 0) {
+        d.arw_G[((size_t)I * n + 6 * li + r) * R + 6 * (-1 - pj) + c] = val;
+      } else if (pj >= 0) {
+        d.arw_G[((size_t)J * n + 6 * lj + c) * R + 6 * (-1 - pi) + r] = val;
+      } else {
+        const int bi = -1 - pi, bj = -1 - pj;
+        d.bd_A[(size_t)(6 * bi + r) * Rp + 6 * bj + c] = val;
+        d.bd_A[(size_t)(6 * bj + c) * Rp + 6 * bi + r] = val;
       }
     }
   }
-  if (threadIdx.x < 6) v.g[(size_t)I * n + 6 * li + threadIdx.x] = d.g[6 * i + threadIdx.x];
-  // identity on padded rows (cameras past nP in the last superblock, rows >= 6B)
-  if (li == 0) {
-    for (int r = 6 * v.B + threadIdx.x; r < n; r += blockDim.x) blk(v.D, I, n)[r * n + r] = 1.0;
-    if (I == v.p - 1) {
-      const int used = v.nP - I * v.B;
-      for (int r = 6 * used + threadIdx.x; r < 6 * v.B; r += blockDim.x) blk(v.D, I, n)[r * n + r] = 1.0;
+  if (threadIdx.x < 6) {
+    if (pi >= 0) v.g[(size_t)I * n + 6 * li + threadIdx.x] = d.g[6 * i + threadIdx.x];
+    else d.bd_r[6 * (-1 - pi) + threadIdx.x] = d.g[6 * i + threadIdx.x];
+  }
+  // identity on padded rows (cameras past the band in the last superblock, rows >= 6B)
+  if (i < v.p && threadIdx.x < 64) {
+    const int K = i, used = min(v.B, d.cr_nband - K * v.B);
+    for (int r = 6 * used + threadIdx.x; r < n; r += 64) {
+      blk(v.D, K, n)[r * n + r] = 1.0;
+      v.g[(size_t)K * n + r] = 0.0;
     }
   }
   if (i == 0 && threadIdx.x == 0) v.flags[0] = 1;
@@ -1213,8 +1231,195 @@ int launch_cr_multi(double *D, double *E, double *A, double *C, double *gs, doub
 __global__ void k_cr_gather(DevProblem d, CRView v) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= 6 * v.nP) return;
-  const int i = k / 6, r = k % 6, I = i / v.B, li = i - I * v.B;
-  d.dx[k] = v.flags[0] ? v.x[(size_t)I * v.n + 6 * li + r] : 0.0;
+  const int i = k / 6, r = k % 6, pi = d.cam_pos ? d.cam_pos[i] : i;
+  double x = 0.0;
+  if (pi >= 0) {
+    const int I = pi / v.B, li = pi - I * v.B;
+    x = v.x[(size_t)I * v.n + 6 * li + r];
+  } else {
+    x = d.bd_x[6 * (-1 - pi) + r];
+  }
+  d.dx[k] = v.flags[0] ? x : 0.0;
+}
+
+// ---- band + border ("arrow") solve of a loop-closed reduced camera system ----
+// Replaces SimplicialLDLT + AMD on S (linear_solver_eigen.h:60-75,94-124) when
+// loop closures couple cameras far off the band. The border cameras (a greedy
+// vertex cover of the blocks farther than kBandMaxCams cameras off the
+// diagonal) are ordered last, so in the permuted camera order
+//   S = [ B  F^T ]   B: block-tridiagonal band (CR superblocks),
+//       [ F  G   ]   F: band-border coupling, G: border block.
+// With the band's cyclic reduction written as a permuted block Cholesky
+// B = P L L^T P^T (L's diagonal blocks are the CR factors, its off-diagonal
+// blocks the A / C eliminations), the forward sweep applied to the columns of
+// F^T gives W = L^-1 P^T F^T (blocks Z_I), applied to r_b gives w (the CR's
+// z_I). Then
+//   (G - W^T W) x_c = r_c - W^T w          (dense border system, MFMA Cholesky)
+//   x_b = P L^-T (w - W x_c)               (correct z_I, back substitution)
+// which is the exact block elimination of S (same math as g2o's LDL^T, another
+// elimination order). F^T is nonzero only in the few superblocks next to the
+// border cameras; the forward sweep keeps that sparsity (a superblock's
+// right-hand side becomes nonzero only when an eliminated neighbour's is), so
+// Z is formed for O(#coupled + log p) superblocks, from host-built lists.
+struct ArwView {
+  int p, n, R;
+  const double *D, *A, *C;  // D_I = Linv_I once factored
+  double *G, *Z;            // [p][n][R]
+  double *g;                // [p][n]: z_I after the forward sweep
+};
+
+// Z_I = Linv_I G_I for the superblocks I of `list`
+__global__ __launch_bounds__(64) void k_arw_fwd(ArwView a, const int *list, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int nt = a.n >> 4, rt = a.R >> 4, per = nt * rt;
+  const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, I = list[q];
+  const size_t nn = (size_t)a.n * a.n, nr = (size_t)a.n * a.R;
+  const d4 acc = mm_tile<false>(a.D + I * nn, a.n, a.G + I * nr, a.R, ti, tj, 0, 16 * (ti + 1));
+  mm_store(a.Z + I * nr, a.R, ti, tj, acc, 1.0, false);
+}
+
+// even J of level h: G_J = [G_J] - A_{J+h}^T Z_{J+h} - C_{J-h}^T Z_{J-h}, the
+// terms present per the entry's flags (a superblock without a right-hand side
+// yet starts from zero)
+__global__ __launch_bounds__(64) void k_arw_upd(ArwView a, int h, const int *list, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  const int n = a.n, nt = n >> 4, rt = a.R >> 4, per = nt * rt;
+  const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt;
+  const int e = list[q], J = e & kUpdMask;
+  const size_t nn = (size_t)n * n, nr = (size_t)n * a.R;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  if (e & kUpdRight) acc = mm_tile<true>(a.A + (J + h) * nn, n, a.Z + (J + h) * nr, a.R, ti, tj, 0, n);
+  if (e & kUpdLeft) acc += mm_tile<true>(a.C + (J - h) * nn, n, a.Z + (J - h) * nr, a.R, ti, tj, 0, n);
+  mm_store(a.G + J * nr, a.R, ti, tj, acc, -1.0, (e & kUpdHad) != 0);
+}
+
+// Border Schur complement, lower 16x16 tiles: Ab -= sum_{I in elim} Z_I^T Z_I
+// (superblocks in list order: deterministic)
+__global__ __launch_bounds__(64) void k_arw_gram(ArwView a, const int *elim, int ne, double *Ab, int ldb, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  int ti = 0, tj = lb;
+  while (tj > ti) { tj -= ti + 1; ++ti; }
+  const size_t nr = (size_t)a.n * a.R;
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int q = 0; q < ne; ++q) {
+    const double *Z = a.Z + elim[q] * nr;
+    acc += mm_tile<true>(Z, a.R, Z, a.R, ti, tj, 0, a.n);
+  }
+  mm_store(Ab, ldb, ti, tj, acc, -1.0, true);
+}
+
+// rb -= sum_{I in elim} Z_I^T z_I: 64 columns per workgroup, four k-quarters
+// summed in a fixed order
+__global__ __launch_bounds__(256) void k_arw_gvec(ArwView a, const int *elim, int ne, double *rb) {
+  __shared__ double part[4][64];
+  const int cl = threadIdx.x & 63, kq = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  double s = 0.0;
+  if (c < a.R) {
+    for (int q = 0; q < ne; ++q) {
+      const int I = elim[q];
+      const double *Z = a.Z + (size_t)I * a.n * a.R, *z = a.g + (size_t)I * a.n;
+      for (int k = kq; k < a.n; k += 4) s += Z[(size_t)k * a.R + c] * z[k];
+    }
+  }
+  part[kq][cl] = s;
+  __syncthreads();
+  if (kq == 0 && c < a.R) rb[c] -= ((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl];
+}
+
+// z_I -= Z_I x_c for I in elim: one wavefront per row
+__global__ __launch_bounds__(256) void k_arw_correct(ArwView a, const int *elim, int ne, const double *xc) {
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (w >= ne * a.n) return;
+  const int I = elim[w / a.n], k = w % a.n;
+  const double *Zr = a.Z + ((size_t)I * a.n + k) * a.R;
+  double s = 0.0;
+  for (int c = lane; c < a.R; c += 64) s += Zr[c] * xc[c];
+  s = wave_sum_d(s);
+  if (lane == 0) a.g[(size_t)I * a.n + k] -= s;
+}
+
+// x_0 = Linv_0^T z_0 (the top superblock, factored by k_cr_factor_at)
+__global__ __launch_bounds__(128) void k_arw_top_back(ArwView a, double *x) {
+  const int c = threadIdx.x;
+  if (c >= a.n) return;
+  double s = 0.0;
+  for (int r = c; r < a.n; ++r) s += a.D[(size_t)r * a.n + c] * a.g[r];
+  x[c] = s;
+}
+
+// Border system init per trial: clear F^T in the superblocks that carry it,
+// the border matrix (identity on its padding rows) and its right-hand side.
+__global__ __launch_bounds__(256) void k_arw_clear(DevProblem d, const int *init, int ninit) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nr = (int64_t)d.cr_n * d.arw_R, Rp = d.arw_Rp;
+  if (gid < ninit * nr) {
+    const int64_t q = gid / nr, e = gid - q * nr;
+    d.arw_G[(int64_t)init[q] * nr + e] = 0.0;
+    return;
+  }
+  const int64_t g2 = gid - ninit * nr;
+  if (g2 < Rp * Rp) {
+    const int64_t r = g2 / Rp, c = g2 - r * Rp;
+    d.bd_A[g2] = (r == c && r >= 6 * (d.nP - d.cr_nband)) ? 1.0 : 0.0;
+    if (c == 0) d.bd_r[r] = 0.0;
+  }
+}
+
+void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
+  const int64_t items = (int64_t)pl.init_cnt * pl.n * pl.R + (int64_t)pl.Rp * pl.Rp;
+  hipLaunchKernelGGL(k_arw_clear, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, d,
+                     pl.sched_dev + pl.init_off, pl.init_cnt);
+}
+
+// The CR levels of launch_cr_core with the sparse right-hand sides F^T carried
+// along, the border system, and the back substitution.
+static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
+  const int p = pl.p, n = pl.n, R = pl.R;
+  CRView v{p, n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags};
+  ArwView a{p, n, R, d.cr_D, d.cr_A, d.cr_C, d.arw_G, d.arw_Z, d.cr_g};
+  const size_t lds = cr_factor_lds(n);
+  const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt, rhs = nt * (R / 16);
+  static const int fuse_min = std::getenv("SQLM_CR_FUSE_MIN") ? std::atoi(std::getenv("SQLM_CR_FUSE_MIN")) : 128;
+  static const bool fuse_ok = std::getenv("SQLM_CR_UNFUSED") == nullptr;
+  const int *S = pl.sched_dev;
+  int h = 1, lv = 0;
+  for (; h < p; h *= 2, ++lv) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
+    const int n_even = (p + 2 * h - 1) / (2 * h);
+    const int fo = pl.lvl[4 * lv], fc = pl.lvl[4 * lv + 1], uo = pl.lvl[4 * lv + 2], uc = pl.lvl[4 * lv + 3];
+    if (fuse_ok && n_odd >= fuse_min) {
+      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd), dim3(512), lds, st, v, h);
+    } else {
+      hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
+      hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
+    }
+    if (fc) hipLaunchKernelGGL(k_arw_fwd, dim3(xcd_grid(fc * rhs)), dim3(64), 0, st, a, S + fo, fc * rhs);
+    hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
+    if (uc) hipLaunchKernelGGL(k_arw_upd, dim3(xcd_grid(uc * rhs)), dim3(64), 0, st, a, h, S + uo, uc * rhs);
+  }
+  // top superblock: factor (Linv_0 into D_0, z_0 into g_0) and its Z_0
+  hipLaunchKernelGGL(k_cr_factor_at, dim3(1), dim3(512), lds, st, v, 0);
+  const int *elim = S + pl.elim_off;
+  if (pl.top_active)
+    hipLaunchKernelGGL(k_arw_fwd, dim3(xcd_grid(rhs)), dim3(64), 0, st, a, elim + pl.elim_cnt - 1, rhs);
+  // border system (G - W^T W) x_c = r_c - W^T w
+  if (pl.elim_cnt) {
+    const int rt = R / 16, lt = rt * (rt + 1) / 2;
+    hipLaunchKernelGGL(k_arw_gram, dim3(xcd_grid(lt)), dim3(64), 0, st, a, elim, pl.elim_cnt, d.bd_A, pl.Rp, lt);
+    hipLaunchKernelGGL(k_arw_gvec, dim3((R + 63) / 64), dim3(256), 0, st, a, elim, pl.elim_cnt, d.bd_r);
+  }
+  launch_dense_spd_solve(d.bd_A, d.bd_L, d.bd_Linv, d.bd_r, d.bd_x, d.flags, pl.Rp, st);
+  // x_b = P L^-T (w - W x_c)
+  if (pl.elim_cnt)
+    hipLaunchKernelGGL(k_arw_correct, dim3((pl.elim_cnt * n + 3) / 4), dim3(256), 0, st, a, elim, pl.elim_cnt, d.bd_x);
+  hipLaunchKernelGGL(k_arw_top_back, dim3(1), dim3(128), 0, st, a, d.cr_x);
+  for (h /= 2; h >= 1; h /= 2) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
+    hipLaunchKernelGGL(k_cr_back, dim3(n_odd), dim3(64 * nt), (size_t)n * sizeof(double), st, v, h);
+  }
 }
 
 // Levels, top solve and back substitution on D/E/g already in CR layout.
@@ -1252,9 +1457,11 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
     const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
     if (hipMemsetAsync(d.cr_D, 0, blkbytes, st) != hipSuccess) return -2;
     if (hipMemsetAsync(d.cr_E, 0, blkbytes, st) != hipSuccess) return -2;
+    if (pl.R) launch_arrow_clear(d, pl, st);
     hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
   }
-  launch_cr_core(d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
+  if (pl.R) launch_arrow_solve(d, pl, st);
+  else launch_cr_core(d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
   hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }

@@ -96,6 +96,14 @@ class Context:
         check(lib().sqlm_global_ba(self._h, int(iterations), ptr(stop), C.byref(st), C.byref(n)), "sqlm_global_ba")
         return n.value, st.as_dict()
 
+    def rcs_layout(self) -> dict:
+        """The reduced-camera-system layout of the last optimize() (sqlm_get_rcs_layout)."""
+        out = (C.c_int * 8)()
+        check(lib().sqlm_get_rcs_layout(self._h, out), "sqlm_get_rcs_layout")
+        kind = {0: "none", 1: "band", 2: "band+border", 3: "dense"}[out[0]]
+        return dict(kind=kind, B=out[1], p=out[2], n=out[3], border_cams=out[4], R=out[5], n_free=out[6],
+                    coupled_superblocks=out[7])
+
     def bench(self, warmup: int, n: int):
         ms = C.c_double(0)
         kms = np.zeros(_lib.NKERNEL_TIMERS)

@@ -144,19 +144,39 @@ def pose_through_f32(R: np.ndarray, t: np.ndarray):
 
 def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_window: int = 0,
                  n_fixed: int = 1, seed: int = 0, outlier_frac: float = 0.02, robust: bool = True,
-                 huber_delta: float | None = None, noise: bool = True, perturb: bool = True) -> BAProblem:
+                 huber_delta: float | None = None, noise: bool = True, perturb: bool = True,
+                 loop: int = 0, loop_cams: int = 24) -> BAProblem:
     """Generate a synthetic BA problem.
 
     pair_window > 0 selects the local-BA layout of config 2: every landmark has
     exactly two observers, the second within ``pair_window`` keyframes of the
-    first. Otherwise k ~ U{k_min..k_max} consecutive keyframes (config 4)."""
+    first. Otherwise k ~ U{k_min..k_max} consecutive keyframes (config 4).
+
+    loop > 0 closes the trajectory: the keyframes drive a circle of
+    circumference n_kf - loop metres (1 m per keyframe) and the last ``loop``
+    keyframes revisit the places of the first ``loop`` ones, 0.5 m to the side.
+    Every landmark is also observed by the keyframes of the other pass at the
+    places of its track (its "twins", up to ``loop_cams`` observers in all), as
+    a loop-closed map is after LoopClosing::CorrectLoop fuses the matched
+    points (src/backend/LoopClosing.cc:863-877): the reduced camera system then
+    couples keyframes 0.. with n_kf - loop.. far off its band."""
     rng = SplitMix64(seed)
     fx, fy, cx, cy = KITTI_INTR
     W, H = KITTI_WH
     idx = np.arange(n_kf)
-    yaw = 0.02 * np.sin(idx / 10.0)
+    if loop > 0:
+        Lc = n_kf - loop
+        place = np.where(idx < Lc, idx, idx - Lc)
+        th = 2.0 * np.pi * place / Lc
+        rad = Lc / (2.0 * np.pi)
+        yaw = th + 0.02 * np.sin(idx / 10.0)
+        side = np.where(idx < Lc, 0.0, 0.5)
+        c = np.stack([rad * (1.0 - np.cos(th)) + side * np.cos(th), np.zeros(n_kf),
+                      rad * np.sin(th) - side * np.sin(th)], axis=1)
+    else:
+        yaw = 0.02 * np.sin(idx / 10.0)
+        c = np.stack([np.zeros(n_kf), np.zeros(n_kf), idx * 1.0], axis=1)
     R_wc = _rot_y(yaw)
-    c = np.stack([np.zeros(n_kf), np.zeros(n_kf), idx * 1.0], axis=1)
     R_cw = np.transpose(R_wc, (0, 2, 1))
     t_cw = -np.einsum("nij,nj->ni", R_cw, c)
 
@@ -192,7 +212,19 @@ def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_
         starts = np.repeat(a, k)
         first = np.repeat(np.cumsum(k) - k, k)
         kf = starts + (np.arange(lm.size) - first)
-    Xc = np.einsum("nij,nj->ni", R_cw[kf], X[lm]) + t_cw[kf]
+    if loop > 0:
+        # twins: the other pass's keyframe at the place of each track keyframe,
+        # in track order, while the landmark has fewer than loop_cams observers
+        Lc = n_kf - loop
+        tw = np.where(kf < loop, kf + Lc, np.where(kf >= Lc, kf - Lc, -1))
+        cand = tw >= 0
+        cnt = np.bincount(lm[cand], minlength=n_lm)
+        rank_in_lm = np.cumsum(cand) - 1 - (np.cumsum(cnt) - cnt)[lm]  # lm is grouped, ascending
+        room = loop_cams - k[lm]
+        sel = cand & (rank_in_lm < room)
+        lm = np.concatenate([lm, lm[sel]])
+        kf = np.concatenate([kf, tw[sel]])
+    Xc =np.einsum("nij,nj->ni", R_cw[kf], X[lm]) + t_cw[kf]
     u = fx * Xc[:, 0] / Xc[:, 2] + cx
     v = fy * Xc[:, 1] / Xc[:, 2] + cy
     vis = (Xc[:, 2] > 0.5) & (u >= 0) & (u < W) & (v >= 0) & (v < H)
@@ -279,6 +311,19 @@ def config4(seed: int = 4, scale: float = 1.0, **kw) -> BAProblem:
     n_lm = max(100, int(round(500000 * scale)))
     kw.setdefault("robust", False)
     return make_problem(n_kf, n_lm, k_min=2, k_max=18, n_fixed=1, seed=seed, **kw)
+
+
+def config4_loop(seed: int = 4, scale: float = 1.0, loop: int = 30, **kw) -> BAProblem:
+    """Config 4 on a loop-closed map, the shape the reference's GBA always has
+    (it only runs after a loop closure: LoopClosing.cc:877, :987-991): a
+    circular trajectory whose last ``loop`` keyframes revisit the first ones,
+    every landmark at those places also observed from the other pass (a few
+    thousand landmarks co-observed by KF 0..~47 and KF n-loop..n-1). Same
+    counts, track lengths and GBA schedule as config 4 otherwise."""
+    n_kf = max(20, int(round(5000 * scale)))
+    n_lm = max(100, int(round(500000 * scale)))
+    kw.setdefault("robust", False)
+    return make_problem(n_kf, n_lm, k_min=2, k_max=18, n_fixed=1, seed=seed, loop=min(loop, n_kf // 4), **kw)
 
 
 def add_lidar_flat(prob: BAProblem, pose: int, n: int, *, seed: int = 0, noise: float = 0.01,
