@@ -46,6 +46,14 @@ def make_workload(name: str, scale: float):
         desc = {"workload": "synthetic global BA (BASELINE config 4)", "n_pose": prob.n_pose,
                 "n_landmark": prob.n_pt, "n_obs": prob.n_obs, "track_len": "U{2..18}", "robust": False,
                 "seed": 4, "scale": scale}
+    elif name == "gba_loop":
+        # the shape the reference's GBA always has: it only runs after a loop
+        # closure (LoopClosing.cc:877, :987-991), so S couples the revisited
+        # keyframes far off its band (band + border solve)
+        prob = synth.config4_loop(seed=4, scale=scale)
+        desc = {"workload": "synthetic loop-closed global BA (BASELINE config 4 + 30-KF loop closure)",
+                "n_pose": prob.n_pose, "n_landmark": prob.n_pt, "n_obs": prob.n_obs, "track_len": "U{2..18}",
+                "loop_kf": 30, "robust": False, "seed": 4, "scale": scale}
     else:
         prob = synth.config2(seed=2)
         desc = {"workload": "synthetic local BA (BASELINE config 2)", "n_pose": prob.n_pose,
@@ -146,6 +154,25 @@ def reprojection_sse(p, q, t, X):
     return float(np.sum(e * e)), float(p.n_obs)
 
 
+def host_cpu() -> dict:
+    """CPU model and core counts of the host the baseline ran on (lscpu's
+    model name from /proc/cpuinfo; nproc = the cores this process may use)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": usable, "machine_cpus": os.cpu_count()}
+
+
 def cpu_baseline(prob, name: str):
     """Single-threaded oracle (g2o-semantics port, G2O_USE_OPENMP=OFF like the
     reference build) on a bounded sample of the same workload: a fixed number of
@@ -157,12 +184,12 @@ def cpu_baseline(prob, name: str):
     while True:
         g = O.OracleGraph(prob)
         t0 = time.perf_counter()
-        n, st = g.optimize(0, 8 if name == "gba" else 10)
+        n, st = g.optimize(0, 8 if name.startswith("gba") else 10)
         total_dt += time.perf_counter() - t0
         total_n += max(n, 1)
         runs += 1
         del g
-        if name == "gba" or total_dt >= 10.0:
+        if name.startswith("gba") or total_dt >= 10.0:
             break
     return {"value": total_n / total_dt, "unit": "LM iterations/s", "cores": 1, "kind": "port",
             "sample": f"{total_n} LM iterations ({runs} x optimize()) on the full {name} workload, "
@@ -379,7 +406,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["gba", "lba", "eg", "orb"], default="gba")
+    ap.add_argument("--config", choices=["gba", "gba_loop", "lba", "eg", "orb"], default="gba")
     ap.add_argument("--scale", type=float, default=1.0, help="shrink config 4 (parity / debugging only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
@@ -429,7 +456,7 @@ def main():
                "lm_iterations": int(sum(x["iterations"] for x in sts)),
                "setup_ms": float(sum(x["ms_setup"] for x in sts)), "optimize_ms": float(sum(x["ms_total"] for x in sts)),
                "what": "sqlm_set_problem + sqlm_local_ba (3-pass schedule) + sqlm_get_poses/points, host buffers"}
-    if world == 1 and args.config == "gba":
+    if world == 1 and args.config in ("gba", "gba_loop"):
         # the drop-in call as the reference makes it (GlobalBundleAdjustemnt, 10
         # iterations): host arrays in, setup (sorting, tiles, H2D), the solve,
         # results out (D2H) — reported beside the metric, never as `value`

@@ -153,7 +153,7 @@ enum BufId {
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
-  B_BDR, B_BDX
+  B_BDR, B_BDX, B_LONGS, B_LONGG
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -162,7 +162,9 @@ enum BufId {
 struct TilePlan {
   std::vector<int> lm_ptr{0}, cam_ptr{0}, cams, obs_local, ld, red_ptr, gred_ptr;
   std::vector<int2> urange, gred_idx;
-  std::vector<int64_t> red_off;  // absolute offset (doubles) of each contribution's 6x6 block in part
+  std::vector<int64_t> red_off;   // absolute offset (doubles) of each contribution's 6x6 block in part
+  std::vector<int64_t> gred_off;  // ... and of each g contribution's 6 doubles in gpart
+  std::vector<int> long_s, long_g;  // S blocks / cameras with more than kRedLong contributions
   std::vector<int64_t> part_ptr{0}, gpart_ptr{0};
   int max_cp = 0;
   bool dups = false;
@@ -291,6 +293,13 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::ve
   tp.red_off.resize(red_idx.size());
   for (size_t k = 0; k < red_idx.size(); ++k) tp.red_off[k] = tp.part_ptr[red_idx[k].x] + 36 * (int64_t)red_idx[k].y;
   csr(gred, nP, tp.gred_ptr, tp.gred_idx);
+  tp.gred_off.resize(tp.gred_idx.size());
+  for (size_t k = 0; k < tp.gred_idx.size(); ++k)
+    tp.gred_off[k] = tp.gpart_ptr[tp.gred_idx[k].x] + 6 * (int64_t)tp.gred_idx[k].y;
+  for (int s = 0; s < s_row[nP]; ++s)
+    if (tp.red_ptr[s + 1] - tp.red_ptr[s] > kRedLong) tp.long_s.push_back(s);
+  for (int i = 0; i < nP; ++i)
+    if (tp.gred_ptr[i + 1] - tp.gred_ptr[i] > kRedLong) tp.long_g.push_back(i);
 }
 
 // Reduced-camera-system solver plan from the upper block pattern of S (hidx
@@ -627,6 +636,17 @@ int prepare(sqlm_ctx *c, int level) {
   phase("S pattern");
   build_tiles(nP, nL, lm_begin, obs_camh, s_row, s_col, lm_cap, tp);
   phase("tiles");
+  if (ptime) {  // plan shape: tile count, longest reduction lists, solver layout
+    int rmax = 0, gmax = 0;
+    for (size_t s = 0; s + 1 < tp.red_ptr.size(); ++s) rmax = std::max(rmax, tp.red_ptr[s + 1] - tp.red_ptr[s]);
+    for (size_t s = 0; s + 1 < tp.gred_ptr.size(); ++s) gmax = std::max(gmax, tp.gred_ptr[s + 1] - tp.gred_ptr[s]);
+    std::fprintf(stderr,
+                 "prepare plan: nP %d nL %d nnzb %d tiles %zu max_cp %d red %zu (max/block %d, long %zu) gred max %d "
+                 "(long %zu) | CR %d B %d p %d n %d border %d R %d init %d elim %d\n",
+                 nP, nL, s_row[nP], tp.lm_ptr.size() - 1, tp.max_cp, tp.red_off.size(), rmax, tp.long_s.size(), gmax,
+                 tp.long_g.size(),
+                 (int)c->cr.enabled, c->cr.B, c->cr.p, c->cr.n, c->cr.nbc, c->cr.R, c->cr.init_cnt, c->cr.elim_cnt);
+  }
   c->use_tiles = nP > 0 && tp.max_cp <= kTileHardCams;
   c->tile_max_cp = tp.max_cp;
   c->tile_max_k = 0;
@@ -703,6 +723,7 @@ int prepare(sqlm_ctx *c, int level) {
     for (int sl = 0; sl < nL; ++sl) mk = std::max(mk, lm_begin[sl + 1] - lm_begin[sl]);
     d.tile_maxk = mk;
   }
+  d.n_long_s = d.n_long_g = 0;
   if (c->use_tiles) {
     UP(B_TLM, tp.lm_ptr, d.tile_lm_ptr);
     UP(B_TCAMP, tp.cam_ptr, d.tile_cam_ptr);
@@ -717,7 +738,11 @@ int prepare(sqlm_ctx *c, int level) {
     UP(B_REDP, tp.red_ptr, d.red_ptr);
     UP(B_REDI, tp.red_off, d.red_off);
     UP(B_GREDP, tp.gred_ptr, d.gred_ptr);
-    UP(B_GREDI, tp.gred_idx, d.gred_idx);
+    UP(B_GREDI, tp.gred_off, d.gred_off);
+    UP(B_LONGS, tp.long_s, d.long_s);
+    UP(B_LONGG, tp.long_g, d.long_g);
+    d.n_long_s = (int)tp.long_s.size();
+    d.n_long_g = (int)tp.long_g.size();
   }
   UP(B_OBSLM, obs_lm, d.obs_lm);
   UP(B_OBSCAM, obs_cam, d.obs_cam);

@@ -97,7 +97,11 @@ struct DevProblem {
   int *red_ptr = nullptr;                   // [nnzb+1] S block -> contributions
   int64_t *red_off = nullptr;               //   offset in part of the contribution's 36-double block
   int *gred_ptr = nullptr;                  // [nP+1] camera -> contributions
-  int2 *gred_idx = nullptr;                 //   (tile, u)
+  int64_t *gred_off = nullptr;              //   offset in gpart of the contribution's 6 doubles
+  // S blocks / g rows with more than kRedLong contributions (loop-closure
+  // cameras: hundreds) are summed by a whole workgroup each
+  int n_long_s = 0, n_long_g = 0;
+  int *long_s = nullptr, *long_g = nullptr;
   int tile_dups = 0;                        // some landmark observed twice by one camera
   int tile_maxk = 0;                        // longest track (staging fast path needs <= kTileFastK = 64)
   // block-tridiagonal cyclic reduction workspace (sqlm_rcs_solve.hip)
@@ -213,6 +217,7 @@ void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st);
 #ifdef SQLM_TILE_PROF
 int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase counters
 #endif
+constexpr int kRedLong = 24;
 constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);  // zeroes + scatters unless cr_direct

@@ -1097,73 +1097,119 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
   }
 }
 
-// S block s = sum of its tile partials (tile order) + H_pp + lambda I on the
-// diagonal; g row i likewise. Each contribution is one 36-double block of a
-// tile's block-major partial (tile_blk). With cr_direct the sums go
-// straight into the block-tridiagonal superblocks of the CR solver (D_I and
-// its mirror, E_I = S(I, I+1), g_I, identity on padded rows), replacing the
-// BSR copy and its scatter.
-__global__ __launch_bounds__(256) void k_rcs_reduce(DevProblem d, double lambda) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// S block s = sum of its tile partials + H_pp + lambda I on the diagonal; g
+// row i likewise. Each contribution is one 36-double block of a tile's
+// block-major partial (tile_blk), or 6 doubles of its g partial, at a
+// host-precomputed offset. With cr_direct the sums go straight into the
+// block-tridiagonal superblocks of the CR solver (D_I and its mirror,
+// E_I = S(I, I+1), g_I, identity on padded rows) or, on a band + border layout,
+// into F^T / the border system, replacing the BSR copy and its scatter.
+//
+// Summation order is fixed (deterministic, no atomics): a list of up to
+// kRedLong contributions is summed by one thread in list order, eight loads in
+// flight; a longer one (the cameras of a loop closure collect hundreds) by a
+// workgroup, groups of threads taking every G-th contribution, the group sums
+// then added in group order.
+__device__ __forceinline__ void rcs_put_s(const DevProblem &d, int s, int e, double v, double lambda) {
+  const int r = e / 6, c = e % 6;
   const bool own = !d.sharded || d.rank == 0;
-  if (gid < d.nnzb * 36) {
-    const int s = (int)(gid / 36), e = (int)(gid % 36), r = e / 6, c = e % 6;
-    double v = 0.0;
-    const int k0 = d.red_ptr[s], k1 = d.red_ptr[s + 1];
-    for (int k = k0; k < k1; k += 4) {  // four contributions' loads in flight, summed in list order
-      double p4[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) p4[u] = k + u < k1 ? d.part[d.red_off[k + u] + e] : 0.0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v += p4[u];
-    }
-    const int j = d.s_col[s];
-    if (s == d.s_row_ptr[j]) {  // diagonal block (first block of row j); sharded: this rank's share
-      v += d.Hpp[36 * j + e];
-      if (r == c && own) v += lambda;
-    }
-    if (!d.cr_direct) {
-      d.S[gid] = v;
+  const int j = d.s_col[s];
+  if (s == d.s_row_ptr[j]) {  // diagonal block (first block of row j); sharded: this rank's share
+    v += d.Hpp[36 * j + e];
+    if (r == c && own) v += lambda;
+  }
+  if (!d.cr_direct) {
+    d.S[(int64_t)s * 36 + e] = v;
+    return;
+  }
+  const int i = d.s_row[s], n = d.cr_n, B = d.cr_B;
+  const int pi = d.cam_pos ? d.cam_pos[i] : i, pj = d.cam_pos ? d.cam_pos[j] : j;
+  if (pi >= 0 && pj >= 0) {  // band (positions ascend with the camera index)
+    const int I = pi / B, li = pi - I * B, J = pj / B, lj = pj - J * B;
+    double *base = (J == I ? d.cr_D : d.cr_E) + (size_t)I * n * n;
+    base[(6 * li + r) * n + 6 * lj + c] = v;
+    if (J == I && j != i) base[(6 * lj + c) * n + 6 * li + r] = v;
+  } else if (pi >= 0) {  // band row, border column: F^T
+    const int I = pi / B, li = pi - I * B;
+    d.arw_G[((size_t)I * n + 6 * li + r) * d.arw_R + 6 * (-1 - pj) + c] = v;
+  } else if (pj >= 0) {
+    const int J = pj / B, lj = pj - J * B;
+    d.arw_G[((size_t)J * n + 6 * lj + c) * d.arw_R + 6 * (-1 - pi) + r] = v;
+  } else {  // border system, both triangles
+    const int bi = -1 - pi, bj = -1 - pj;
+    d.bd_A[(size_t)(6 * bi + r) * d.arw_Rp + 6 * bj + c] = v;
+    d.bd_A[(size_t)(6 * bj + c) * d.arw_Rp + 6 * bi + r] = v;
+  }
+}
+
+__device__ __forceinline__ void rcs_put_g(const DevProblem &d, int i, int r, double v) {
+  v += d.bp[8 * i + r];
+  d.g[6 * i + r] = v;
+  if (d.cr_direct) {
+    const int pi = d.cam_pos ? d.cam_pos[i] : i;
+    if (pi >= 0) {
+      const int I = pi / d.cr_B, li = pi - I * d.cr_B;
+      d.cr_g[(size_t)I * d.cr_n + 6 * li + r] = v;
     } else {
-      const int i = d.s_row[s], n = d.cr_n, B = d.cr_B;
-      const int pi = d.cam_pos ? d.cam_pos[i] : i, pj = d.cam_pos ? d.cam_pos[j] : j;
-      if (pi >= 0 && pj >= 0) {  // band (positions ascend with the camera index)
-        const int I = pi / B, li = pi - I * B, J = pj / B, lj = pj - J * B;
-        double *base = (J == I ? d.cr_D : d.cr_E) + (size_t)I * n * n;
-        base[(6 * li + r) * n + 6 * lj + c] = v;
-        if (J == I && j != i) base[(6 * lj + c) * n + 6 * li + r] = v;
-      } else if (pi >= 0) {  // band row, border column: F^T
-        const int I = pi / B, li = pi - I * B;
-        d.arw_G[((size_t)I * n + 6 * li + r) * d.arw_R + 6 * (-1 - pj) + c] = v;
-      } else if (pj >= 0) {
-        const int J = pj / B, lj = pj - J * B;
-        d.arw_G[((size_t)J * n + 6 * lj + c) * d.arw_R + 6 * (-1 - pi) + r] = v;
-      } else {  // border system, both triangles
-        const int bi = -1 - pi, bj = -1 - pj;
-        d.bd_A[(size_t)(6 * bi + r) * d.arw_Rp + 6 * bj + c] = v;
-        d.bd_A[(size_t)(6 * bj + c) * d.arw_Rp + 6 * bi + r] = v;
+      d.bd_r[6 * (-1 - pi) + r] = v;
+    }
+  }
+}
+
+// sum of src[off[k] + e] over k = k0, k0 + step, ... < k1 in that order, eight loads in flight
+__device__ __forceinline__ double red_sum(const double *src, const int64_t *off, int k0, int k1, int step, int e) {
+  double v = 0.0;
+  for (int k = k0; k < k1; k += 8 * step) {
+    double p8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p8[u] = k + u * step < k1 ? src[off[k + u * step] + e] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v += p8[u];
+  }
+  return v;
+}
+
+constexpr int kRedThreads = 256;
+constexpr int kRedGroupsS = kRedThreads / 36, kRedGroupsG = kRedThreads / 6;
+
+__global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double lambda, int short_blocks) {
+  if ((int)blockIdx.x >= short_blocks) {  // one long S block or g row per workgroup
+    __shared__ double part[kRedThreads];
+    const int w = blockIdx.x - short_blocks, tid = threadIdx.x;
+    if (w < d.n_long_s) {
+      const int s = d.long_s[w], e = tid % 36, grp = tid / 36;
+      const int k0 = d.red_ptr[s], k1 = d.red_ptr[s + 1];
+      if (grp < kRedGroupsS) part[tid] = red_sum(d.part, d.red_off, k0 + grp, k1, kRedGroupsS, e);
+      __syncthreads();
+      if (tid < 36) {
+        double v = 0.0;
+        for (int g = 0; g < kRedGroupsS; ++g) v += part[36 * g + tid];
+        rcs_put_s(d, s, tid, v, lambda);
+      }
+    } else {
+      const int i = d.long_g[w - d.n_long_s], e = tid % 6, grp = tid / 6;
+      const int k0 = d.gred_ptr[i], k1 = d.gred_ptr[i + 1];
+      if (grp < kRedGroupsG) part[tid] = red_sum(d.gpart, d.gred_off, k0 + grp, k1, kRedGroupsG, e);
+      __syncthreads();
+      if (tid < 6) {
+        double v = 0.0;
+        for (int g = 0; g < kRedGroupsG; ++g) v += part[6 * g + tid];
+        rcs_put_g(d, i, tid, v);
       }
     }
+    return;
+  }
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid < d.nnzb * 36) {
+    const int s = (int)(gid / 36), e = (int)(gid % 36);
+    const int k0 = d.red_ptr[s], k1 = d.red_ptr[s + 1];
+    if (k1 - k0 <= kRedLong) rcs_put_s(d, s, e, red_sum(d.part, d.red_off, k0, k1, 1, e), lambda);
   }
   const int64_t g2 = gid - d.nnzb * 36;
   if (g2 >= 0 && g2 < (int64_t)d.nP * 6) {
     const int i = (int)(g2 / 6), r = (int)(g2 % 6);
-    double v = 0.0;
-    for (int k = d.gred_ptr[i]; k < d.gred_ptr[i + 1]; ++k) {
-      const int2 ct = d.gred_idx[k];
-      v += d.gpart[d.tile_gpart_ptr[ct.x] + 6 * ct.y + r];
-    }
-    v += d.bp[8 * i + r];
-    d.g[6 * i + r] = v;
-    if (d.cr_direct) {
-      const int pi = d.cam_pos ? d.cam_pos[i] : i;
-      if (pi >= 0) {
-        const int I = pi / d.cr_B, li = pi - I * d.cr_B;
-        d.cr_g[(size_t)I * d.cr_n + 6 * li + r] = v;
-      } else {
-        d.bd_r[6 * (-1 - pi) + r] = v;
-      }
-    }
+    const int k0 = d.gred_ptr[i], k1 = d.gred_ptr[i + 1];
+    if (k1 - k0 <= kRedLong) rcs_put_g(d, i, r, red_sum(d.gpart, d.gred_off, k0, k1, 1, r));
   }
   if (d.cr_direct) {  // identity on the padded rows of every superblock; solve flag
     const int64_t g3 = g2 - (int64_t)d.nP * 6;
@@ -1206,7 +1252,9 @@ int tile_profile_read(long long *out) {
 void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st) {
   if (d.nP == 0) return;
   const int64_t items = d.nnzb * 36 + (int64_t)d.nP * 6 + (d.cr_direct ? (int64_t)d.cr_p * d.cr_n : 0);
-  hipLaunchKernelGGL(k_rcs_reduce, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, d, lambda);
+  const int short_blocks = (int)((items + kRedThreads - 1) / kRedThreads);
+  hipLaunchKernelGGL(k_rcs_reduce, dim3((unsigned)(short_blocks + d.n_long_s + d.n_long_g)), dim3(kRedThreads), 0, st,
+                     d, lambda, short_blocks);
 }
 
 // ---------------------------------------------------------------- dense solve

@@ -1311,22 +1311,28 @@ __global__ __launch_bounds__(64) void k_arw_gram(ArwView a, const int *elim, int
   mm_store(Ab, ldb, ti, tj, acc, -1.0, true);
 }
 
-// rb -= sum_{I in elim} Z_I^T z_I: 64 columns per workgroup, four k-quarters
-// summed in a fixed order
-__global__ __launch_bounds__(256) void k_arw_gvec(ArwView a, const int *elim, int ne, double *rb) {
-  __shared__ double part[4][64];
-  const int cl = threadIdx.x & 63, kq = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+// rb -= sum_{I in elim} Z_I^T z_I: one wavefront per 16 columns (lane: column
+// r16, k-quarter k4), a superblock's n / 4 loads per lane issued before its
+// FMAs, superblocks in list order, the quarters summed at the end
+__global__ __launch_bounds__(64) void k_arw_gvec(ArwView a, const int *elim, int ne, double *rb) {
+  const int lane = threadIdx.x, r16 = lane & 15, k4 = lane >> 4, c = 16 * blockIdx.x + r16;
+  constexpr int S = kCRMaxN / 4;
   double s = 0.0;
-  if (c < a.R) {
-    for (int q = 0; q < ne; ++q) {
-      const int I = elim[q];
-      const double *Z = a.Z + (size_t)I * a.n * a.R, *z = a.g + (size_t)I * a.n;
-      for (int k = kq; k < a.n; k += 4) s += Z[(size_t)k * a.R + c] * z[k];
+  for (int q = 0; q < ne; ++q) {
+    const int I = elim[q];
+    const double *Z = a.Z + (size_t)I * a.n * a.R, *z = a.g + (size_t)I * a.n;
+    double zv[S], gv[S];
+#pragma unroll
+    for (int t = 0; t < S; ++t) {
+      const int k = 4 * t + k4, kc = k < a.n ? k : a.n - 1;
+      zv[t] = Z[(size_t)kc * a.R + c];
+      gv[t] = k < a.n ? z[kc] : 0.0;
     }
+#pragma unroll
+    for (int t = 0; t < S; ++t) s = fma(zv[t], gv[t], s);
   }
-  part[kq][cl] = s;
-  __syncthreads();
-  if (kq == 0 && c < a.R) rb[c] -= ((part[0][cl] + part[1][cl]) + part[2][cl]) + part[3][cl];
+  s = k4_sum(s);
+  if (k4 == 0) rb[c] -= s;
 }
 
 // z_I -= Z_I x_c for I in elim: one wavefront per row
@@ -1409,7 +1415,7 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
   if (pl.elim_cnt) {
     const int rt = R / 16, lt = rt * (rt + 1) / 2;
     hipLaunchKernelGGL(k_arw_gram, dim3(xcd_grid(lt)), dim3(64), 0, st, a, elim, pl.elim_cnt, d.bd_A, pl.Rp, lt);
-    hipLaunchKernelGGL(k_arw_gvec, dim3((R + 63) / 64), dim3(256), 0, st, a, elim, pl.elim_cnt, d.bd_r);
+    hipLaunchKernelGGL(k_arw_gvec, dim3(R / 16), dim3(64), 0, st, a, elim, pl.elim_cnt, d.bd_r);
   }
   launch_dense_spd_solve(d.bd_A, d.bd_L, d.bd_Linv, d.bd_r, d.bd_x, d.flags, pl.Rp, st);
   // x_b = P L^-T (w - W x_c)

@@ -145,7 +145,7 @@ def pose_through_f32(R: np.ndarray, t: np.ndarray):
 def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_window: int = 0,
                  n_fixed: int = 1, seed: int = 0, outlier_frac: float = 0.02, robust: bool = True,
                  huber_delta: float | None = None, noise: bool = True, perturb: bool = True,
-                 loop: int = 0, loop_cams: int = 24) -> BAProblem:
+                 loop: int = 0, loop_cams: int = 24, perturb_center: bool = False) -> BAProblem:
     """Generate a synthetic BA problem.
 
     pair_window > 0 selects the local-BA layout of config 2: every landmark has
@@ -159,7 +159,12 @@ def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_
     places of its track (its "twins", up to ``loop_cams`` observers in all), as
     a loop-closed map is after LoopClosing::CorrectLoop fuses the matched
     points (src/backend/LoopClosing.cc:863-877): the reduced camera system then
-    couples keyframes 0.. with n_kf - loop.. far off its band."""
+    couples keyframes 0.. with n_kf - loop.. far off its band.
+
+    perturb_center: the initial pose error is a rotation about the camera
+    centre plus a displacement of the centre (a drifted keyframe), instead of a
+    perturbation of T_cw = [R | t] itself, whose rotation part swings the
+    centre by |c| x angle (metres at kilometres from the origin)."""
     rng = SplitMix64(seed)
     fx, fy, cx, cy = KITTI_INTR
     W, H = KITTI_WH
@@ -278,7 +283,10 @@ def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_
         dth = rng.normal(3 * free.size).reshape(-1, 3) * np.deg2rad(0.3)
         dt = rng.normal(3 * free.size).reshape(-1, 3) * 0.05
         R0[free] = _so3_exp(dth) @ R0[free]
-        t0[free] = t0[free] + dt
+        if perturb_center:
+            t0[free] = -np.einsum("nij,nj->ni", R0[free], c[free] + dt)
+        else:
+            t0[free] = t0[free] + dt
         X0 = X0 + rng.normal(3 * X0.shape[0]).reshape(-1, 3) * 0.1
     q0, t0 = pose_through_f32(R0, t0)
     X0 = X0.astype(np.float32).astype(np.float64)
@@ -319,10 +327,14 @@ def config4_loop(seed: int = 4, scale: float = 1.0, loop: int = 30, **kw) -> BAP
     circular trajectory whose last ``loop`` keyframes revisit the first ones,
     every landmark at those places also observed from the other pass (a few
     thousand landmarks co-observed by KF 0..~47 and KF n-loop..n-1). Same
-    counts, track lengths and GBA schedule as config 4 otherwise."""
+    counts, track lengths and GBA schedule as config 4 otherwise; the initial
+    error is a drift of every keyframe about its own centre (on a 790 m
+    circle a perturbation of T_cw itself would move centres by metres and put
+    points behind cameras)."""
     n_kf = max(20, int(round(5000 * scale)))
     n_lm = max(100, int(round(500000 * scale)))
     kw.setdefault("robust", False)
+    kw.setdefault("perturb_center", True)
     return make_problem(n_kf, n_lm, k_min=2, k_max=18, n_fixed=1, seed=seed, loop=min(loop, n_kf // 4), **kw)
 
 
