@@ -9,6 +9,7 @@
 // ascending mnId (g2o vertex ids mnId / mnId + maxKFid + 1), edges in
 // insertion order (point list order, then GetObservations() map order).
 #include "backend/hipOptimizer.h"
+#include "backend/g2oOptimizer.h"  // fallback for the configurations libsqrtlm does not cover
 
 #include <pcl/common/transforms.h>
 #include <pcl/kdtree/kdtree_flann.h>
@@ -222,11 +223,7 @@ void build_lba(KeyFrame* pKF, SeamGraph& g, std::vector<KeyFrame*>& local, std::
 void lidar_pairs(KeyFrame* pKF, const std::vector<KeyFrame*>& local, const SeamGraph& g,
                  const std::vector<double>& q, const std::vector<double>& t, const lidarConfig* cfg,
                  SeamGraph& out) {
-  if (!cfg) return;
-  if (cfg->using_sharp_point)
-    std::cerr << "hipOptimizer: EdgeLidarCornerPoint is not implemented by libsqrtlm; corner pairs skipped"
-              << std::endl;
-  if (!cfg->using_flat_point) return;
+  if (!cfg || !cfg->using_flat_point) return;  // corner points: LocalBundleAdjustment routes to g2o
   auto world_of = [&](KeyFrame* k) {
     const int i = g.kf_index.at(k);
     float T[16];
@@ -299,6 +296,19 @@ bool hipOptimizer::CaptureEnabled() { return capture_dir() != nullptr; }
 // ---------------------------------------------------------------- LBA
 
 void hipOptimizer::LocalBundleAdjustment(KeyFrame* pKF, bool* pbStopFlag, Map* pMap, const lidarConfig* cfg) {
+  if (cfg && cfg->using_sharp_point) {
+    // EdgeLidarCornerPoint (pass 3 with using_sharp_point, lidarOdom.cc's ROS
+    // default) is not implemented by libsqrtlm: run the reference backend for
+    // this call instead of silently dropping the corner constraints
+    static bool warned = false;
+    if (!warned) {
+      std::cerr << "hipOptimizer: using_sharp_point=1 -> g2oOptimizer::LocalBundleAdjustment "
+                   "(EdgeLidarCornerPoint not implemented by libsqrtlm)" << std::endl;
+      warned = true;
+    }
+    g2oOptimizer::LocalBundleAdjustment(pKF, pbStopFlag, pMap, cfg);
+    return;
+  }
   sqlm_ctx* ctx = thread_ctx();
   if (!ctx) return;
   SeamGraph g;

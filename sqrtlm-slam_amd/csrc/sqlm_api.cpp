@@ -607,14 +607,40 @@ int prepare(sqlm_ctx *c, int level) {
       for (auto &t : th) t.join();
     }
     if (sharded) {
-      // a common pattern for the S all-reduce: the band of the widest shard
-      int bw = 0;
+      // every rank needs the same pattern: the union of the shards' patterns.
+      // Blocks within kNearCams of the diagonal as one flag per (row, offset),
+      // OR-ed by an all-reduce (max); the few far blocks (loop closures) as
+      // (row, column) pairs all-gathered through a summed, zero-padded buffer
+      constexpr int kNearCams = 64;
+      std::vector<uint8_t> near((size_t)nP * kNearCams, 0);
+      std::vector<int> far;
       for (int i = 0; i < nP; ++i)
-        if (rows[i].size() > 1) bw = std::max(bw, rows[i].back() - i);
-      if (comm_allreduce_host(c->comm, &bw, 1, SQLM_DT_I32, SQLM_OP_MAX, c->stream)) return SQLM_ERR_COMM;
+        for (size_t k = 1; k < rows[i].size(); ++k) {
+          const int off = rows[i][k] - i;
+          if (off < kNearCams) near[(size_t)i * kNearCams + off] = 1;
+          else { far.push_back(i); far.push_back(rows[i][k]); }
+        }
+      if (comm_allreduce_host(c->comm, near.data(), (int64_t)near.size(), SQLM_DT_U8, SQLM_OP_MAX, c->stream))
+        return SQLM_ERR_COMM;
+      const int R = c->comm.nranks, me = c->comm.rank;
+      std::vector<int> cnt(R, 0);
+      cnt[me] = (int)far.size();
+      if (comm_allreduce_host(c->comm, cnt.data(), R, SQLM_DT_I32, SQLM_OP_SUM, c->stream)) return SQLM_ERR_COMM;
+      int64_t tot = 0, mine = 0;
+      for (int r = 0; r < R; ++r) { if (r < me) mine += cnt[r]; tot += cnt[r]; }
+      std::vector<int> all((size_t)tot, 0);
+      std::copy(far.begin(), far.end(), all.begin() + mine);
+      if (tot && comm_allreduce_host(c->comm, all.data(), tot, SQLM_DT_I32, SQLM_OP_SUM, c->stream))
+        return SQLM_ERR_COMM;
       for (int i = 0; i < nP; ++i) {
-        rows[i].clear();
-        for (int j = i; j <= std::min(nP - 1, i + bw); ++j) rows[i].push_back(j);
+        rows[i].assign(1, i);
+        for (int off = 1; off < kNearCams && i + off < nP; ++off)
+          if (near[(size_t)i * kNearCams + off]) rows[i].push_back(i + off);
+      }
+      for (int64_t k = 0; k < tot; k += 2) rows[all[k]].push_back(all[k + 1]);
+      for (int i = 0; i < nP; ++i) {
+        std::sort(rows[i].begin() + 1, rows[i].end());
+        rows[i].erase(std::unique(rows[i].begin() + 1, rows[i].end()), rows[i].end());
       }
     }
     for (int i = 0; i < nP; ++i) s_row[i + 1] = s_row[i] + (int)rows[i].size();

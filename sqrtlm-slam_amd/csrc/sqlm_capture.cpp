@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <new>
 #include <vector>
 
 namespace {
@@ -145,6 +146,13 @@ int sqlm_capture_read(const char *path, sqlm_capture **out) {
   *out = nullptr;
   FILE *f = std::fopen(path, "rb");
   if (!f) return SQLM_ERR_INVALID_ARG;
+  // bytes in the file: a section header may not claim more payload than is left
+  int64_t file_size = -1;
+  if (std::fseek(f, 0, SEEK_END) == 0) file_size = (int64_t)std::ftell(f);
+  if (file_size < 0 || std::fseek(f, 0, SEEK_SET) != 0) {
+    std::fclose(f);
+    return SQLM_ERR_INVALID_ARG;
+  }
   char magic[8];
   uint32_t version = 0, kind = 0;
   std::map<uint32_t, Section> secs;
@@ -159,10 +167,20 @@ int sqlm_capture_read(const char *path, sqlm_capture **out) {
       ok = false;
       break;
     }
+    const int64_t pos = (int64_t)std::ftell(f);
+    if (pos < 0 || (uint64_t)elem * count > (uint64_t)(file_size - pos)) {  // truncated / corrupt header
+      ok = false;
+      break;
+    }
     Section s;
     s.elem = elem;
     s.count = count;
-    s.data.resize((size_t)elem * count);
+    try {
+      s.data.resize((size_t)elem * count);
+    } catch (const std::bad_alloc &) {
+      std::fclose(f);
+      return SQLM_ERR_OOM;
+    }
     if (!s.data.empty() && std::fread(s.data.data(), 1, s.data.size(), f) != s.data.size()) {
       ok = false;
       break;

@@ -589,6 +589,7 @@ __device__ __forceinline__ void strip_tiles(const double *L, int ld, const doubl
 // Wave w owns the output column strips w and w + 8 of [A_I | C_I]; both
 // E strips are loaded before the first MFMA.
 __global__ __launch_bounds__(512) void k_cr_factor_elim(CRView v, int h) {
+  static_assert(2 * (kCRMaxN / 16) <= 2 * 8, "two strips per wave of 8 cover at most 16 strips (kCRMaxN <= 128)");
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int fail;
   const int I = h + 2 * h * blockIdx.x;

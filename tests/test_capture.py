@@ -77,6 +77,12 @@ def test_reader_rejects_corrupt_and_skips_unknown(tmp_path):
     capture.write(bad, c)
     with pytest.raises(SqlmError):
         capture.read(bad)
+    # a section header claiming far more payload than the file holds (up to
+    # 64 TiB by its own limits): rejected before anything is allocated
+    huge = tmp_path / "huge.sqcap"
+    huge.write_bytes(src[:16] + struct.pack("<IIQ", 0x4B4E5558, 64, (1 << 40) - 1) + b"\x00" * 64)
+    with pytest.raises(SqlmError):
+        capture.read(huge)
     # unknown trailing section: ignored
     ext = tmp_path / "ext.sqcap"
     ext.write_bytes(src + struct.pack("<IIQ", 0x4B4E5558, 4, 2) + b"\x00" * 8)
@@ -122,7 +128,7 @@ def test_stereo_gba_matches_oracle(gpu_ctx, oracle, robust):
     ng, sg = gpu_ctx.global_ba(10)
     assert ng == nr
     assert sg["iterations"] == sr["iterations"] and sg["trace_trials"] == sr["trace_trials"]
-    np.testing.assert_allclose(sg["trace_chi2"], sr["trace_chi2"], rtol=1e-5)
+    np.testing.assert_allclose(sg["trace_chi2"], sr["trace_chi2"], rtol=TOL)
     q, t = gpu_ctx.poses()
     assert np.abs(q - ref.pose_q).max() < TOL
     assert _rel(t, ref.pose_t) < TOL and _rel(gpu_ctx.points(), ref.pt) < TOL

@@ -6,10 +6,12 @@ What is compared, and why (measured):
     Cholesky, Sim3 update) — estimates within 1e-8 relative;
   * to convergence, noise-free graphs: the same optimum within 1e-9;
   * to convergence with measurement noise: final chi2 within 1e-6 relative and
-    estimates within 1e-4. The LM stops on accept/reject decisions made on
-    chi2 differences at the numeric-Jacobian noise floor (central differences
-    over 1e-9), so the last iteration can differ and the optimum is flat in
-    some directions: iteration counts are not compared.
+    estimates within max(1e-6, 10x the oracle's own sensitivity to a 1-ulp
+    change of one measurement), measured in the test. The LM stops on
+    accept/reject decisions made on chi2 differences at the numeric-Jacobian
+    noise floor (central differences over 1e-9), so the last iteration can
+    differ and the optimum is flat in some directions: iteration counts are
+    not compared.
 Problems use bFixScale = true (stereo / RGB-D, the KITTI case). With a free
 scale, g2o's Sim3(update) (sim3.h:98-104, theta < 1e-5 <= |sigma|) computes
 B = ((sigma^2/2 - sigma + 1) s) / sigma^3, which makes the update erratic; the
@@ -25,6 +27,23 @@ pytestmark = pytest.mark.gpu
 
 def _rel(a, b):
     return np.abs(a - b).max() / max(1.0, np.abs(b).max())
+
+
+def _oracle_sensitivity(oracle, pg, iters, ref_siw):
+    """Relative change of the ORACLE's own result when one edge measurement
+    moves by 1 ulp: the rounding-noise floor of the reference path on this
+    graph (central-difference Jacobians over delta = 1e-9 amplify last-ulp
+    differences of sin / cos / exp, which the GPU's and glibc's libms have)."""
+    p2 = pg.copy()
+    p2.Sji[0, 4] = np.nextafter(p2.Sji[0, 4], 1e9)  # a translation component
+    g = oracle.OracleEG(p2)
+    g.optimize(iters, 1e-16)
+    return _rel(g.Siw, ref_siw)
+
+
+def _tol(oracle, pg, iters, ref_siw):
+    """max(1e-6, 10x the oracle's own 1-ulp sensitivity)."""
+    return max(1e-6, 10.0 * _oracle_sensitivity(oracle, pg, iters, ref_siw))
 
 
 def _both(gpu_ctx, oracle, pg, iters):
@@ -49,7 +68,7 @@ def test_eg_first_iteration_matches(gpu_ctx, oracle, seed):
 def test_eg_free_scale_first_iteration(gpu_ctx, oracle):
     pg = synth.make_pose_graph(60, window=4, n_loops=3, seed=3, noise=False, fix_scale=False)
     ref, sr, sg = _both(gpu_ctx, oracle, pg, 1)
-    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-5
+    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < _tol(oracle, pg, 1, ref.Siw)
 
 
 @pytest.mark.parametrize("seed", [1, 2])
@@ -67,7 +86,7 @@ def test_eg_noisy_same_optimum(gpu_ctx, oracle, seed):
                                trans_noise=5e-4)
     ref, sr, sg = _both(gpu_ctx, oracle, pg, 20)
     assert abs(sg["chi2_end"] - sr["chi2_end"]) <= 1e-6 * sr["chi2_end"]
-    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-4
+    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < _tol(oracle, pg, 20, ref.Siw)
 
 
 def test_eg_facade_writes_back(gpu_ctx, oracle):
@@ -98,7 +117,7 @@ def test_eg_layouts_match(gpu_ctx, oracle, monkeypatch, dense):
     # still creeping down at iteration 20, so the end chi2 is compared at 1e-5
     ref, sr, sg = _both(gpu_ctx, oracle, pg, 20)
     assert abs(sg["chi2_end"] - sr["chi2_end"]) <= 1e-5 * sr["chi2_end"]
-    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < 1e-4
+    assert _rel(gpu_ctx.eg_poses(), ref.Siw) < _tol(oracle, pg, 20, ref.Siw)
     pg = synth.make_pose_graph(500, noise=False, **kw)
     ref, sr, sg = _both(gpu_ctx, oracle, pg, 20)
     assert sg["chi2_end"] < 1e-18 and sr["chi2_end"] < 1e-18

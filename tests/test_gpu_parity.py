@@ -11,11 +11,10 @@ from sqrtlm import synth
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-6
-# chi2 traces: an LM path on a converged problem drifts by ~1e-6 after ~15
-# iterations from FP64 rounding order alone (observed on the LiDAR pass); the
-# graded quantities are the final poses / points (TOL) and the decisions
-# (iteration counts, trial counts, outlier tags), which must match exactly.
-TRACE_TOL = 1e-5
+# chi2 traces: the north-star 1e-6 everywhere; the golden LiDAR pass (numeric
+# central-difference Jacobians) widens it to 10x the oracle's own measured
+# 1-ulp sensitivity (test_gpu_matches_golden), like the estimates.
+TRACE_TOL = TOL
 
 
 def _rel(a, b):
@@ -121,7 +120,7 @@ def test_gpu_matches_golden(gpu_ctx, name):
     else:
         n, s = gpu_ctx.global_ba(10)
         assert n == int(exp["pass0_iters"])
-        np.testing.assert_allclose(s["trace_chi2"], exp["pass0_trace_chi2"], rtol=TRACE_TOL)
+        np.testing.assert_allclose(s["trace_chi2"], exp["pass0_trace_chi2"], rtol=max(TRACE_TOL, tol_t))
     q, t = gpu_ctx.poses()
     assert np.abs(q - exp["out_pose_q"]).max() < tol_t
     assert _rel(t, exp["out_pose_t"]) < tol_t
