@@ -173,16 +173,20 @@ def host_cpu() -> dict:
     return {"cpu_model": model, "nproc": usable, "machine_cpus": os.cpu_count()}
 
 
-def cpu_baseline(prob, name: str):
-    """Single-threaded oracle (g2o-semantics port, G2O_USE_OPENMP=OFF like the
-    reference build) on a bounded sample of the same workload: a fixed number of
-    LM iterations of the full config-4 problem, or repeated 10-iteration solves
-    of config 2 until >= 10 s. Only the optimize() calls are timed."""
+def cpu_baseline(prob, name: str, omp: bool = False):
+    """The oracle (g2o-semantics port) on a bounded sample of the same
+    workload: a fixed number of LM iterations of the full config-4 problem, or
+    repeated 10-iteration solves of config 2 until >= 10 s. Only the optimize()
+    calls are timed. Single thread by default, matching the reference build
+    (G2O_USE_OPENMP=OFF, Thirdparty/g2o/build/CMakeCache.txt:175); omp=True is
+    the labelled all-cores variant (g2o's OpenMP loops on OMP_NUM_THREADS
+    threads, bit-identical results). Both are -O2 C, not g2o + Eigen built
+    -O3 -march=native, which cannot be built here."""
     from oracle import oracle as O
     O.build()
     total_n, total_dt, runs = 0, 0.0, 0
     while True:
-        g = O.OracleGraph(prob)
+        g = O.OracleGraph(prob, omp=omp)
         t0 = time.perf_counter()
         n, st = g.optimize(0, 8 if name.startswith("gba") else 10)
         total_dt += time.perf_counter() - t0
@@ -191,9 +195,12 @@ def cpu_baseline(prob, name: str):
         del g
         if name.startswith("gba") or total_dt >= 10.0:
             break
-    return {"value": total_n / total_dt, "unit": "LM iterations/s", "cores": 1, "kind": "port",
-            "sample": f"{total_n} LM iterations ({runs} x optimize()) on the full {name} workload, "
-                      f"single thread, {total_dt:.1f} s of optimize() time"}
+    host = host_cpu()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or host["nproc"] or 1) if omp else 1
+    return dict({"value": total_n / total_dt, "unit": "LM iterations/s", "cores": threads, "kind": "port",
+                 "sample": f"{total_n} LM iterations ({runs} x optimize()) on the full {name} workload, "
+                           f"{threads} thread(s), {total_dt:.1f} s of optimize() time",
+                 "build": "oracle/g2o_ref.c gcc -O2" + (" -fopenmp (ORC_OMP)" if omp else "")}, **host)
 
 
 EG_N_KF = 1500  # KITTI-00 keyframe count of ORB-SLAM2-style mapping (SURVEY.md §8 sizes, config 5: EG 7*#KF)
@@ -296,8 +303,9 @@ def bench_eg(args, world):
             t0 = time.perf_counter()
             nr, _ = ref.optimize(3, 1e-16)
             dt = time.perf_counter() - t0
-            out["cpu_baseline"] = {"value": nr / dt, "unit": "LM iterations/s", "cores": 1, "kind": "port",
-                                   "sample": f"{nr} LM iterations of the same graph, single thread, {dt:.1f} s"}
+            out["cpu_baseline"] = dict({"value": nr / dt, "unit": "LM iterations/s", "cores": 1, "kind": "port",
+                                        "sample": f"{nr} LM iterations of the same graph, single thread, {dt:.1f} s"},
+                                       **host_cpu())
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
@@ -394,8 +402,9 @@ def bench_orb(args, world):
                 OB.extract(p, img)
                 nf += 1
             dt = time.perf_counter() - t0
-            out["cpu_baseline"] = {"value": nf / dt, "unit": "frames/s", "cores": 1, "kind": "port",
-                                   "sample": f"{nf} extractions of the same frame, single thread, {dt:.1f} s"}
+            out["cpu_baseline"] = dict({"value": nf / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+                                        "sample": f"{nf} extractions of the same frame, single thread, {dt:.1f} s"},
+                                       **host_cpu())
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
@@ -524,6 +533,7 @@ def main():
             out["end_to_end"] = e2e
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(prob, args.config)
+            out["cpu_baseline_all_cores"] = cpu_baseline(prob, args.config, omp=True)
         print(json.dumps(out))
     ctx.close()
     if dist is not None:

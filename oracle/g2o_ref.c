@@ -1,9 +1,14 @@
 /*
  * g2o_ref.c — TEST INFRASTRUCTURE (oracle). CPU restatement of the reference
  * g2o bundle-adjustment path. See oracle.h for the file:line map and the
- * "parity unpinned" note. Single-threaded on purpose: the reference builds g2o
+ * "parity unpinned" note. Single-threaded by default: the reference builds g2o
  * with G2O_USE_OPENMP=OFF (Thirdparty/g2o/build/CMakeCache.txt:175), so this is
- * also the CPU baseline ("kind": "port") timed by bench.py.
+ * also the CPU baseline ("kind": "port") timed by bench.py. Built with
+ * -fopenmp -DORC_OMP (liboracle_omp.so) it is the labelled all-cores variant:
+ * the loops g2o parallelises under G2O_OPENMP (sparse_optimizer.cpp:71,
+ * block_solver.hpp:379,527) run on every core, each accumulator owned by one
+ * thread and summed in the serial order, so its results equal the serial
+ * build's bit for bit (tests/test_oracle.py).
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load
  * this library; the product path (libsqrtlm.so) never links or calls it.
@@ -244,6 +249,14 @@ typedef struct {
   double *bschur;        /* [6 nP] */
   skyline sky;
   double *bk_q, *bk_t, *bk_X; /* push/pop backup */
+#ifdef ORC_OMP
+  /* owner-computes lists (ORC_OMP): active mono edges per landmark / per free
+   * pose in id order; per free pose i2 the (landmark, block) pairs with that
+   * row, landmarks ascending; per-landmark Dinv b_l and per-block B Dinv */
+  int64_t *le_ptr, *le, *pe_ptr, *pe, *pl_ptr, *pl_blk;
+  int *pl_lm;
+  double *db, *BDinv, *chi_e;
+#endif
 } lm_ws;
 
 static int cmp_blk(const void *a, const void *b) {
@@ -352,6 +365,45 @@ static int ws_init(lm_ws *w, orc_graph *g, int level) {
   w->bk_q = malloc(sizeof(double) * 4 * (w->nP ? w->nP : 1));
   w->bk_t = malloc(sizeof(double) * 3 * (w->nP ? w->nP : 1));
   w->bk_X = malloc(sizeof(double) * 3 * (w->nL ? w->nL : 1));
+#ifdef ORC_OMP
+  {
+    const int64_t ne = w->n_ae;
+    w->le_ptr = calloc(w->nL + 1, sizeof(int64_t));
+    w->pe_ptr = calloc(w->nP + 1, sizeof(int64_t));
+    w->pl_ptr = calloc(w->nP + 1, sizeof(int64_t));
+    w->le = malloc(sizeof(int64_t) * (ne ? ne : 1));
+    w->pe = malloc(sizeof(int64_t) * (ne ? ne : 1));
+    w->pl_blk = malloc(sizeof(int64_t) * (w->nblk ? w->nblk : 1));
+    w->pl_lm = malloc(sizeof(int) * (w->nblk ? w->nblk : 1));
+    for (int64_t i = 0; i < ne; ++i) {
+      const int64_t e = w->ae[i];
+      w->le_ptr[w->lhid[g->obs_pt[e]] + 1]++;
+      if (w->phid[g->obs_pose[e]] >= 0) w->pe_ptr[w->phid[g->obs_pose[e]] + 1]++;
+    }
+    for (int64_t k = 0; k < w->nblk; ++k) w->pl_ptr[w->blk_row[k] + 1]++;
+    for (int l = 0; l < w->nL; ++l) w->le_ptr[l + 1] += w->le_ptr[l];
+    for (int i = 0; i < w->nP; ++i) { w->pe_ptr[i + 1] += w->pe_ptr[i]; w->pl_ptr[i + 1] += w->pl_ptr[i]; }
+    int64_t *fl = malloc(sizeof(int64_t) * (w->nL + 1)), *fp = malloc(sizeof(int64_t) * (w->nP + 1));
+    memcpy(fl, w->le_ptr, sizeof(int64_t) * (w->nL + 1));
+    memcpy(fp, w->pe_ptr, sizeof(int64_t) * (w->nP + 1));
+    for (int64_t i = 0; i < ne; ++i) {
+      const int64_t e = w->ae[i];
+      w->le[fl[w->lhid[g->obs_pt[e]]]++] = e;
+      if (w->phid[g->obs_pose[e]] >= 0) w->pe[fp[w->phid[g->obs_pose[e]]]++] = e;
+    }
+    memcpy(fp, w->pl_ptr, sizeof(int64_t) * (w->nP + 1));
+    for (int l = 0; l < w->nL; ++l)
+      for (int64_t k = w->col_ptr[l]; k < w->col_ptr[l + 1]; ++k) {
+        const int64_t o = fp[w->blk_row[k]]++;
+        w->pl_blk[o] = k;
+        w->pl_lm[o] = l;
+      }
+    free(fl); free(fp);
+    w->db = malloc(sizeof(double) * 3 * (w->nL ? w->nL : 1));
+    w->BDinv = malloc(sizeof(double) * 18 * (w->nblk ? w->nblk : 1));
+    w->chi_e = malloc(sizeof(double) * (ne ? ne : 1));
+  }
+#endif
   return 1;
 }
 
@@ -361,11 +413,16 @@ static void ws_free(lm_ws *w) {
   free(w->b); free(w->x); free(w->Dinv); free(w->coeff); free(w->bschur);
   free(w->sky.first); free(w->sky.cptr); free(w->sky.val);
   free(w->bk_q); free(w->bk_t); free(w->bk_X);
+#ifdef ORC_OMP
+  free(w->le_ptr); free(w->le); free(w->pe_ptr); free(w->pe); free(w->pl_ptr); free(w->pl_blk); free(w->pl_lm);
+  free(w->db); free(w->BDinv); free(w->chi_e);
+#endif
 }
 
 /* SparseOptimizer::computeActiveErrors (sparse_optimizer.cpp:61-88). */
 static void compute_active_errors(lm_ws *w) {
   orc_graph *g = w->g;
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < w->n_ae; ++i) edge_error(g, w->ae[i]);
   for (int64_t i = 0; i < w->n_al; ++i) lidar_error(g, w->al[i], g->lid_err + w->al[i]);
 }
@@ -374,12 +431,24 @@ static void compute_active_errors(lm_ws *w) {
 static double active_robust_chi2(lm_ws *w) {
   orc_graph *g = w->g;
   double chi = 0.0, rho[2];
+#ifdef ORC_OMP
+  /* per-edge terms in parallel, summed in id order (the serial sum's bits) */
+#pragma omp parallel for schedule(static) private(rho)
+  for (int64_t i = 0; i < w->n_ae; ++i) {
+    int64_t e = w->ae[i];
+    double c = mono_chi2(g, e);
+    if (g->obs_delta[e] > 0.0) { huber(g->obs_delta[e], c, rho); c = rho[0]; }
+    w->chi_e[i] = c;
+  }
+  for (int64_t i = 0; i < w->n_ae; ++i) chi += w->chi_e[i];
+#else
   for (int64_t i = 0; i < w->n_ae; ++i) {
     int64_t e = w->ae[i];
     double c = mono_chi2(g, e);
     if (g->obs_delta[e] > 0.0) { huber(g->obs_delta[e], c, rho); chi += rho[0]; }
     else chi += c;
   }
+#endif
   for (int64_t i = 0; i < w->n_al; ++i) {
     int64_t e = w->al[i];
     double er = g->lid_err[e];
@@ -388,11 +457,113 @@ static double active_robust_chi2(lm_ws *w) {
   return chi;
 }
 
+#ifdef ORC_OMP
+/* One mono / stereo edge linearised as in build_system: Jacobians A (point),
+ * B (pose), -(rho' info) e and the robust weight. */
+static int edge_lin(const orc_graph *g, int64_t e, double A[9], double B[18], double omega_r[3], double *wgt) {
+  const int p = g->obs_pose[e], l = g->obs_pt[e];
+  const int nr = is_stereo(g, e) ? 3 : 2;
+  double er[3];
+  if (nr == 3)
+    orc_stereo_jacobians(g->pose_q + 4 * p, g->pose_t + 3 * p, g->intr + 4 * p, g->pose_bf[p], g->pt + 3 * l, A, B);
+  else
+    orc_mono_jacobians(g->pose_q + 4 * p, g->pose_t + 3 * p, g->intr + 4 * p, g->pt + 3 * l, A, B);
+  er[0] = g->obs_err[2 * e];
+  er[1] = g->obs_err[2 * e + 1];
+  er[2] = nr == 3 ? g->obs_err3[e] : 0.0;
+  const double info = g->obs_info[e];
+  for (int r = 0; r < nr; ++r) omega_r[r] = -(info * er[r]);
+  *wgt = info;
+  if (g->obs_delta[e] > 0.0) {
+    double rho[2];
+    huber(g->obs_delta[e], mono_chi2(g, e), rho);
+    *wgt = rho[1] * info;
+    for (int r = 0; r < nr; ++r) omega_r[r] *= rho[1];
+  }
+  return nr;
+}
+
+/* build_system with one owner per accumulator: landmark blocks (H_ll, b_l,
+ * H_pl) by landmark, pose blocks (H_pp, b_p) by pose, each over its edges in
+ * id order -- the serial loop's summation order, so the same bits. */
+static void build_system_omp(lm_ws *w) {
+  orc_graph *g = w->g;
+  const int np6 = 6 * w->nP;
+  memset(w->Hpp, 0, sizeof(double) * 36 * w->nP);
+  memset(w->Hll, 0, sizeof(double) * 9 * w->nL);
+  memset(w->blk, 0, sizeof(double) * 18 * w->nblk);
+  memset(w->b, 0, sizeof(double) * (np6 + 3 * w->nL));
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int lh = 0; lh < w->nL; ++lh) {
+    double *bl = w->b + np6 + 3 * lh, *H = w->Hll + 9 * lh;
+    for (int64_t k = w->le_ptr[lh]; k < w->le_ptr[lh + 1]; ++k) {
+      const int64_t e = w->le[k];
+      double A[9], B[18], omega_r[3], wgt;
+      const int nr = edge_lin(g, e, A, B, omega_r, &wgt);
+      for (int r = 0; r < 3; ++r) {
+        double sb = 0.0;
+        for (int q = 0; q < nr; ++q) sb += A[q * 3 + r] * omega_r[q];
+        bl[r] += sb;
+        for (int c = 0; c < 3; ++c) {
+          double sh = 0.0;
+          for (int q = 0; q < nr; ++q) sh += (A[q * 3 + r] * wgt) * A[q * 3 + c];
+          H[r * 3 + c] += sh;
+        }
+      }
+      if (w->phid[g->obs_pose[e]] >= 0) {
+        double *Bl = w->blk + 18 * w->edge_blk[e];
+        for (int r = 0; r < 6; ++r)
+          for (int c = 0; c < 3; ++c) {
+            double sh = 0.0;
+            for (int q = 0; q < nr; ++q) sh += (B[q * 6 + r] * wgt) * A[q * 3 + c];
+            Bl[r * 3 + c] += sh;
+          }
+      }
+    }
+  }
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int ph = 0; ph < w->nP; ++ph) {
+    double *bp = w->b + 6 * ph, *Hp = w->Hpp + 36 * ph;
+    for (int64_t k = w->pe_ptr[ph]; k < w->pe_ptr[ph + 1]; ++k) {
+      double A[9], B[18], omega_r[3], wgt;
+      const int nr = edge_lin(g, w->pe[k], A, B, omega_r, &wgt);
+      for (int r = 0; r < 6; ++r) {
+        double sb = 0.0;
+        for (int q = 0; q < nr; ++q) sb += B[q * 6 + r] * omega_r[q];
+        bp[r] += sb;
+        for (int c = 0; c < 6; ++c) {
+          double sh = 0.0;
+          for (int q = 0; q < nr; ++q) sh += (B[q * 6 + r] * wgt) * B[q * 6 + c];
+          Hp[r * 6 + c] += sh;
+        }
+      }
+    }
+  }
+  for (int64_t i = 0; i < w->n_al; ++i) {  /* after every mono edge, as in the serial loop */
+    const int64_t e = w->al[i];
+    const int p = g->lid_pose[e], ph = w->phid[p];
+    double J[6];
+    orc_lidar_jacobian(g->pose_q + 4 * p, g->pose_t + 3 * p, g->lid_pc + 3 * e, g->lid_pw + 3 * e,
+                       g->lid_n + 3 * e, J);
+    const double info = g->lid_info[e], er = g->lid_err[e];
+    double *bp = w->b + 6 * ph, *Hp = w->Hpp + 36 * ph;
+    for (int r = 0; r < 6; ++r) {
+      bp[r] -= (J[r] * info) * er;
+      for (int c = 0; c < 6; ++c) Hp[r * 6 + c] += (J[r] * info) * J[c];
+    }
+  }
+}
+#endif
+
 /* BlockSolver::buildSystem (block_solver.hpp:502-560) with
  * BaseBinaryEdge / BaseUnaryEdge::constructQuadraticForm. */
 static void build_system(lm_ws *w) {
   orc_graph *g = w->g;
   const int np6 = 6 * w->nP;
+#ifdef ORC_OMP
+  build_system_omp(w);
+  return;
+#endif
   memset(w->Hpp, 0, sizeof(double) * 36 * w->nP);
   memset(w->Hll, 0, sizeof(double) * 9 * w->nL);
   memset(w->blk, 0, sizeof(double) * 18 * w->nblk);
@@ -480,10 +651,84 @@ static double max_diagonal(lm_ws *w) {
   return m;
 }
 
+#ifdef ORC_OMP
+/* schur_solve with owners: per landmark Dinv, Dinv b_l and B Dinv (parallel);
+ * S block column i2 (and coeff row i2) by one thread, over the landmarks that
+ * touch it in ascending order -- each entry sums in the serial loop's order. */
+static int schur_solve_omp(lm_ws *w, double lambda) {
+  skyline *s = &w->sky;
+  const int np6 = 6 * w->nP;
+  memset(s->val, 0, sizeof(double) * s->cptr[s->n]);
+  for (int i = 0; i < w->nP; ++i)
+    for (int c = 0; c < 6; ++c)
+      for (int r = 0; r <= c; ++r)
+        *sky_at(s, 6 * i + r, 6 * i + c) = w->Hpp[36 * i + r * 6 + c] + (r == c ? lambda : 0.0);
+  memset(w->coeff, 0, sizeof(double) * np6);
+#pragma omp parallel for schedule(dynamic, 256)
+  for (int l = 0; l < w->nL; ++l) {
+    double D[9];
+    for (int k = 0; k < 9; ++k) D[k] = w->Hll[9 * l + k] + ((k % 4 == 0) ? lambda : 0.0);
+    double *Dinv = w->Dinv + 9 * l;
+    o3_inverse(D, Dinv);
+    const double *bl = w->b + np6 + 3 * l;
+    double *db = w->db + 3 * l;
+    for (int r = 0; r < 3; ++r) db[r] = Dinv[r * 3 + 0] * bl[0] + Dinv[r * 3 + 1] * bl[1] + Dinv[r * 3 + 2] * bl[2];
+    for (int64_t ko = w->col_ptr[l]; ko < w->col_ptr[l + 1]; ++ko) {
+      const double *Bi = w->blk + 18 * ko;
+      double *BDinv = w->BDinv + 18 * ko;
+      for (int r = 0; r < 6; ++r)
+        for (int c = 0; c < 3; ++c)
+          BDinv[r * 3 + c] = Bi[r * 3 + 0] * Dinv[0 * 3 + c] + Bi[r * 3 + 1] * Dinv[1 * 3 + c] + Bi[r * 3 + 2] * Dinv[2 * 3 + c];
+    }
+  }
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int i2 = 0; i2 < w->nP; ++i2) {
+    for (int64_t q = w->pl_ptr[i2]; q < w->pl_ptr[i2 + 1]; ++q) {
+      const int l = w->pl_lm[q];
+      const int64_t ki = w->pl_blk[q];
+      const double *Bj = w->blk + 18 * ki, *db = w->db + 3 * l;
+      for (int r = 0; r < 6; ++r) w->coeff[6 * i2 + r] += Bj[r * 3 + 0] * db[0] + Bj[r * 3 + 1] * db[1] + Bj[r * 3 + 2] * db[2];
+      for (int64_t ko = w->col_ptr[l]; ko <= ki; ++ko) {
+        const int i1 = w->blk_row[ko];
+        const double *BDinv = w->BDinv + 18 * ko;
+        for (int c = 0; c < 6; ++c)
+          for (int r = 0; r < 6; ++r) {
+            if (i1 == i2 && r > c) continue;
+            double v = BDinv[r * 3 + 0] * Bj[c * 3 + 0] + BDinv[r * 3 + 1] * Bj[c * 3 + 1] + BDinv[r * 3 + 2] * Bj[c * 3 + 2];
+            *sky_at(s, 6 * i1 + r, 6 * i2 + c) -= v;
+          }
+      }
+    }
+  }
+  for (int i = 0; i < np6; ++i) w->bschur[i] = w->b[i] - w->coeff[i];
+  if (!sky_factor(s)) return 0;
+  sky_solve(s, w->bschur, w->x);
+#pragma omp parallel for schedule(static)
+  for (int l = 0; l < w->nL; ++l) {
+    double cl[3] = {w->b[np6 + 3 * l], w->b[np6 + 3 * l + 1], w->b[np6 + 3 * l + 2]};
+    for (int64_t k = w->col_ptr[l]; k < w->col_ptr[l + 1]; ++k) {
+      const double *Bk = w->blk + 18 * k, *xp = w->x + 6 * w->blk_row[k];
+      for (int c = 0; c < 3; ++c) {
+        double acc = 0.0;
+        for (int r = 0; r < 6; ++r) acc += Bk[r * 3 + c] * (-xp[r]);
+        cl[c] += acc;
+      }
+    }
+    const double *Dinv = w->Dinv + 9 * l;
+    for (int r = 0; r < 3; ++r)
+      w->x[np6 + 3 * l + r] = Dinv[r * 3 + 0] * cl[0] + Dinv[r * 3 + 1] * cl[1] + Dinv[r * 3 + 2] * cl[2];
+  }
+  return 1;
+}
+#endif
+
 /* BlockSolver::solve (block_solver.hpp:369-483) on the lambda-damped system. */
 static int schur_solve(lm_ws *w, double lambda) {
   skyline *s = &w->sky;
   const int np6 = 6 * w->nP;
+#ifdef ORC_OMP
+  return schur_solve_omp(w, lambda);
+#endif
   /* _Hschur = _Hpp (damped diagonal blocks), off-diagonal pattern zero */
   memset(s->val, 0, sizeof(double) * s->cptr[s->n]);
   for (int i = 0; i < w->nP; ++i)
@@ -547,6 +792,7 @@ static void push_state(lm_ws *w) {
     memcpy(w->bk_q + 4 * i, g->pose_q + 4 * w->pose_of[i], 4 * sizeof(double));
     memcpy(w->bk_t + 3 * i, g->pose_t + 3 * w->pose_of[i], 3 * sizeof(double));
   }
+#pragma omp parallel for schedule(static)
   for (int l = 0; l < w->nL; ++l) memcpy(w->bk_X + 3 * l, g->pt + 3 * w->pt_of[l], 3 * sizeof(double));
 }
 
@@ -556,6 +802,7 @@ static void pop_state(lm_ws *w) {
     memcpy(g->pose_q + 4 * w->pose_of[i], w->bk_q + 4 * i, 4 * sizeof(double));
     memcpy(g->pose_t + 3 * w->pose_of[i], w->bk_t + 3 * i, 3 * sizeof(double));
   }
+#pragma omp parallel for schedule(static)
   for (int l = 0; l < w->nL; ++l) memcpy(g->pt + 3 * w->pt_of[l], w->bk_X + 3 * l, 3 * sizeof(double));
 }
 
@@ -567,6 +814,7 @@ static void apply_update(lm_ws *w) {
     int p = w->pose_of[i];
     ose3_oplus(g->pose_q + 4 * p, g->pose_t + 3 * p, w->x + 6 * i);
   }
+#pragma omp parallel for schedule(static)
   for (int l = 0; l < w->nL; ++l) {
     double *X = g->pt + 3 * w->pt_of[l];
     X[0] += w->x[np6 + 3 * l]; X[1] += w->x[np6 + 3 * l + 1]; X[2] += w->x[np6 + 3 * l + 2];

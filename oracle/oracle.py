@@ -14,6 +14,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_LIB_OMP_PATH = os.path.join(_HERE, "_build", "liboracle_omp.so")  # all-cores variant (ORC_OMP)
 TRACE_MAX = 256
 
 
@@ -46,7 +47,7 @@ class OrcStats(C.Structure):
                     trace_trials=list(self.trace_trials[:n]))
 
 
-_lib = None
+_libs = {}
 
 
 def build() -> str:
@@ -54,17 +55,20 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB_PATH):
+def lib(omp: bool = False) -> C.CDLL:
+    """The serial oracle, or (omp=True) the same restatement built with g2o's
+    OpenMP loops on every core (OMP_NUM_THREADS), bit-identical results."""
+    if omp not in _libs:
+        path = _LIB_OMP_PATH if omp else _LIB_PATH
+        if not os.path.exists(path):
             build()
-        _lib = C.CDLL(_LIB_PATH)
-        _lib.orc_optimize.restype = C.c_int
-        _lib.orc_local_ba.restype = C.c_int
-        _lib.orc_global_ba.restype = C.c_int
-        _lib.orc_lidar_error.restype = C.c_double
-    return _lib
+        L = C.CDLL(path)
+        L.orc_optimize.restype = C.c_int
+        L.orc_local_ba.restype = C.c_int
+        L.orc_global_ba.restype = C.c_int
+        L.orc_lidar_error.restype = C.c_double
+        _libs[omp] = L
+    return _libs[omp]
 
 
 def _p(a):
@@ -74,7 +78,8 @@ def _p(a):
 class OracleGraph:
     """Owns numpy copies of a BAProblem and the orc_graph view over them."""
 
-    def __init__(self, prob):
+    def __init__(self, prob, omp: bool = False):
+        self._omp = omp
         self.pose_q = prob.pose_q.copy()
         self.pose_t = prob.pose_t.copy()
         self.pose_fixed = prob.pose_fixed.copy()
@@ -107,33 +112,33 @@ class OracleGraph:
 
     def optimize(self, level=0, iterations=10, user_lambda=0.0, stop=None):
         st = OrcStats()
-        n = lib().orc_optimize(C.byref(self.g), level, iterations, C.c_double(user_lambda),
+        n = lib(self._omp).orc_optimize(C.byref(self.g), level, iterations, C.c_double(user_lambda),
                                _p(stop), C.byref(st))
         return n, st.as_dict()
 
     def local_ba(self, stop=None):
         st = (OrcStats * 3)()
         outl = np.zeros(self.obs_pose.shape[0], np.uint8)
-        ran = lib().orc_local_ba(C.byref(self.g), _p(stop), _p(outl), st)
+        ran = lib(self._omp).orc_local_ba(C.byref(self.g), _p(stop), _p(outl), st)
         return ran, outl, [s.as_dict() for s in st]
 
     def global_ba(self, iterations=10, stop=None):
         st = OrcStats()
-        n = lib().orc_global_ba(C.byref(self.g), iterations, _p(stop), C.byref(st))
+        n = lib(self._omp).orc_global_ba(C.byref(self.g), iterations, _p(stop), C.byref(st))
         return n, st.as_dict()
 
     def edge_chi2(self):
         out = np.zeros(self.obs_pose.shape[0])
-        lib().orc_edge_chi2(C.byref(self.g), _p(out))
+        lib(self._omp).orc_edge_chi2(C.byref(self.g), _p(out))
         return out
 
     def depth_positive(self):
         out = np.zeros(self.obs_pose.shape[0], np.uint8)
-        lib().orc_depth_positive(C.byref(self.g), _p(out))
+        lib(self._omp).orc_depth_positive(C.byref(self.g), _p(out))
         return out
 
     def compute_errors(self):
-        lib().orc_compute_mono_errors(C.byref(self.g))
+        lib(self._omp).orc_compute_mono_errors(C.byref(self.g))
         return self.obs_err
 
 

@@ -181,3 +181,23 @@ def test_converter_roundtrip(oracle):
         np.testing.assert_allclose(q2, q, atol=1e-6)
         np.testing.assert_allclose(t2, t, atol=1e-5)
         assert q2[3] >= 0
+
+
+@pytest.mark.parametrize("gen", ["window", "config4", "loop"])
+def test_openmp_variant_bit_identical(gen):
+    """liboracle_omp.so (the labelled all-cores CPU baseline) runs g2o's
+    OpenMP loops with one owner per accumulator, summing in the serial order:
+    traces, poses and points equal the serial build's bit for bit."""
+    from oracle import oracle as O
+    if gen == "window":
+        prob = synth.make_problem(20, 800, pair_window=4, n_fixed=3, seed=5, robust=True)
+    elif gen == "config4":
+        prob = synth.config4(scale=0.01, seed=4)
+    else:
+        prob = synth.config4_loop(scale=0.02, loop=8)
+    a, b = O.OracleGraph(prob), O.OracleGraph(prob, omp=True)
+    na, sa = a.global_ba(6) if gen != "window" else a.optimize(0, 8)
+    nb, sb = b.global_ba(6) if gen != "window" else b.optimize(0, 8)
+    assert na == nb and sa == sb
+    for k in ("pose_q", "pose_t", "pt", "obs_err"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
