@@ -888,7 +888,7 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
   // wave w owns the accumulator tiles q with q % kTileWaves == w; 3 waves per SIMD
   // for mono problems (167 VGPRs), 2 with the stereo row (spill-free)
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
-  constexpr int NC = NT * 16, NG = (NC + TH - 1) / TH;
+  constexpr int NC = NT * 16;
   constexpr int BL = kTileBL;
   __shared__ double Ys[2][kTileRows][NC];
   // per-landmark data of the whole tile, loaded once: offsets, camera span, w, R'^-1
@@ -906,9 +906,11 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
   d4v acc[NQW];
 #pragma unroll
   for (int q = 0; q < NQW; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
-  double gacc[NG];
-#pragma unroll
-  for (int m = 0; m < NG; ++m) gacc[m] = 0.0;
+  // gradient column tid - 64 of the tile (waves 1.., while wave 0, which
+  // stages the common batch alone, moves on)
+  static_assert(NT * 16 <= kTileThreads - 64, "one gradient column per thread of waves 1..");
+  const int gcol = tid - 64;
+  double gacc = 0.0;
   for (int k = tid; k < 2 * kTileRows * NC; k += TH) (&Ys[0][0][0])[k] = 0.0;
   const int l0 = d.tile_lm_ptr[t], l1 = d.tile_lm_ptr[t + 1], ntl = l1 - l0;
   const int nbatch = (ntl + BL - 1) / BL;
@@ -947,16 +949,15 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
     }
   };
   if (nbatch > 0) fetch(0);
-  int2 prev = int2{-1, -1};
-  int wrote = -1;  // fast path: offset in Ys[buf] of this thread's staged 3 x 6 block, -1 none
+  int2 prev = int2{-1, -1};  // column span of the previous batch (its buffer is cleared next)
   lds_barrier();
-  int wrote_prev;
   TP_DECL
   for (int bt = 0; bt < nbatch; ++bt) {
     const int buf = bt & 1, lb = BL * bt, nl = min(BL, ntl - lb);
-    wrote_prev = wrote;
     double (*Y)[NC] = Ys[buf];
-    // ---- stage Y rows 4li..4li+2 = R'^-T P for every landmark li of the batch
+    // ---- stage Y rows 4li..4li+2 = R'^-T P for every landmark li of the batch;
+    // meanwhile the waves without observations clear the previous batch's
+    // columns in the other buffer (read by the MFMAs before the last barrier)
     if (!slow) {
       if (pu >= 0) {  // Y block of the observation: (R'^-1)^T jl^T jp, Jacobians recomputed once
         const double *pr = Lc[pu], *xl = Lx[pli], *r = Lr[pli];
@@ -980,9 +981,6 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
           Y[row + 1][col + c] = r[1] * p0 + r[3] * p1;
           Y[row + 2][col + c] = r[2] * p0 + r[4] * p1 + r[5] * p2;
         }
-        wrote = row * NC + col;
-      } else {
-        wrote = -1;
       }
     } else if (tid < 6) {  // repeated cameras / long tracks: serial, observation order
       for (int li = 0; li < nl; ++li) {
@@ -1002,30 +1000,22 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
         }
       }
     }
+    if (prev.x >= 0 && tid >= 64) {  // waves 1.. (wave 0 stages the common case alone)
+#pragma unroll
+      for (int row = 0; row < kTileRows; ++row)
+        for (int col = prev.x + tid - 64; col < prev.y; col += TH - 64) Ys[buf ^ 1][row][col] = 0.0;
+    }
     TP(0);
-    lds_barrier();  // (A) batch staged; every thread is done with the previous batch
+    lds_barrier();  // (A) batch staged, the other buffer clear
     TP(1);
     if (bt + 1 < nbatch) fetch(bt + 1);  // in flight during the MFMAs below
     TP(2);
-    if (!slow) {  // zero exactly the entries this thread staged into the other buffer last batch
-      double *Yo = &Ys[buf ^ 1][0][0];
-      if (bt > 0 && wrote_prev >= 0) {
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          Yo[wrote_prev + c] = 0.0; Yo[wrote_prev + NC + c] = 0.0; Yo[wrote_prev + 2 * NC + c] = 0.0;
-        }
-      }
-    } else if (prev.x >= 0) {  // clear the previous batch's columns in the other buffer
-#pragma unroll
-      for (int row = 0; row < kTileRows; ++row)
-        for (int col = prev.x + tid; col < prev.y; col += TH) Ys[buf ^ 1][row][col] = 0.0;
-    }
-    TP(3);
     int cmin = 1 << 30, cmax = -1;
     for (int li = 0; li < nl; ++li) {
       const int2 ur = Lu[lb + li];
       if (ur.x >= 0) { cmin = min(cmin, 6 * ur.x); cmax = max(cmax, 6 * ur.y + 6); }
     }
+    TP(3);
     if (cmax > 0) {
       const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
       switch (wave) {
@@ -1035,23 +1025,19 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
         default: tile_mfma<NT, 3>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
       }
       TP(4);
-#pragma unroll
-      for (int m = 0; m < NG; ++m) {
-        const int col = tid + TH * m;
-        if (col >= cmin && col < cmax) {
-          double gs = 0.0;
-          for (int li = 0; li < nl; ++li)
-            gs += Y[3 * li][col] * Lw[lb + li][0] + Y[3 * li + 1][col] * Lw[lb + li][1] +
-                  Y[3 * li + 2][col] * Lw[lb + li][2];
-          gacc[m] -= gs;
-        }
+      if (gcol >= cmin && gcol < cmax) {
+        double gs = 0.0;
+        for (int li = 0; li < nl; ++li)
+          gs += Y[3 * li][gcol] * Lw[lb + li][0] + Y[3 * li + 1][gcol] * Lw[lb + li][1] +
+                Y[3 * li + 2][gcol] * Lw[lb + li][2];
+        gacc -= gs;
       }
       prev = int2{cmin, cmax};
     } else {
       prev = int2{-1, -1};
     }
     TP(5);
-    lds_barrier();  // (B) the other buffer is clear before it is staged
+    lds_barrier();  // (B) every wave is done with this buffer before it is cleared
     TP(6);
   }
   TP_STORE;
@@ -1090,11 +1076,7 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
       }
     }
   double *go = d.gpart + d.tile_gpart_ptr[t];
-#pragma unroll
-  for (int m = 0; m < NG; ++m) {
-    const int col = tid + TH * m;
-    if (col < ncol) go[col] = gacc[m];
-  }
+  if (gcol >= 0 && gcol < ncol) go[gcol] = gacc;
 }
 
 // S block s = sum of its tile partials + H_pp + lambda I on the diagonal; g

@@ -17,10 +17,11 @@
 //     broadcasts; the panel solve is row-parallel; the trailing update runs on
 //     the FP64 matrix cores while wave 0 already factors the next diagonal
 //     block (look-ahead); the diagonal inverses are formed in parallel.
-//   * k_cr_factor_elim: the first level (>= 128 odd superblocks) runs the
-//     factor and the A_I / C_I tiles in one workgroup with Linv_I still in
-//     LDS; deeper levels, with few superblocks, keep the tile-parallel
-//     k_cr_elim_gemm, whose tiles spread over every CU (fused there: slower).
+//   * k_cr_factor_elim: every level runs the factor and the A_I / C_I tiles
+//     in one launch with Linv_I still in LDS: one workgroup per odd
+//     superblock on wide levels (>= 128), several on the deep ones, each
+//     factoring redundantly and forming a share of the strips (the tiles
+//     spread over the idle CUs without a second launch).
 //   * k_cr_elim_gemm / k_cr_update_gemm: one wavefront per 16x16 output tile
 //     (v_mfma_f64_16x16x4f64), workgroups remapped so that the tiles of one
 //     superblock run on one XCD and share its L2; only the lower triangle of
@@ -121,8 +122,10 @@ __device__ __forceinline__ void panel_factor(double *L, int ld, int n, int c0, d
     const double t = row[k] * (y * y);
 #pragma unroll
     for (int j = k + 1; j < 16; ++j) row[j] = fma(-t, col[j], row[j]);
-    row[k] = i == k ? pv * y : (i > k ? row[k] * y : row[k]);
-    if (lane == k) myinv = y;
+    // selects, not branches: l_kk = piv y on the pivot row, l_ik = a_ik y below
+    const double scaled = (i == k ? pv : row[k]) * y;
+    row[k] = i >= k ? scaled : row[k];
+    myinv = lane == k ? y : myinv;
   }
   if (lane < 16) {
     if (wave == 0) {
@@ -583,22 +586,27 @@ __device__ __forceinline__ void strip_tiles(const double *L, int ld, const doubl
   }
 }
 
-// Level h, steps 1 + 2 in one workgroup per odd superblock: the factor of
-// k_cr_factor, then A_I = Linv_I E_{I-h}^T and C_I = Linv_I E_I with Linv_I
-// still in LDS (one launch and one global read of Linv_I less per level).
-// Wave w owns the output column strips w and w + 8 of [A_I | C_I]; both
-// E strips are loaded before the first MFMA.
-__global__ __launch_bounds__(512) void k_cr_factor_elim(CRView v, int h) {
-  static_assert(2 * (kCRMaxN / 16) <= 2 * 8, "two strips per wave of 8 cover at most 16 strips (kCRMaxN <= 128)");
+// Level h, steps 1 + 2 fused: the factor of k_cr_factor, then
+// A_I = Linv_I E_{I-h}^T and C_I = Linv_I E_I with Linv_I still in LDS (one
+// launch and one global read of Linv_I less per level). `split` workgroups
+// serve one odd superblock: each factors it (redundantly: the deep levels
+// leave the CUs idle, and the 112-pivot chain is the level's latency either
+// way) and forms every split-th of the 2 n/16 output column strips; only the
+// first stores Linv_I and z_I. Wave w of a workgroup owns its strips w and
+// w + 8; both E strips are loaded before the first MFMA.
+__global__ __launch_bounds__(512) void k_cr_factor_elim(CRView v, int h, int split) {
+  static_assert(kCRMaxN / 16 <= 8, "two strips per wave of 8 cover at most 16 strips (kCRMaxN <= 128)");
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int fail;
-  const int I = h + 2 * h * blockIdx.x;
+  const int ob = blockIdx.x / split, sidx = blockIdx.x - ob * split;
+  const int I = h + 2 * h * ob;
   const int n = v.n, ld = n + 1, nt = n >> 4;
   const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6;
   const int jobs = (I + h < v.p ? 2 : 1) * nt;
-  const int q0 = wave, q1 = wave + nw;
+  const int q0 = sidx + split * wave, q1 = sidx + split * (wave + nw);
   double b0x[kCRMaxN / 8], b0y[kCRMaxN / 8], b1x[kCRMaxN / 8], b1y[kCRMaxN / 8];
-  cr_factor_store(v, I, lds, &fail);
+  if (sidx == 0) cr_factor_store(v, I, lds, &fail);
+  else cr_factor_block(v, I, lds, &fail);
   const double *L = lds, *Dinv = lds + n * ld + 2 * n;
   if (q0 < jobs) {
     if (q0 < nt) load_strip<true>(blk(v.E, I - h, n), n, q0, b0x, b0y);
@@ -611,6 +619,10 @@ __global__ __launch_bounds__(512) void k_cr_factor_elim(CRView v, int h) {
   if (q0 < jobs) strip_tiles(L, ld, Dinv, b0x, b0y, q0 < nt ? blk(v.A, I, n) : blk(v.C, I, n), n, q0 % nt);
   if (q1 < jobs) strip_tiles(L, ld, Dinv, b1x, b1y, q1 < nt ? blk(v.A, I, n) : blk(v.C, I, n), n, q1 % nt);
 }
+
+// Workgroups per odd superblock of the fused factor + elimination: enough to
+// spread a level's strips over the chip (one 134 KB-LDS workgroup per CU)
+inline int cr_split(int n_odd, int nt) { return std::max(1, std::min(2 * nt, 256 / std::max(1, n_odd))); }
 
 // Level h, step 3: every even superblock J absorbs its eliminated neighbours:
 // D_J -= A_{J+h}^T A_{J+h} + C_{J-h}^T C_{J-h} (lower tiles only);
@@ -1397,8 +1409,9 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
     const int fo = pl.lvl[4 * lv], fc = pl.lvl[4 * lv + 1], uo = pl.lvl[4 * lv + 2], uc = pl.lvl[4 * lv + 3];
-    if (fuse_ok && n_odd >= fuse_min) {
-      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd), dim3(512), lds, st, v, h);
+    if (fuse_ok) {
+      const int sp = n_odd >= fuse_min ? 1 : cr_split(n_odd, nt);
+      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd * sp), dim3(512), lds, st, v, h, sp);
     } else {
       hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
       hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
@@ -1443,8 +1456,9 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
   for (; h < p; h *= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
-    if (fuse_ok && n_odd >= fuse_min) {
-      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd), dim3(512), lds, st, v, h);
+    if (fuse_ok) {
+      const int sp = n_odd >= fuse_min ? 1 : cr_split(n_odd, nt);
+      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd * sp), dim3(512), lds, st, v, h, sp);
     } else {
       hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
       hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);

@@ -1,11 +1,13 @@
 """The CR solve's fused factor + elimination (k_cr_factor_elim) against the
 separate launches (k_cr_factor + k_cr_elim_gemm), at every level.
 
-The default fuses only levels with >= 128 odd superblocks (full-size config 4,
-covered by test_gpu_parity.py::test_config4_full_size_two_iterations); here
-SQLM_CR_FUSE_MIN=1 forces the fused kernel onto every level of a 14-superblock
-system, including the last odd block, which has no right neighbour. The two
-schedules run the same MFMA K order, so the results must be bit-identical.
+The default runs every level fused: one workgroup per odd superblock on levels
+with >= 128 of them (full-size config 4), `split` workgroups per superblock
+below (each factors it redundantly and forms a share of the strips).
+SQLM_CR_FUSE_MIN=1 forces one workgroup per superblock on every level of a
+14-superblock system, including the last odd block, which has no right
+neighbour; SQLM_CR_UNFUSED=1 runs the separate launches. All three schedules
+run the same MFMA K order, so the results must be bit-identical.
 The threshold is read once per process, hence one child process per schedule.
 """
 import os
@@ -47,6 +49,8 @@ def _run(tmp_path, tag, env_extra):
 def test_fused_every_level_bit_identical(tmp_path):
     a = _run(tmp_path, "fused", {"SQLM_CR_FUSE_MIN": "1"})
     b = _run(tmp_path, "unfused", {"SQLM_CR_UNFUSED": "1"})
-    assert int(a["n"]) == int(b["n"]) > 0
+    c = _run(tmp_path, "split", {})
+    assert int(a["n"]) == int(b["n"]) == int(c["n"]) > 0
     for k in ("q", "t", "X", "chi2"):
         assert np.array_equal(a[k], b[k]), k
+        assert np.array_equal(c[k], b[k]), k
