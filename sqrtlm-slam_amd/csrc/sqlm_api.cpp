@@ -153,7 +153,7 @@ enum BufId {
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
-  B_BDR, B_BDX, B_LONGS, B_LONGG
+  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -578,6 +578,18 @@ int prepare(sqlm_ctx *c, int level) {
     });
   }
   phase("obs+camcsr");
+  // pose id window of every per-landmark block tile (k_landmark_update)
+  std::vector<int2> upd_rng;
+  for (Bucket &b : c->buckets) {
+    b.rng_off = (int)upd_rng.size();
+    const int spb = kBlock / b.W;
+    for (int s0 = b.slot_begin; s0 < b.slot_end; s0 += spb) {
+      const int s1 = std::min(s0 + spb, b.slot_end);
+      int lo = std::numeric_limits<int>::max(), hi = -1;
+      for (int o = lm_begin[s0]; o < lm_begin[s1]; ++o) { lo = std::min(lo, obs_cam[o]); hi = std::max(hi, obs_cam[o]); }
+      upd_rng.push_back(hi < 0 ? int2{1, 0} : int2{lo, hi});
+    }
+  }
   // reduced-camera-system pattern (upper, diagonal first)
   std::vector<int> s_row(nP + 1, 0), s_col;
   {
@@ -770,6 +782,7 @@ int prepare(sqlm_ctx *c, int level) {
     d.n_long_s = (int)tp.long_s.size();
     d.n_long_g = (int)tp.long_g.size();
   }
+  UP(B_UPDRNG, upd_rng, d.upd_rng);
   UP(B_OBSLM, obs_lm, d.obs_lm);
   UP(B_OBSCAM, obs_cam, d.obs_cam);
   UP(B_OBSCAMH, obs_camh, d.obs_camh);

@@ -101,6 +101,9 @@ struct DevProblem {
   // S blocks / g rows with more than kRedLong contributions (loop-closure
   // cameras: hundreds) are summed by a whole workgroup each
   int n_long_s = 0, n_long_g = 0;
+  // per-landmark kernels: pose id range [x, y] of each block tile's
+  // observations (tiles of kBlock / W consecutive slots, buckets concatenated)
+  int2 *upd_rng = nullptr;
   int *long_s = nullptr, *long_g = nullptr;
   int tile_dups = 0;                        // some landmark observed twice by one camera
   int tile_maxk = 0;                        // longest track (staging fast path needs <= kTileFastK = 64)
@@ -192,6 +195,7 @@ struct Bucket {
   int W;            // segment width
   int slot_begin;   // first landmark slot
   int slot_end;
+  int rng_off = 0;  // first entry of this bucket's tiles in DevProblem::upd_rng
 };
 
 // kernel launchers (sqlm_kernels.hip). All asynchronous on `st`.

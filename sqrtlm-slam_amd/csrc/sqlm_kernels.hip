@@ -20,6 +20,8 @@
 //   k_reduce           deterministic fixed-order sums of the block partials
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <algorithm>
 
 #include "se3_dev.h"
@@ -1319,16 +1321,27 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st) {
 
 // Back-substitution dl = M (b_l - sum_i H_lp,i dx_i), X' = X + dl, then the
 // residuals of the landmark's edges at the trial state (computeActiveErrors).
+// A block's landmarks are consecutive slots (trajectory order), so their
+// observations see a short window of cameras (host-computed per tile, `rng`):
+// the window's poses at both states and its dx are staged in LDS once per
+// tile, and the per-observation gathers read LDS instead of L2. Tiles whose
+// window is wider (loop-closure landmarks) read the global arrays.
+constexpr int kUpdWin = 64;
 template <int W, bool ST, bool SPEC>
 __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
-                                                         double lambda, int part_off) {
+                                                         double lambda, int part_off, const int2 *rng) {
   __shared__ double red[4];
+  __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
   constexpr int SPB = kBlock / W;
   const int lane = threadIdx.x & (W - 1);
   const int nseg = slot_end - slot_begin;
   const int ntiles = (nseg + SPB - 1) / SPB;
   double chi_acc = 0.0, sc_acc = 0.0;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // one tile: P0 / P1 = pose rows (R t fx fy cx cy) at the linearization / trial
+  // state indexed by pose id, DX = dx rows (by pose id in the window, by free
+  // camera otherwise)
+  auto tile_body = [&](int tile, const double *P0, const double *P1, const double *DX, auto in_win) {
+    constexpr bool WIN = decltype(in_win)::value;
     const int seg = tile * SPB + threadIdx.x / W;
     const int slot = slot_begin + seg;
     const bool valid = seg < nseg;
@@ -1343,7 +1356,7 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
     // H_lp dx_cam = jl^T (jp dx_cam), Jacobians recomputed at the linearization point
     auto hlp_dx = [&](const ObsIn &o) {
       if (o.camh < 0) return;
-      const double *prt = d.pose_rt[0] + 16 * o.cam, *dx = d.dx + 6 * o.camh;
+      const double *prt = P0 + 16 * o.cam, *dx = WIN ? DX + 8 * o.cam : DX + 6 * o.camh;
       double x[6];
 #pragma unroll
       for (int k = 0; k < 6; ++k) x[k] = dx[k];
@@ -1391,20 +1404,19 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
         store2(Xo, X0, X1); store2(Xo + 2, X2, 0.0);
         sc_acc += dl0 * (lambda * dl0 + bl[0]) + dl1 * (lambda * dl1 + bl[1]) + dl2 * (lambda * dl2 + bl[2]);
       }
-      const double *prt_all = d.pose_rt[1];
       if (SPEC) {  // the next linearization at the trial state (used if the trial is accepted)
 #pragma unroll
         for (int i = 0; i < kObsPreload; ++i) {
           const int e = beg + lane + i * W;
-          if (e < end) lin_edge<ST>(d, o[i], e, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
+          if (e < end) lin_edge<ST>(d, o[i], e, P1, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
         }
         for (int e = beg + lane + kObsPreload * W; e < end; e += W)
-          lin_edge<ST>(d, load_obs<ST, true>(d, e, true), e, prt_all, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2,
+          lin_edge<ST>(d, load_obs<ST, true>(d, e, true), e, P1, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2,
                        g0, g1, g2, chi);
       } else {
         auto trial_err = [&](const ObsIn &o, int e) {
           MonoEval m;
-          const double *prt = prt_all + 16 * o.cam;
+          const double *prt = P1 + 16 * o.cam;
           if (ST && o.ur >= 0.0) stereo_error(prt, X0, X1, X2, o.u, o.v, o.ur, d.pose_bf[o.cam], o.info, o.delta, m);
           else mono_error(prt, X0, X1, X2, o.u, o.v, o.info, o.delta, m);
           store2(d.obs_err + 2 * e, m.e0, m.e1);
@@ -1429,6 +1441,25 @@ __global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_
       chi = seg_sum<W>(chi);
     }
     if (valid && lane == 0) chi_acc += chi;
+  };
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int2 rg = rng[tile];  // pose id range of the tile's observations (x > y: none)
+    const int nw = rg.y - rg.x + 1;
+    if (nw <= kUpdWin) {
+      __syncthreads();  // the previous tile's readers are done with the window
+      for (int k = threadIdx.x; k < 16 * nw; k += blockDim.x) {
+        Wp0[k] = d.pose_rt[0][16 * rg.x + k];
+        Wp1[k] = d.pose_rt[1][16 * rg.x + k];
+      }
+      for (int k = threadIdx.x; k < 8 * nw; k += blockDim.x) {
+        const int c = k >> 3, r = k & 7, h = d.pose_hidx[rg.x + c];
+        Wdx[k] = (h >= 0 && r < 6) ? d.dx[6 * h + r] : 0.0;
+      }
+      __syncthreads();
+      tile_body(tile, Wp0 - 16 * rg.x, Wp1 - 16 * rg.x, Wdx - 8 * rg.x, std::true_type{});
+    } else {
+      tile_body(tile, d.pose_rt[0], d.pose_rt[1], d.dx, std::false_type{});
+    }
   }
   const double s1 = block_sum(chi_acc, red);
   const double s2 = block_sum(sc_acc, red);
@@ -1445,7 +1476,7 @@ void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda,
   if (nb <= 0) return;
 #define SQLM_LAUNCH(WW, STT, SP) \
   hipLaunchKernelGGL((k_landmark_update<WW, STT, SP>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, \
-                     lambda, part_off)
+                     lambda, part_off, d.upd_rng + b.rng_off)
 #define SQLM_CASE(WW)                                   \
   case WW:                                              \
     if (d.has_stereo) {                                 \
