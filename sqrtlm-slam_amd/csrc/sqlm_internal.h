@@ -189,7 +189,10 @@ __host__ __device__ inline int tile_blk(int u, int w, int cp) { return u * (2 * 
 constexpr int kObsPerLane = SQLM_OBS_PER_LANE;
 // loaded up front (the rest of a lane's observations stream in a loop): 3
 // would push the speculative landmark update to 130 VGPRs, 3 waves per SIMD
-constexpr int kObsPreload = 2;
+#ifndef SQLM_OBS_PRELOAD
+#define SQLM_OBS_PRELOAD 2
+#endif
+constexpr int kObsPreload = SQLM_OBS_PRELOAD;
 
 struct Bucket {
   int W;            // segment width
