@@ -816,7 +816,12 @@ typedef double d4v __attribute__((ext_vector_type(4)));
 // v_mfma_f64_16x16x4_f64 per 16x16 tile (no padding rows).
 // The raw P columns of the next batch are prefetched into registers while the
 // current batch runs on the matrix cores.
-constexpr int kTileWaves = 4, kTileThreads = 64 * kTileWaves;
+#ifndef SQLM_TILE_WAVES
+#define SQLM_TILE_WAVES 4
+#endif
+constexpr int kTileWaves = SQLM_TILE_WAVES, kTileThreads = 64 * kTileWaves;
+// waves per SIMD the tile kernel is compiled for (VGPR budget 512 / this)
+constexpr int kTileOcc = kTileWaves == 4 ? 3 : 4;
 
 // Phase cycle counters of the first kTileProfTiles tiles (diagnostic build
 // -DSQLM_TILE_PROF only; read with sqlm_debug_tile_profile).
@@ -885,8 +890,18 @@ __device__ __forceinline__ void tile_mfma(d4v *acc, const double (*Y)[NC], int t
   }
 }
 
+// tile_mfma for this wave's accumulator tiles (P = wave, a compile-time constant)
+template <int NT, int P = 0, int NC>
+__device__ __forceinline__ void tile_mfma_wave(int wave, d4v *acc, const double (*Y)[NC], int tmin, int tmax, int nks,
+                                               int r16, int k4) {
+  if constexpr (P + 1 < kTileWaves) {
+    if (wave != P) return tile_mfma_wave<NT, P + 1>(wave, acc, Y, tmin, tmax, nks, r16, k4);
+  }
+  tile_mfma<NT, P>(acc, Y, tmin, tmax, nks, r16, k4);
+}
+
 template <int NT, bool ST>
-__global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProblem d, double lambda) {
+__global__ __launch_bounds__(kTileThreads, ST ? 2 : kTileOcc) void k_rcs_tile(DevProblem d, double lambda) {
   // wave w owns the accumulator tiles q with q % kTileWaves == w; 3 waves per SIMD
   // for mono problems (167 VGPRs), 2 with the stereo row (spill-free)
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
@@ -1020,12 +1035,7 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : 3) void k_rcs_tile(DevProble
     TP(3);
     if (cmax > 0) {
       const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
-      switch (wave) {
-        case 0: tile_mfma<NT, 0>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
-        case 1: tile_mfma<NT, 1>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
-        case 2: tile_mfma<NT, 2>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
-        default: tile_mfma<NT, 3>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4); break;
-      }
+      tile_mfma_wave<NT>(wave, acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4);
       TP(4);
       if (gcol >= cmin && gcol < cmax) {
         double gs = 0.0;
