@@ -78,6 +78,7 @@ struct sqlm_ctx {
   int tile_max_cp = 0, tile_max_k = 0;
   // ---- device memory ----
   std::vector<DevBuf> bufs;
+  std::vector<DevBuf> pins;  // page-locked host staging of the large uploads (async DMA)
   double *h_scalars = nullptr;  // pinned
   // ---- comm ----
   Comm comm;
@@ -145,6 +146,47 @@ int upload(sqlm_ctx *c, int idx, const std::vector<T> &v, T **out) {
   return SQLM_OK;
 }
 
+// A page-locked host array from the context's arena (grown, never shrunk):
+// the large observation arrays are built in place and copied to the device
+// asynchronously while the host goes on with the setup.
+template <class T>
+struct PinVec {
+  T *p = nullptr;
+  size_t n = 0;
+  T &operator[](size_t i) const { return p[i]; }
+  T *data() const { return p; }
+  size_t size() const { return n; }
+  T *begin() const { return p; }
+  T *end() const { return p + n; }
+};
+
+template <class T>
+int pinned(sqlm_ctx *c, int idx, size_t n, PinVec<T> &out) {
+  if ((int)c->pins.size() <= idx) c->pins.resize(idx + 1);
+  DevBuf &b = c->pins[idx];
+  const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+  if (b.cap < bytes) {
+    if (b.p) (void)hipHostFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) return SQLM_ERR_OOM;
+    b.cap = bytes;
+  }
+  out.p = static_cast<T *>(b.p);
+  out.n = n;
+  return SQLM_OK;
+}
+
+template <class T>
+int upload(sqlm_ctx *c, int idx, const PinVec<T> &v, T **out) {
+  int s = ensure(c, idx, v.size(), out);
+  if (s) return s;
+  if (v.size()) HIP_OK(hipMemcpyAsync(*out, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  return SQLM_OK;
+}
+
+enum PinId { P_OBSLM, P_OBSCAM, P_OBSCAMH, P_OBSUV, P_OBSINFO, P_OBSDELTA, P_OBSUR, P_RQT, P_RX, P_RERR, P_RERR3, P_RLERR };
+
 enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
   B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS, B_CAMSLOT, B_CAMUV, B_SROWIDX,
@@ -186,39 +228,67 @@ inline int host_threads(int64_t work) {
   return (int)std::max<int64_t>(1, std::min<int64_t>({16, want, (int64_t)std::thread::hardware_concurrency()}));
 }
 
-void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const std::vector<int> &obs_camh,
+// v <- src[0 .. n) on host threads (the caller's arrays are copied in: ABI)
+template <class T>
+void par_assign(std::vector<T> &v, const T *src, size_t n) {
+  v.resize(n);  // same size as the last call: no fill
+  const int nth = host_threads((int64_t)n);
+  run_threads(nth, [&](int t) {
+    const size_t a = n * t / nth, b = n * (t + 1) / nth;
+    if (b > a) {
+      if (src) std::memcpy(v.data() + a, src + a, (b - a) * sizeof(T));
+      else std::memset(static_cast<void *>(v.data() + a), 0, (b - a) * sizeof(T));
+    }
+  });
+}
+
+void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *obs_camh,
                  const std::vector<int> &s_row, const std::vector<int> &s_col, int lm_cap, TilePlan &tp) {
   const int64_t nE = lm_begin[nL];
   tp.obs_local.assign(nE, -1);
   tp.urange.assign(nL, int2{-1, -1});
-  // pass 1 (sequential, greedy): tile boundaries — a tile closes before the
-  // landmark that would push its window past kTileMaxCams cameras or lm_cap
-  std::vector<int> tstart{0};
+  // pass 1 (greedy): tile boundaries -- a tile closes before the landmark that
+  // would push its window past kTileMaxCams cameras or lm_cap; the slots are
+  // cut into one chunk per host thread (a tile never crosses a chunk start)
+  std::vector<int> tstart;
   {
-    std::vector<int> stamp(nP, -1), lmst(nP, -1);
-    int t = 0, ncur = 0, cur_lm = 0;
-    for (int sl = 0; sl < nL; ++sl) {
-      int nnew = 0;
-      for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
-        const int h = obs_camh[o];
-        if (h < 0) continue;
-        if (lmst[h] == sl) { tp.dups = true; continue; }
-        lmst[h] = sl;
-        if (stamp[h] != t) ++nnew;
+    const int nth = host_threads(nE);
+    std::vector<std::vector<int>> cuts(nth);
+    std::vector<uint8_t> dup(nth, 0);
+    run_threads(nth, [&](int th) {
+      const int s0 = (int)((int64_t)nL * th / nth), s1 = (int)((int64_t)nL * (th + 1) / nth);
+      std::vector<int> stamp(nP, -1), lmst(nP, -1);
+      std::vector<int> &cv = cuts[th];
+      int t = 0, ncur = 0, cur_lm = 0;
+      for (int sl = s0; sl < s1; ++sl) {
+        int nnew = 0;
+        for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+          const int h = obs_camh[o];
+          if (h < 0) continue;
+          if (lmst[h] == sl) { dup[th] = 1; continue; }
+          lmst[h] = sl;
+          if (stamp[h] != t) ++nnew;
+        }
+        if (cur_lm == 0 || ncur + nnew > kTileMaxCams || cur_lm >= lm_cap) {
+          cv.push_back(sl);
+          ++t;
+          ncur = 0;
+          cur_lm = 0;
+        }
+        for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+          const int h = obs_camh[o];
+          if (h >= 0 && stamp[h] != t) { stamp[h] = t; ++ncur; }
+        }
+        ++cur_lm;
       }
-      if (cur_lm > 0 && (ncur + nnew > kTileMaxCams || cur_lm >= lm_cap)) {
-        tstart.push_back(sl);
-        ++t;
-        ncur = 0;
-        cur_lm = 0;
-      }
-      for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
-        const int h = obs_camh[o];
-        if (h >= 0 && stamp[h] != t) { stamp[h] = t; ++ncur; }
-      }
-      ++cur_lm;
+    });
+    for (int th = 0; th < nth; ++th) {
+      tstart.insert(tstart.end(), cuts[th].begin(), cuts[th].end());
+      if (dup[th]) tp.dups = true;
     }
-    if (cur_lm > 0) tstart.push_back(nL);
+    if (tstart.empty() || tstart[0] != 0) tstart.insert(tstart.begin(), 0);
+    if (nL > 0) tstart.push_back(nL);
+    else tstart.assign(1, 0);
   }
   const int nt = (int)tstart.size() - 1;
   // pass 2 (tiles on host threads): window cameras, local camera of every
@@ -430,13 +500,27 @@ int prepare(sqlm_ctx *c, int level) {
   };
   std::vector<uint8_t> pose_act(c->n_pose, 0), pt_act(c->n_pt, 0);
   std::vector<int> kcount(c->n_pt, 0);
+  std::vector<int> span_lo(c->n_pt, std::numeric_limits<int>::max()), span_hi(c->n_pt, -1);
   int64_t n_ae = 0;
-  for (int64_t e = 0; e < c->n_obs; ++e) {
-    if (c->obs_level[e] != level) continue;
-    pose_act[c->obs_pose[e]] = 1;
-    pt_act[c->obs_pt[e]] = 1;
-    kcount[c->obs_pt[e]]++;
-    ++n_ae;
+  {  // active set, track lengths and camera spans in one pass on host threads (relaxed atomics)
+    const int nth = host_threads(c->n_obs);
+    std::vector<int64_t> cnt(nth, 0);
+    run_threads(nth, [&](int t) {
+      const int64_t e0 = c->n_obs * t / nth, e1 = c->n_obs * (t + 1) / nth;
+      int64_t n = 0;
+      for (int64_t e = e0; e < e1; ++e) {
+        if (c->obs_level[e] != level) continue;
+        const int l = c->obs_pt[e], pp = c->obs_pose[e];
+        __atomic_store_n(&pose_act[pp], (uint8_t)1, __ATOMIC_RELAXED);
+        __atomic_store_n(&pt_act[l], (uint8_t)1, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&kcount[l], 1, __ATOMIC_RELAXED);
+        __atomic_fetch_min(&span_lo[l], pp, __ATOMIC_RELAXED);
+        __atomic_fetch_max(&span_hi[l], pp, __ATOMIC_RELAXED);
+        ++n;
+      }
+      cnt[t] = n;
+    });
+    for (int64_t v : cnt) n_ae += v;
   }
   std::vector<int64_t> lid_act;
   const bool sharded = c->comm.enabled();
@@ -459,13 +543,7 @@ int prepare(sqlm_ctx *c, int level) {
   // landmark slots: bucket by segment width; inside a bucket by camera span
   // (first, last observing pose, then id), so a batch of consecutive slots in
   // the RCS tiles shares nearly one span (dense MFMA panels)
-  std::vector<int> pts, span_lo(c->n_pt, std::numeric_limits<int>::max()), span_hi(c->n_pt, -1);
-  for (int64_t e = 0; e < c->n_obs; ++e) {
-    if (c->obs_level[e] != level) continue;
-    const int l = c->obs_pt[e], pp = c->obs_pose[e];
-    span_lo[l] = std::min(span_lo[l], pp);
-    span_hi[l] = std::max(span_hi[l], pp);
-  }
+  std::vector<int> pts;
   // (segment width, first pose) buckets by a counting sort, then last pose
   // inside a bucket; ties keep id order (the order a stable sort would give)
   {
@@ -480,10 +558,24 @@ int prepare(sqlm_ctx *c, int level) {
     std::vector<int> f(bcnt.begin(), bcnt.end() - 1);
     for (int l = 0; l < c->n_pt; ++l)
       if (key[l] >= 0) pts[f[key[l]]++] = l;
-    for (int64_t b = 0; b < nb; ++b)
-      if (bcnt[b + 1] - bcnt[b] > 1)
-        std::stable_sort(pts.begin() + bcnt[b], pts.begin() + bcnt[b + 1],
-                         [&](int a, int bb) { return span_hi[a] < span_hi[bb]; });
+    // buckets hold a few dozen points: a stable insertion sort, buckets on host threads
+    const int nth = host_threads(c->n_pt * 8);
+    run_threads(nth, [&](int t) {
+      for (int64_t b = nb * t / nth; b < nb * (t + 1) / nth; ++b) {
+        int *v = pts.data() + bcnt[b];
+        const int m = bcnt[b + 1] - bcnt[b];
+        if (m > 64) {
+          std::stable_sort(v, v + m, [&](int a, int bb) { return span_hi[a] < span_hi[bb]; });
+          continue;
+        }
+        for (int i = 1; i < m; ++i) {
+          const int x = v[i], key = span_hi[x];
+          int j = i - 1;
+          while (j >= 0 && span_hi[v[j]] > key) { v[j + 1] = v[j]; --j; }
+          v[j + 1] = x;
+        }
+      }
+    });
   }
   const int nL = (int)pts.size();
   phase("active+sort");
@@ -511,8 +603,16 @@ int prepare(sqlm_ctx *c, int level) {
   const int64_t nE = lm_begin[nL];
   if (nE > (int64_t)std::numeric_limits<int>::max()) return SQLM_ERR_UNSUPPORTED;
   c->dev_edge.assign(nE, 0);
-  std::vector<int> obs_lm(nE), obs_cam(nE), obs_camh(nE);
-  std::vector<double> obs_uv(2 * nE), obs_info(nE), obs_delta(nE), obs_ur(c->has_stereo ? nE : 0);
+  PinVec<int> obs_lm, obs_cam, obs_camh;
+  PinVec<double> obs_uv, obs_info, obs_delta, obs_ur;
+  {
+    int e = 0;
+    if ((e = pinned(c, P_OBSLM, nE, obs_lm)) || (e = pinned(c, P_OBSCAM, nE, obs_cam)) ||
+        (e = pinned(c, P_OBSCAMH, nE, obs_camh)) || (e = pinned(c, P_OBSUV, 2 * nE, obs_uv)) ||
+        (e = pinned(c, P_OBSINFO, nE, obs_info)) || (e = pinned(c, P_OBSDELTA, nE, obs_delta)) ||
+        (e = pinned(c, P_OBSUR, c->has_stereo ? nE : 0, obs_ur)))
+      return e;
+  }
   // Stable scatter of the observations into slot order on a few host threads:
   // chunk t of the edge range counts its edges per slot, the per-(chunk, slot)
   // bases follow by a prefix over chunks (edge-id order inside a landmark is
@@ -577,7 +677,20 @@ int prepare(sqlm_ctx *c, int level) {
         if (obs_camh[o] >= 0) cam_obs[fill[obs_camh[o]]++] = (int)o;
     });
   }
+  {  // the observation arrays go to the device now, overlapped with the rest of the setup
+    int e = 0;
+    if ((e = upload(c, B_OBSLM, obs_lm, &d.obs_lm)) || (e = upload(c, B_OBSCAM, obs_cam, &d.obs_cam)) ||
+        (e = upload(c, B_OBSCAMH, obs_camh, &d.obs_camh)) || (e = upload(c, B_OBSUV, obs_uv, &d.obs_uv)) ||
+        (e = upload(c, B_OBSINFO, obs_info, &d.obs_info)) || (e = upload(c, B_OBSDELTA, obs_delta, &d.obs_delta)))
+      return e;
+    if (c->has_stereo && (e = upload(c, B_OBSUR, obs_ur, &d.obs_ur))) return e;
+    (void)hipStreamQuery(c->stream);  // submit now: the runtime would otherwise batch them until the next sync
+  }
   phase("obs+camcsr");
+  if (ptime && std::getenv("SQLM_PREP_SYNC")) {  // diagnostic: the early uploads alone
+    (void)hipStreamSynchronize(c->stream);
+    phase("obs upload");
+  }
   // pose id window of every per-landmark block tile (k_landmark_update)
   std::vector<int2> upd_rng;
   for (Bucket &b : c->buckets) {
@@ -672,7 +785,7 @@ int prepare(sqlm_ctx *c, int level) {
   // otherwise run ~40 long tiles on 256 CUs)
   const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
   phase("S pattern");
-  build_tiles(nP, nL, lm_begin, obs_camh, s_row, s_col, lm_cap, tp);
+  build_tiles(nP, nL, lm_begin, obs_camh.data(), s_row, s_col, lm_cap, tp);
   phase("tiles");
   if (ptime) {  // plan shape: tile count, longest reduction lists, solver layout
     int rmax = 0, gmax = 0;
@@ -783,12 +896,7 @@ int prepare(sqlm_ctx *c, int level) {
     d.n_long_g = (int)tp.long_g.size();
   }
   UP(B_UPDRNG, upd_rng, d.upd_rng);
-  UP(B_OBSLM, obs_lm, d.obs_lm);
-  UP(B_OBSCAM, obs_cam, d.obs_cam);
-  UP(B_OBSCAMH, obs_camh, d.obs_camh);
-  UP(B_OBSUV, obs_uv, d.obs_uv);
-  UP(B_OBSINFO, obs_info, d.obs_info);
-  UP(B_OBSDELTA, obs_delta, d.obs_delta);
+
   AL(B_OBSS, (size_t)nE, d.obs_s);
   if (c->use_tiles) {
     d.obs_P = nullptr;  // consumers recompute the H_lp blocks from obs_s
@@ -800,7 +908,6 @@ int prepare(sqlm_ctx *c, int level) {
   UP(B_CAMOBS, cam_obs, d.cam_obs);
   d.has_stereo = c->has_stereo ? 1 : 0;
   if (c->has_stereo) {
-    UP(B_OBSUR, obs_ur, d.obs_ur);
     UP(B_POSEBF, c->pose_bf, d.pose_bf);
     AL(B_OBSERR3, (size_t)nE, d.obs_err3);
     AL(B_CAMUR, cam_obs.size(), d.cam_ur);
@@ -811,6 +918,15 @@ int prepare(sqlm_ctx *c, int level) {
   // the X gather), gathered on the device from the slot-ordered arrays
   AL(B_CAMSLOT, cam_obs.size(), d.cam_slot);
   AL(B_CAMUV, 4 * cam_obs.size(), d.cam_uv);
+  launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
+    (void)hipEventRecord(e1, c->stream);
+    launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
+    (void)hipEventRecord(e2, c->stream);
+    (void)hipEventSynchronize(e2);
+    float a = 0, b = 0;
+    (void)hipEventElapsedTime(&a, e0, e1); (void)hipEventElapsedTime(&b, e1, e2);
+    std::fprintf(stderr, "diag cam_gather %.3f ms then %.3f ms (n %zu)\n", a, b, cam_obs.size());
+  }
   launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
@@ -935,14 +1051,23 @@ int prepare(sqlm_ctx *c, int level) {
   if (d.obs_err3) HIP_OK(hipMemsetAsync(d.obs_err3, 0, sizeof(double) * std::max<int64_t>(nE, 1), c->stream));
   launch_pose_prep(d, 0, c->stream);
   phase("upload");
+  if (ptime) {  // how long the queued copies and setup kernels still run after the host is done
+    (void)hipStreamSynchronize(c->stream);
+    phase("gpu drain");
+  }
   return SQLM_OK;
 }
 
 void finish(sqlm_ctx *c) {
   DevProblem &d = c->d;
-  std::vector<double> qt(8 * (size_t)c->n_pose), X(4 * (size_t)d.nL), err(2 * (size_t)d.nE), lerr(d.nLid);
-  std::vector<double> err3(d.obs_err3 ? d.nE : 0);
-  if (!err3.empty())
+  // device -> page-locked staging (one DMA each), then the scatter back to
+  // caller order on host threads
+  PinVec<double> qt, X, err, err3, lerr;
+  if (pinned(c, P_RQT, 8 * (size_t)c->n_pose, qt) || pinned(c, P_RX, 4 * (size_t)d.nL, X) ||
+      pinned(c, P_RERR, 2 * (size_t)d.nE, err) || pinned(c, P_RERR3, d.obs_err3 ? (size_t)d.nE : 0, err3) ||
+      pinned(c, P_RLERR, (size_t)d.nLid, lerr))
+    return;
+  if (err3.size())
     (void)hipMemcpyAsync(err3.data(), d.obs_err3, err3.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
   (void)hipMemcpyAsync(qt.data(), d.pose_qt[0], qt.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
   if (d.nL) (void)hipMemcpyAsync(X.data(), d.X[0], X.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
@@ -953,13 +1078,16 @@ void finish(sqlm_ctx *c) {
     for (int k = 0; k < 4; ++k) c->pose_q[4 * p + k] = qt[8 * p + k];
     for (int k = 0; k < 3; ++k) c->pose_t[3 * p + k] = qt[8 * p + 4 + k];
   }
-  for (int s = 0; s < d.nL; ++s)
-    for (int k = 0; k < 3; ++k) c->pt[3 * c->slot_pt[s] + k] = X[4 * s + k];
-  for (int64_t o = 0; o < d.nE; ++o) {
-    c->obs_err[2 * c->dev_edge[o]] = err[2 * o];
-    c->obs_err[2 * c->dev_edge[o] + 1] = err[2 * o + 1];
-    if (!err3.empty()) c->obs_err3[c->dev_edge[o]] = err3[o];
-  }
+  const int nth = host_threads(d.nE);
+  run_threads(nth, [&](int t) {
+    for (int s = (int)((int64_t)d.nL * t / nth); s < (int)((int64_t)d.nL * (t + 1) / nth); ++s)
+      for (int k = 0; k < 3; ++k) c->pt[3 * c->slot_pt[s] + k] = X[4 * s + k];
+    for (int64_t o = d.nE * t / nth; o < d.nE * (t + 1) / nth; ++o) {
+      c->obs_err[2 * c->dev_edge[o]] = err[2 * o];
+      c->obs_err[2 * c->dev_edge[o] + 1] = err[2 * o + 1];
+      if (err3.size()) c->obs_err3[c->dev_edge[o]] = err3[o];
+    }
+  });
   for (int64_t t = 0; t < d.nLid; ++t) c->lid_err[c->dev_lid_edge[t]] = lerr[t];
 }
 
@@ -1350,6 +1478,8 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   if (c->orb) orb_destroy(c->orb);
   for (auto &b : c->bufs)
     if (b.p) (void)hipFree(b.p);
+  for (auto &b : c->pins)
+    if (b.p) (void)hipHostFree(b.p);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
@@ -1374,8 +1504,16 @@ int sqlm_set_problem(sqlm_ctx *c, int n_pose, const double *pose_q, const double
   if ((n_pose && (!pose_q || !pose_t || !pose_fixed || !intr)) || (n_pt && !pt) ||
       (n_obs && (!obs_pose || !obs_pt || !obs_uv || !obs_info)))
     return SQLM_ERR_INVALID_ARG;
-  for (int64_t e = 0; e < n_obs; ++e)
-    if (obs_pose[e] < 0 || obs_pose[e] >= n_pose || obs_pt[e] < 0 || obs_pt[e] >= n_pt) return SQLM_ERR_INVALID_ARG;
+  {
+    const int nth = host_threads(n_obs);
+    std::vector<uint8_t> bad(nth, 0);
+    run_threads(nth, [&](int t) {
+      for (int64_t e = n_obs * t / nth; e < n_obs * (t + 1) / nth; ++e)
+        if (obs_pose[e] < 0 || obs_pose[e] >= n_pose || obs_pt[e] < 0 || obs_pt[e] >= n_pt) { bad[t] = 1; break; }
+    });
+    for (uint8_t b : bad)
+      if (b) return SQLM_ERR_INVALID_ARG;
+  }
   c->n_pose = n_pose;
   c->n_pt = n_pt;
   c->n_obs = n_obs;
@@ -1383,16 +1521,14 @@ int sqlm_set_problem(sqlm_ctx *c, int n_pose, const double *pose_q, const double
   c->pose_t.assign(pose_t, pose_t + 3 * (size_t)n_pose);
   c->pose_fixed.assign(pose_fixed, pose_fixed + n_pose);
   c->intr.assign(intr, intr + 4 * (size_t)n_pose);
-  c->pt.assign(pt, pt + 3 * (size_t)n_pt);
-  c->obs_pose.assign(obs_pose, obs_pose + n_obs);
-  c->obs_pt.assign(obs_pt, obs_pt + n_obs);
-  c->obs_uv.assign(obs_uv, obs_uv + 2 * n_obs);
-  c->obs_info.assign(obs_info, obs_info + n_obs);
-  if (obs_delta) c->obs_delta.assign(obs_delta, obs_delta + n_obs);
-  else c->obs_delta.assign(n_obs, 0.0);
-  if (obs_level) c->obs_level.assign(obs_level, obs_level + n_obs);
-  else c->obs_level.assign(n_obs, 0);
-  c->obs_err.assign(2 * n_obs, 0.0);
+  par_assign(c->pt, pt, 3 * (size_t)n_pt);
+  par_assign(c->obs_pose, obs_pose, (size_t)n_obs);
+  par_assign(c->obs_pt, obs_pt, (size_t)n_obs);
+  par_assign(c->obs_uv, obs_uv, 2 * (size_t)n_obs);
+  par_assign(c->obs_info, obs_info, (size_t)n_obs);
+  par_assign(c->obs_delta, obs_delta, (size_t)n_obs);  // null: no robust kernel (zeros)
+  par_assign(c->obs_level, obs_level, (size_t)n_obs);  // null: level 0
+  par_assign(c->obs_err, (const double *)nullptr, 2 * (size_t)n_obs);
   c->has_stereo = false;
   c->obs_ur.clear(); c->pose_bf.clear(); c->obs_err3.clear();
   c->n_lid = 0;
