@@ -919,15 +919,6 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_CAMSLOT, cam_obs.size(), d.cam_slot);
   AL(B_CAMUV, 4 * cam_obs.size(), d.cam_uv);
   launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
-    (void)hipEventRecord(e1, c->stream);
-    launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
-    (void)hipEventRecord(e2, c->stream);
-    (void)hipEventSynchronize(e2);
-    float a = 0, b = 0;
-    (void)hipEventElapsedTime(&a, e0, e1); (void)hipEventElapsedTime(&b, e1, e2);
-    std::fprintf(stderr, "diag cam_gather %.3f ms then %.3f ms (n %zu)\n", a, b, cam_obs.size());
-  }
-  launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
   {
