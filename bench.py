@@ -36,7 +36,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # 2048 FLOP per 64-cycle issue, the SQ_VALU_MFMA_BUSY_CYCLES we measure per MFMA)
 # = 78.6 TFLOP/s, AMD's MI355X FP64-matrix figure. The guide has no f64 row.
 MFMA_F64_PEAK_TFLOPS = 78.6
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r01")
+# committed PMC summaries, newest round first (pmc_traffic takes the first on the same workload)
+PROFILE_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r02", "r01")]
 
 
 def make_workload(name: str, scale: float):
@@ -100,11 +101,13 @@ def pmc_traffic(kernel_prefix: str, workload: str, n_obs: int):
     summary (scripts/gpu_pmc.sh + scripts/pmc_summary.py: separate FETCH_SIZE
     and WRITE_SIZE passes, FETCH_SIZE doubled for gfx950). None if the summary
     was not taken on this exact workload."""
-    path = os.path.join(PROFILE_DIR, f"pmc_{workload}.json")
-    if not os.path.exists(path):
-        return None, None
-    summ = json.load(open(path))
-    if int(summ.get("meta", {}).get("n_obs", -1)) != n_obs:
+    for pdir in PROFILE_DIRS:
+        path = os.path.join(pdir, f"pmc_{workload}.json")
+        if os.path.exists(path):
+            summ = json.load(open(path))
+            if int(summ.get("meta", {}).get("n_obs", -1)) == n_obs:
+                break
+    else:
         return None, None
     hits = [e["traffic_bytes"] for k, e in summ["kernels"].items()
             if k.startswith(kernel_prefix) and "traffic_bytes" in e]  # all template instances (buckets)
