@@ -96,6 +96,23 @@ typedef struct sqlm_replay_out {
 int sqlm_capture_replay(sqlm_ctx *ctx, const sqlm_capture *cap, const volatile uint8_t *stop,
                         sqlm_replay_out *out);
 
+/* System::SaveTrajectoryKITTI (src/System.cc:503-560): one line per tracked
+ * frame, the 3x4 [Rwc | twc] of its camera-to-world pose, "%.9f" fixed, space
+ * separated, in the origin keyframe's frame. Frame f's pose is Tcr[f] (its
+ * pose relative to its reference keyframe, Tracking::mlRelativeFramePoses)
+ * times the reference keyframe's pose; a bad reference keyframe is replaced by
+ * its parent, accumulating Tcp (KeyFrame::mTcp), as the reference does. All
+ * products in float (cv::Mat CV_32F); Two = the origin keyframe's pose
+ * inverse as KeyFrame::SetPose forms it ([R^T | -R^T t]).
+ *   Tcr     [n_frames][16] row-major 4x4   frame_ref [n_frames] keyframe index
+ *   Tcw     [n_kf][16] keyframe poses      Tcp [n_kf][16], parent [n_kf] (-1 none)
+ *   bad     [n_kf] (may be NULL)           origin_kf: index of the first keyframe (lowest mnId)
+ * Returns SQLM_ERR_INVALID_ARG for bad arguments or an unwritable path, or a
+ * bad keyframe without a good ancestor. */
+int sqlm_save_trajectory_kitti(const char *path, int n_frames, const float *Tcr, const int32_t *frame_ref, int n_kf,
+                               const float *Tcw, const float *Tcp, const int32_t *parent, const uint8_t *bad,
+                               int origin_kf);
+
 #ifdef __cplusplus
 }
 #endif

@@ -345,3 +345,71 @@ int sqlm_capture_replay(sqlm_ctx *ctx, const sqlm_capture *c, const volatile uin
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- KITTI trajectory
+
+namespace {
+// c = a b for row-major 4x4 float matrices, k summed in order in float
+void mul4(const float *a, const float *b, float *c) {
+  float t[16];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j) {
+      float s = 0.f;
+      for (int k = 0; k < 4; ++k) s += a[4 * i + k] * b[4 * k + j];
+      t[4 * i + j] = s;
+    }
+  std::memcpy(c, t, sizeof(t));
+}
+}  // namespace
+
+int sqlm_save_trajectory_kitti(const char *path, int n_frames, const float *Tcr, const int32_t *frame_ref, int n_kf,
+                               const float *Tcw, const float *Tcp, const int32_t *parent, const uint8_t *bad,
+                               int origin_kf) {
+  if (!path || n_frames < 0 || n_kf <= 0 || origin_kf < 0 || origin_kf >= n_kf || !Tcw || !parent ||
+      (n_frames && (!Tcr || !frame_ref)) || (bad && !Tcp))
+    return SQLM_ERR_INVALID_ARG;
+  for (int f = 0; f < n_frames; ++f)
+    if (frame_ref[f] < 0 || frame_ref[f] >= n_kf) return SQLM_ERR_INVALID_ARG;
+  // Two = origin keyframe's Twc (KeyFrame::SetPose: Rwc = Rcw^T, Ow = -Rwc tcw)
+  const float *T0 = Tcw + 16 * (size_t)origin_kf;
+  float Two[16] = {0};
+  for (int i = 0; i < 3; ++i) {
+    float o = 0.f;
+    for (int k = 0; k < 3; ++k) {
+      Two[4 * i + k] = T0[4 * k + i];
+      o += -T0[4 * k + i] * T0[4 * k + 3];
+    }
+    Two[4 * i + 3] = o;
+  }
+  Two[15] = 1.f;
+  FILE *fp = std::fopen(path, "w");
+  if (!fp) return SQLM_ERR_INVALID_ARG;
+  int st = SQLM_OK;
+  for (int f = 0; f < n_frames && st == SQLM_OK; ++f) {
+    float Trw[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    int k = frame_ref[f], hops = 0;
+    while (bad && bad[k]) {  // Trw = Trw * pKF->mTcp; pKF = pKF->GetParent()
+      mul4(Trw, Tcp + 16 * (size_t)k, Trw);
+      k = parent[k];
+      if (k < 0 || k >= n_kf || ++hops > n_kf) { st = SQLM_ERR_INVALID_ARG; break; }
+    }
+    if (st) break;
+    mul4(Trw, Tcw + 16 * (size_t)k, Trw);
+    mul4(Trw, Two, Trw);
+    float T[16];
+    mul4(Tcr + 16 * (size_t)f, Trw, T);
+    // Rwc = R^T, twc = -Rwc t (cv::Mat float products)
+    float Rwc[9], twc[3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Rwc[3 * i + j] = T[4 * j + i];
+    for (int i = 0; i < 3; ++i) {
+      float s = 0.f;
+      for (int j = 0; j < 3; ++j) s += -Rwc[3 * i + j] * T[4 * j + 3];
+      twc[i] = s;
+    }
+    std::fprintf(fp, "%.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f %.9f\n", Rwc[0], Rwc[1], Rwc[2], twc[0],
+                 Rwc[3], Rwc[4], Rwc[5], twc[1], Rwc[6], Rwc[7], Rwc[8], twc[2]);
+  }
+  if (std::fclose(fp) != 0 && st == SQLM_OK) st = SQLM_ERR_INVALID_ARG;
+  return st;
+}

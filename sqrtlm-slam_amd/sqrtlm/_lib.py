@@ -35,7 +35,8 @@ EXPORTS = [
     "sqlm_get_rcs_layout",
 ]
 # every symbol include/sqrtlm_capture.h declares
-CAPTURE_EXPORTS = ["sqlm_capture_write", "sqlm_capture_read", "sqlm_capture_free", "sqlm_capture_replay"]
+CAPTURE_EXPORTS = ["sqlm_capture_write", "sqlm_capture_read", "sqlm_capture_free", "sqlm_capture_replay",
+                   "sqlm_save_trajectory_kitti"]
 # every symbol include/sqrtlm_orb.h declares
 ORB_EXPORTS = ["sqlm_orb_extract", "sqlm_orb_get_level", "sqlm_orb_match_bf", "sqlm_orb_search_for_init",
                "sqlm_orb_bench_extract"]

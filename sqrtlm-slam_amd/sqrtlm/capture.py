@@ -160,3 +160,18 @@ def replay(ctx: Context, cap: Capture, stop=None) -> dict:
     o.Tcw, o.pt, o.outlier, o.chi2 = ptr(Tcw), ptr(pt), ptr(outl), ptr(chi)
     check(lib().sqlm_capture_replay(ctx._h, C.byref(st), ptr(stop), C.byref(o)), "sqlm_capture_replay")
     return dict(Tcw=Tcw, pt=pt, outlier=outl, chi2=chi, ran=o.ran, stats=[s.as_dict() for s in o.stats])
+
+
+def save_trajectory_kitti(path: str, Tcr, frame_ref, Tcw, Tcp, parent, bad=None, origin_kf: int = 0) -> None:
+    """System::SaveTrajectoryKITTI (src/System.cc:503-560) through
+    sqlm_save_trajectory_kitti: Tcr (F,4,4) frame poses relative to their
+    reference keyframe frame_ref (F,), keyframe poses Tcw (K,4,4), Tcp (K,4,4)
+    relative to the parent keyframe parent (K,), bad (K,) flags; float32."""
+    f32 = lambda a: np.ascontiguousarray(a, np.float32).reshape(-1)  # noqa: E731
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)  # noqa: E731
+    Tcr, Tcw, Tcp = f32(Tcr), f32(Tcw), f32(Tcp)
+    fr, par = i32(frame_ref), i32(parent)
+    b = None if bad is None else np.ascontiguousarray(bad, np.uint8)
+    check(lib().sqlm_save_trajectory_kitti(str(path).encode(), int(fr.size), ptr(Tcr), ptr(fr), int(par.size),
+                                           ptr(Tcw), ptr(Tcp), ptr(par), ptr(b) if b is not None else None,
+                                           int(origin_kf)), "sqlm_save_trajectory_kitti")
