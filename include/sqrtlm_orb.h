@@ -76,6 +76,63 @@ int sqlm_orb_search_for_init(sqlm_ctx *ctx, const sqlm_keypoint *k1, const uint8
                              const sqlm_keypoint *k2, const uint8_t *d2, int n2, const sqlm_frame_bounds *f2,
                              float *prev, int32_t *m12, int window, float nnratio, int check_ori, int *n_matches);
 
+/* The Frame fields the projection searches read and write
+ * (include/data_structure/Frame.h): kps = mvKeysUn, desc = mDescriptors
+ * [n][32], uright = mvuRight (NULL: monocular), bounds = mnMinX..mnMaxY,
+ * scale_factors = mvScaleFactors [n_levels], fx fy cx cy, bf = mbf, mb, and
+ * the keypoint slots mvpMapPoints as map-point ids (slot_mp, -1 = NULL) with
+ * slot_obs = that point's Observations() > 0 — both updated by the call. */
+typedef struct sqlm_orb_frame {
+  const sqlm_keypoint *kps;
+  const uint8_t *desc;
+  const float *uright;
+  int32_t n;
+  sqlm_frame_bounds bounds;
+  const float *scale_factors;
+  int32_t n_levels;
+  float fx, fy, cx, cy, bf, mb;
+  int32_t *slot_mp;
+  uint8_t *slot_obs;
+} sqlm_orb_frame;
+
+/* A local map point as Tracking::SearchLocalPoints leaves it (MapPoint.h:
+ * mnId, mTrackProjX/Y/XR, mTrackViewCos, mnTrackScaleLevel, mbTrackInView,
+ * isBad(), Observations() > 0). */
+typedef struct sqlm_track_point {
+  int32_t id;
+  float proj_x, proj_y, proj_xr, view_cos;
+  int32_t level;
+  uint8_t in_view, bad, has_obs, pad;
+} sqlm_track_point;
+
+/* One LastFrame keypoint slot: mvpMapPoints[i] (id, -1 = NULL), the point's
+ * GetWorldPos(), mvKeys[i].octave, mvKeysUn[i].angle, mvbOutlier[i] and the
+ * point's Observations() > 0. */
+typedef struct sqlm_last_point {
+  int32_t id;
+  float x, y, z;
+  int32_t octave;
+  float angle;
+  uint8_t outlier, has_obs, pad[2];
+} sqlm_last_point;
+
+/* ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th)
+ * (ORBmatcher.cc:67-181): mps [n_mp] with their descriptors mp_desc [n_mp][32]
+ * (GetDescriptor()). Candidate windows (GetFeaturesInArea, Frame.cc:1463) and
+ * their Hamming distances on the GPU; the order-dependent acceptance (a slot
+ * taken by an earlier point is skipped) on the host over those lists.
+ * *n_matches = the return value. */
+int sqlm_orb_search_by_projection_local(sqlm_ctx *ctx, sqlm_orb_frame *F, const sqlm_track_point *mps,
+                                        const uint8_t *mp_desc, int n_mp, float th, float nnratio, int *n_matches);
+
+/* ORBmatcher(., check_ori).SearchByProjection(CurrentFrame, LastFrame, th,
+ * bMono) (ORBmatcher.cc:1717-1883): F = CurrentFrame, Tcw / Tlw = the 3x4
+ * rows of CurrentFrame.mTcw / LastFrame.mTcw (float, row-major), lp / ldesc =
+ * LastFrame's n_last slots and their points' descriptors. */
+int sqlm_orb_search_by_projection_last(sqlm_ctx *ctx, sqlm_orb_frame *F, const float *Tcw, const float *Tlw,
+                                       const sqlm_last_point *lp, const uint8_t *ldesc, int n_last, float th,
+                                       int mono, int check_ori, int *n_matches);
+
 /* Bench helper: time `reps` extractions of one image (input uploaded once;
  * timed region = the whole device pipeline incl. the host quadtree step).
  * ms_per_frame, and per-stage device milliseconds [6]: pyramid, fast,

@@ -143,3 +143,72 @@ def search_for_init(k1, d1, k2, d2, grid, prev, window=100, nnratio=0.9, check_o
     n = lib().orc_search_for_init(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2), C.byref(g), _p(prev), _p(m12),
                                   int(window), C.c_float(nnratio), int(bool(check_ori)))
     return n, m12, prev
+
+
+# Projection searches (orb_ref.h orc_frame / orc_track_point / orc_last_point)
+TRACK_POINT_DTYPE = np.dtype([("id", "<i4"), ("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"),
+                              ("view_cos", "<f4"), ("level", "<i4"), ("in_view", "u1"), ("bad", "u1"),
+                              ("has_obs", "u1"), ("pad", "u1")])
+LAST_POINT_DTYPE = np.dtype([("id", "<i4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("octave", "<i4"),
+                             ("angle", "<f4"), ("outlier", "u1"), ("has_obs", "u1"), ("pad", "u1", (2,))])
+
+
+class _Frame(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p), ("n", C.c_int),
+                ("bounds", FrameGrid), ("scale_factors", C.c_void_p), ("n_levels", C.c_int),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("mb", C.c_float), ("slot_mp", C.c_void_p), ("slot_obs", C.c_void_p)]
+
+
+def _frame(kps, desc, bounds, scale, cam, uright, slot_mp, slot_obs):
+    """(struct, arrays kept alive, slot_mp copy, slot_obs copy)."""
+    kps = np.ascontiguousarray(kps, KP_DTYPE)
+    desc = np.ascontiguousarray(desc, np.uint8)
+    scale = np.ascontiguousarray(scale, np.float32)
+    uright = None if uright is None else np.ascontiguousarray(uright, np.float32)
+    slot_mp = np.array(slot_mp, np.int32)
+    slot_obs = np.array(slot_obs, np.uint8)
+    f = _Frame()
+    f.kps, f.desc, f.n = kps.ctypes.data, desc.ctypes.data, len(kps)
+    f.uright = None if uright is None else uright.ctypes.data
+    f.bounds = FrameGrid(*[float(v) for v in bounds])
+    f.scale_factors, f.n_levels = scale.ctypes.data, len(scale)
+    f.fx, f.fy, f.cx, f.cy, f.bf, f.mb = (float(v) for v in cam)
+    f.slot_mp, f.slot_obs = slot_mp.ctypes.data, slot_obs.ctypes.data
+    return f, (kps, desc, scale, uright), slot_mp, slot_obs
+
+
+def features_in_area(kps, bounds, x, y, r, min_level=-1, max_level=-1):
+    """Frame::GetFeaturesInArea (Frame.cc:1463-1552) -> keypoint indices."""
+    n = len(kps)
+    f, keep, _, _ = _frame(kps, np.zeros((n, 32), np.uint8), bounds, [1.0], (0,) * 6, None,
+                           np.full(n, -1), np.zeros(n))
+    out = np.zeros(max(n, 1), np.int32)
+    m = lib().orc_features_in_area(C.byref(f), C.c_float(x), C.c_float(y), C.c_float(r), int(min_level),
+                                   int(max_level), _p(out))
+    return out[:m]
+
+
+def search_by_projection_local(kps, desc, bounds, scale, uright, slot_mp, slot_obs, mps, mp_desc, th=1.0,
+                               nnratio=0.6):
+    """ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th) -> (n, slot_mp, slot_obs)."""
+    f, keep, sm, so = _frame(kps, desc, bounds, scale, (0,) * 6, uright, slot_mp, slot_obs)
+    mps = np.ascontiguousarray(mps, TRACK_POINT_DTYPE)
+    mp_desc = np.ascontiguousarray(mp_desc, np.uint8)
+    n = lib().orc_search_by_projection_local(C.byref(f), _p(mps), _p(mp_desc), len(mps), C.c_float(th),
+                                             C.c_float(nnratio))
+    return n, sm, so
+
+
+def search_by_projection_last(kps, desc, bounds, scale, cam, uright, slot_mp, slot_obs, Tcw, Tlw, lp, ldesc, th,
+                              mono, check_ori=True):
+    """ORBmatcher(., check_ori).SearchByProjection(CurrentFrame, LastFrame, th, bMono)
+    -> (n, slot_mp, slot_obs). cam = (fx, fy, cx, cy, mbf, mb)."""
+    f, keep, sm, so = _frame(kps, desc, bounds, scale, cam, uright, slot_mp, slot_obs)
+    Tcw = np.ascontiguousarray(np.asarray(Tcw, np.float32)[:3, :4])
+    Tlw = np.ascontiguousarray(np.asarray(Tlw, np.float32)[:3, :4])
+    lp = np.ascontiguousarray(lp, LAST_POINT_DTYPE)
+    ldesc = np.ascontiguousarray(ldesc, np.uint8)
+    n = lib().orc_search_by_projection_last(C.byref(f), _p(Tcw), _p(Tlw), _p(lp), _p(ldesc), len(lp),
+                                            C.c_float(th), int(bool(mono)), int(bool(check_ori)))
+    return n, sm, so

@@ -875,3 +875,261 @@ int orc_search_for_init(const orc_kp *k1, const uint8_t *d1, int n1, const orc_k
   free(cnt); free(cell); free(fill); free(lst); free(rot); free(rotbin); free(vMatchedDistance); free(vnMatches21);
   return nmatches;
 }
+
+/* ---- projection searches (SearchByProjection overloads) ---- */
+typedef struct {
+  int *cnt, *lst; /* cell CSR (cell = ix * GRID_ROWS + iy), keypoint order inside a cell */
+  float wi, hi;   /* mfGridElementWidthInv / HeightInv */
+} orc_grid;
+
+/* Frame::AssignFeaturesToGrid (Frame.cc:1268-1285). */
+static void grid_build(const orc_frame *F, orc_grid *G) {
+  const int n = F->n;
+  G->cnt = (int *)calloc(GRID_COLS * GRID_ROWS + 1, sizeof(int));
+  G->lst = (int *)malloc(sizeof(int) * (n > 0 ? n : 1));
+  int *cell = (int *)malloc(sizeof(int) * (n > 0 ? n : 1));
+  for (int i = 0; i < n; ++i) {
+    int px, py;
+    cell[i] = pos_in_grid(&F->bounds, &F->kps[i], &px, &py) ? px * GRID_ROWS + py : -1;
+    if (cell[i] >= 0) G->cnt[cell[i] + 1]++;
+  }
+  for (int c = 0; c < GRID_COLS * GRID_ROWS; ++c) G->cnt[c + 1] += G->cnt[c];
+  int *fill = (int *)malloc(sizeof(int) * GRID_COLS * GRID_ROWS);
+  memcpy(fill, G->cnt, sizeof(int) * GRID_COLS * GRID_ROWS);
+  for (int i = 0; i < n; ++i)
+    if (cell[i] >= 0) G->lst[fill[cell[i]]++] = i;
+  G->wi = (float)GRID_COLS / (F->bounds.max_x - F->bounds.min_x);
+  G->hi = (float)GRID_ROWS / (F->bounds.max_y - F->bounds.min_y);
+  free(cell);
+  free(fill);
+}
+
+static void grid_free(orc_grid *G) {
+  free(G->cnt);
+  free(G->lst);
+}
+
+/* Frame::GetFeaturesInArea (Frame.cc:1463-1552), bCheckLevels as written. */
+static int area(const orc_frame *F, const orc_grid *G, float x, float y, float r, int minLevel, int maxLevel,
+                int *out) {
+  const orc_frame_grid *g = &F->bounds;
+  const int nMinCellX = imax(0, (int)floorf((x - g->min_x - r) * G->wi));
+  if (nMinCellX >= GRID_COLS) return 0;
+  const int nMaxCellX = imin(GRID_COLS - 1, (int)ceilf((x - g->min_x + r) * G->wi));
+  if (nMaxCellX < 0) return 0;
+  const int nMinCellY = imax(0, (int)floorf((y - g->min_y - r) * G->hi));
+  if (nMinCellY >= GRID_ROWS) return 0;
+  const int nMaxCellY = imin(GRID_ROWS - 1, (int)ceilf((y - g->min_y + r) * G->hi));
+  if (nMaxCellY < 0) return 0;
+  const int bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+  int n = 0;
+  for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+    for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+      const int c = ix * GRID_ROWS + iy;
+      for (int q = G->cnt[c]; q < G->cnt[c + 1]; ++q) {
+        const orc_kp *kpUn = &F->kps[G->lst[q]];
+        if (bCheckLevels) {
+          if (kpUn->octave < minLevel) continue;
+          if (maxLevel >= 0)
+            if (kpUn->octave > maxLevel) continue;
+        }
+        const float distx = kpUn->x - x, disty = kpUn->y - y;
+        if (fabsf(distx) < r && fabsf(disty) < r) out[n++] = G->lst[q];
+      }
+    }
+  return n;
+}
+
+int orc_features_in_area(const orc_frame *F, float x, float y, float r, int min_level, int max_level, int *out) {
+  orc_grid G;
+  grid_build(F, &G);
+  const int n = area(F, &G, x, y, r, min_level, max_level, out);
+  grid_free(&G);
+  return n;
+}
+
+#define TH_HIGH 100
+
+/* ORBmatcher::RadiusByViewingCos (ORBmatcher.cc:183-190). */
+static float radius_by_viewing_cos(float viewCos) { return viewCos > 0.998 ? 2.5f : 4.0f; }
+
+int orc_search_by_projection_local(orc_frame *F, const orc_track_point *mps, const uint8_t *mp_desc, int n_mp,
+                                   float th, float nnratio) {
+  orc_grid G;
+  grid_build(F, &G);
+  int *vIndices = (int *)malloc(sizeof(int) * (F->n > 0 ? F->n : 1));
+  int nmatches = 0;
+  const int bFactor = th != 1.0;
+  for (int iMP = 0; iMP < n_mp; iMP++) {
+    const orc_track_point *pMP = &mps[iMP];
+    if (!pMP->in_view) continue; /* :78-83 */
+    if (pMP->bad) continue;
+    const int nPredictedLevel = pMP->level;
+    float r = radius_by_viewing_cos(pMP->view_cos);
+    if (bFactor) r *= th;
+    const float scale = F->scale_factors[nPredictedLevel];
+    const int nI = area(F, &G, pMP->proj_x, pMP->proj_y, r * scale, nPredictedLevel - 1, nPredictedLevel, vIndices);
+    if (nI == 0) continue;
+    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+    for (int v = 0; v < nI; ++v) { /* :118-155 */
+      const int idx = vIndices[v];
+      if (F->slot_mp[idx] >= 0)
+        if (F->slot_obs[idx]) continue;
+      if (F->uright && F->uright[idx] > 0) {
+        const float er = fabsf(pMP->proj_xr - F->uright[idx]);
+        if (er > r * scale) continue;
+      }
+      const int dist = orc_hamming(mp_desc + 32 * (size_t)iMP, F->desc + 32 * (size_t)idx);
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestLevel2 = bestLevel;
+        bestLevel = F->kps[idx].octave;
+        bestIdx = idx;
+      } else if (dist < bestDist2) {
+        bestLevel2 = F->kps[idx].octave;
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= TH_HIGH) { /* :160-175 */
+      if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+      F->slot_mp[bestIdx] = pMP->id;
+      F->slot_obs[bestIdx] = pMP->has_obs;
+      nmatches++;
+    }
+  }
+  free(vIndices);
+  grid_free(&G);
+  return nmatches;
+}
+
+/* cv::Mat 3x3 * 3x1 (+ 3x1) on CV_32F, OpenCV's small-matrix gemm path: float
+ * products summed left to right, then alpha * t + beta * c in double — with
+ * alpha = beta = 1 that is one float addition. OpenCV is absent here, so this
+ * step is "parity unpinned" like the extractor's OpenCV stages. */
+static void mat3_mul_add(const float *T, int transpose, const float *x, const float *c, float sign, float *out) {
+  for (int i = 0; i < 3; ++i) {
+    const float a0 = transpose ? T[0 * 4 + i] : T[i * 4 + 0];
+    const float a1 = transpose ? T[1 * 4 + i] : T[i * 4 + 1];
+    const float a2 = transpose ? T[2 * 4 + i] : T[i * 4 + 2];
+    const float t0 = a0 * x[0] + a1 * x[1] + a2 * x[2];
+    out[i] = c ? (float)((double)t0 * sign + (double)c[i]) : (float)((double)t0 * sign);
+  }
+}
+
+/* ComputeThreeMaxima (ORBmatcher.cc:2048-2090) over bin sizes. */
+static void three_maxima(const int *hist, int *i1, int *i2, int *i3) {
+  int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+  for (int i = 0; i < HISTO_LENGTH; i++) {
+    const int s = hist[i];
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s;
+      ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) {
+    ind2 = -1;
+    ind3 = -1;
+  } else if (max3 < 0.1f * (float)max1) {
+    ind3 = -1;
+  }
+  *i1 = ind1;
+  *i2 = ind2;
+  *i3 = ind3;
+}
+
+int orc_search_by_projection_last(orc_frame *F, const float *Tcw, const float *Tlw, const orc_last_point *lp,
+                                  const uint8_t *ldesc, int n_last, float th, int mono, int check_ori) {
+  orc_grid G;
+  grid_build(F, &G);
+  int *vIndices2 = (int *)malloc(sizeof(int) * (F->n > 0 ? F->n : 1));
+  /* rotHist[bin] lists in push order: (bin, slot) records, replayed per bin */
+  int *rot_bin = (int *)malloc(sizeof(int) * (n_last > 0 ? n_last : 1));
+  int *rot_idx = (int *)malloc(sizeof(int) * (n_last > 0 ? n_last : 1));
+  int nrot = 0, hist[HISTO_LENGTH] = {0};
+  const float factor = HISTO_LENGTH / 360.0f;
+  int nmatches = 0;
+  const float tcw[3] = {Tcw[3], Tcw[7], Tcw[11]}, tlw[3] = {Tlw[3], Tlw[7], Tlw[11]};
+  float twc[3], tlc[3];
+  mat3_mul_add(Tcw, 1, tcw, NULL, -1.0f, twc); /* twc = -Rcw.t()*tcw (:1730) */
+  mat3_mul_add(Tlw, 0, twc, tlw, 1.0f, tlc);   /* tlc = Rlw*twc+tlw (:1735) */
+  const int bForward = tlc[2] > F->mb && !mono;
+  const int bBackward = -tlc[2] > F->mb && !mono;
+  for (int i = 0; i < n_last; i++) {
+    const orc_last_point *pMP = &lp[i];
+    if (pMP->id < 0 || pMP->outlier) continue;
+    const float x3Dw[3] = {pMP->x, pMP->y, pMP->z};
+    float x3Dc[3];
+    mat3_mul_add(Tcw, 0, x3Dw, tcw, 1.0f, x3Dc);
+    const float xc = x3Dc[0], yc = x3Dc[1];
+    const float invzc = (float)(1.0 / (double)x3Dc[2]);
+    if (invzc < 0) continue;
+    const float u = F->fx * xc * invzc + F->cx, v = F->fy * yc * invzc + F->cy;
+    if (u < F->bounds.min_x || u > F->bounds.max_x) continue;
+    if (v < F->bounds.min_y || v > F->bounds.max_y) continue;
+    const int nLastOctave = pMP->octave;
+    const float radius = th * F->scale_factors[nLastOctave];
+    int nI;
+    if (bForward)
+      nI = area(F, &G, u, v, radius, nLastOctave, -1, vIndices2);
+    else if (bBackward)
+      nI = area(F, &G, u, v, radius, 0, nLastOctave, vIndices2);
+    else
+      nI = area(F, &G, u, v, radius, nLastOctave - 1, nLastOctave + 1, vIndices2);
+    if (nI == 0) continue;
+    int bestDist = 256, bestIdx2 = -1;
+    for (int q = 0; q < nI; ++q) { /* :1806-1836 */
+      const int i2 = vIndices2[q];
+      if (F->slot_mp[i2] >= 0)
+        if (F->slot_obs[i2]) continue;
+      if (F->uright && F->uright[i2] > 0) {
+        const float ur = u - F->bf * invzc;
+        const float er = fabsf(ur - F->uright[i2]);
+        if (er > radius) continue;
+      }
+      const int dist = orc_hamming(ldesc + 32 * (size_t)i, F->desc + 32 * (size_t)i2);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = i2;
+      }
+    }
+    if (bestDist <= TH_HIGH) { /* :1839-1858 */
+      F->slot_mp[bestIdx2] = pMP->id;
+      F->slot_obs[bestIdx2] = pMP->has_obs;
+      nmatches++;
+      if (check_ori) {
+        float rot = pMP->angle - F->kps[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)roundf(rot * factor);
+        if (bin == HISTO_LENGTH) bin = 0;
+        rot_bin[nrot] = bin;
+        rot_idx[nrot++] = bestIdx2;
+        hist[bin]++;
+      }
+    }
+  }
+  if (check_ori) { /* :1862-1880: every entry of a rejected bin is cleared */
+    int ind1, ind2, ind3;
+    three_maxima(hist, &ind1, &ind2, &ind3);
+    for (int b = 0; b < HISTO_LENGTH; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (int q = 0; q < nrot; ++q)
+        if (rot_bin[q] == b) {
+          F->slot_mp[rot_idx[q]] = -1;
+          F->slot_obs[rot_idx[q]] = 0;
+          nmatches--;
+        }
+    }
+  }
+  free(vIndices2);
+  free(rot_bin);
+  free(rot_idx);
+  grid_free(&G);
+  return nmatches;
+}

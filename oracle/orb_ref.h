@@ -1,7 +1,7 @@
 /* TEST INFRASTRUCTURE — CPU restatement of the reference's ORB front end
  * (SURVEY.md §8 row f3): ORBextractor::operator() (src/frontend/ORBextractor.cc)
- * and ORBmatcher::DescriptorDistance / SearchForInitialization
- * (src/frontend/ORBmatcher.cc). Only tests/, __graft_entry__.smoke() and
+ * and ORBmatcher::DescriptorDistance / SearchForInitialization /
+ * SearchByProjection (src/frontend/ORBmatcher.cc). Only tests/, __graft_entry__.smoke() and
  * bench.py's cpu_baseline leg use it, as the checker.
  *
  * PARITY: the extractor calls OpenCV 3.3.1 (cv::FAST, cv::resize INTER_LINEAR,
@@ -11,8 +11,12 @@
  * against the reference binary. Everything the reference implements itself
  * (cell grid, FAST thresholds fallback, quadtree distribution, IC_Angle,
  * steered BRIEF, Hamming distance, SearchForInitialization with its
- * tie-breaking, rotation histogram and ComputeThreeMaxima) follows its source
- * line for line, cited per function. */
+ * tie-breaking, rotation histogram and ComputeThreeMaxima, GetFeaturesInArea
+ * and the projection searches' acceptance rules) follows its source line for
+ * line, cited per function; the projection searches are cross-checked against
+ * a second, pure-Python transliteration (tests/test_orb_oracle.py). The one
+ * cv::Mat product they use (3x3 * 3x1 + 3x1 in SearchByProjection(Frame,
+ * Frame)) is restated from OpenCV's small-matrix gemm and is unpinned. */
 #ifndef ORC_ORB_REF_H
 #define ORC_ORB_REF_H
 #include <stdint.h>
@@ -70,4 +74,58 @@ typedef struct orc_frame_grid {
  * window) (ORBmatcher.cc:573-718). prev [n1][2] is updated in place. */
 int orc_search_for_init(const orc_kp *k1, const uint8_t *d1, int n1, const orc_kp *k2, const uint8_t *d2, int n2,
                         const orc_frame_grid *g2, float *prev, int *m12, int window, float nnratio, int check_ori);
+/* The Frame fields ORBmatcher's projection searches read and write
+ * (include/data_structure/Frame.h): mvKeysUn, mDescriptors, mvuRight (NULL:
+ * monocular, every entry < 0), the grid bounds, mvScaleFactors, the
+ * intrinsics and mb / mbf, and mvpMapPoints as map-point ids (slot_mp, -1 =
+ * NULL) with slot_obs = that point's Observations() > 0. Layout equal to
+ * sqlm_orb_frame (include/sqrtlm_orb.h). */
+typedef struct orc_frame {
+  const orc_kp *kps;
+  const uint8_t *desc;
+  const float *uright;
+  int n;
+  orc_frame_grid bounds;
+  const float *scale_factors;
+  int n_levels;
+  float fx, fy, cx, cy, bf, mb;
+  int *slot_mp;
+  uint8_t *slot_obs;
+} orc_frame;
+
+/* MapPoint tracking fields (MapPoint.h mnId, mTrackProjX/Y/XR, mTrackViewCos,
+ * mnTrackScaleLevel, mbTrackInView, isBad(), Observations() > 0). */
+typedef struct orc_track_point {
+  int id;
+  float proj_x, proj_y, proj_xr, view_cos;
+  int level;
+  uint8_t in_view, bad, has_obs, pad;
+} orc_track_point;
+
+/* One LastFrame keypoint slot: mvpMapPoints[i] (id, -1 = NULL), its world
+ * position GetWorldPos(), mvKeys[i].octave, mvKeysUn[i].angle, mvbOutlier[i],
+ * the point's Observations() > 0. */
+typedef struct orc_last_point {
+  int id;
+  float x, y, z;
+  int octave;
+  float angle;
+  uint8_t outlier, has_obs, pad[2];
+} orc_last_point;
+
+/* Frame::GetFeaturesInArea(x, y, r, minLevel, maxLevel) (Frame.cc:1463-1552)
+ * over F's grid (built by AssignFeaturesToGrid, :1268-1285); writes the
+ * indices in the reference's order into out (capacity F->n), returns the count. */
+int orc_features_in_area(const orc_frame *F, float x, float y, float r, int min_level, int max_level, int *out);
+
+/* ORBmatcher(nnratio).SearchByProjection(F, vpMapPoints, th)
+ * (ORBmatcher.cc:67-181): F->slot_mp / slot_obs updated; returns nmatches. */
+int orc_search_by_projection_local(orc_frame *F, const orc_track_point *mps, const uint8_t *mp_desc, int n_mp,
+                                   float th, float nnratio);
+
+/* ORBmatcher(., check_ori).SearchByProjection(CurrentFrame, LastFrame, th,
+ * bMono) (ORBmatcher.cc:1717-1883). Tcw / Tlw: the 3x4 rows of
+ * CurrentFrame.mTcw / LastFrame.mTcw (float, row-major). */
+int orc_search_by_projection_last(orc_frame *F, const float *Tcw, const float *Tlw, const orc_last_point *lp,
+                                  const uint8_t *ldesc, int n_last, float th, int mono, int check_ori);
 #endif

@@ -1820,6 +1820,19 @@ int sqlm_orb_search_for_init(sqlm_ctx *c, const sqlm_keypoint *k1, const uint8_t
   return orb_search_for_init(c->orb, k1, d1, n1, k2, d2, n2, f2, prev, m12, window, nnratio, check_ori, n_matches);
 }
 
+int sqlm_orb_search_by_projection_local(sqlm_ctx *c, sqlm_orb_frame *F, const sqlm_track_point *mps,
+                                        const uint8_t *mp_desc, int n_mp, float th, float nnratio, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_by_projection_local(c->orb, F, mps, mp_desc, n_mp, th, nnratio, n_matches);
+}
+
+int sqlm_orb_search_by_projection_last(sqlm_ctx *c, sqlm_orb_frame *F, const float *Tcw, const float *Tlw,
+                                       const sqlm_last_point *lp, const uint8_t *ldesc, int n_last, float th,
+                                       int mono, int check_ori, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_by_projection_last(c->orb, F, Tcw, Tlw, lp, ldesc, n_last, th, mono, check_ori, n_matches);
+}
+
 int sqlm_orb_bench_extract(sqlm_ctx *c, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
                            int reps, double *ms_per_frame, double *stage_ms) {
   if (int r = orb_engine(c)) return r;

@@ -286,5 +286,10 @@ int orb_search_for_init(OrbEngine *e, const struct sqlm_keypoint *k1, const uint
                         const struct sqlm_keypoint *k2, const uint8_t *d2, int n2,
                         const struct sqlm_frame_bounds *f2, float *prev, int32_t *m12, int window, float nnratio,
                         int check_ori, int *n_matches);
+int orb_search_by_projection_local(OrbEngine *e, struct sqlm_orb_frame *F, const struct sqlm_track_point *mps,
+                                   const uint8_t *mp_desc, int n_mp, float th, float nnratio, int *n_matches);
+int orb_search_by_projection_last(OrbEngine *e, struct sqlm_orb_frame *F, const float *Tcw, const float *Tlw,
+                                  const struct sqlm_last_point *lp, const uint8_t *ldesc, int n_last, float th,
+                                  int mono, int check_ori, int *n_matches);
 
 }  // namespace sqlm

@@ -25,7 +25,7 @@
 //                   256 steered-BRIEF tests, 4 per lane, nibbles merged by a
 //                   lane shuffle.
 // Matching: k_orb_bf (one thread per query, train descriptors staged through
-// LDS, v_bcnt popcounts) and, for SearchForInitialization, k_sfi_list (one
+// LDS, v_bcnt popcounts) and, for the windowed searches, k_area_list (one
 // wavefront per query enumerates the frame grid window in the reference's
 // order and emits (candidate, distance) pairs); the order-dependent
 // acceptance loop (vMatchedDistance, vnMatches21, rotation histogram) runs on
@@ -61,7 +61,7 @@ constexpr int kCellMax = 72;    // largest FAST view side (cell <= 60 + 6 overla
 constexpr int kCellCap = 1024;  // candidates per cell (3x3 NMS: <= 33 x 33)
 constexpr int kMaxLevels = 16;
 constexpr int kGridCols = 64, kGridRows = 48;  // FRAME_GRID_COLS / ROWS (Frame.h:70-75)
-constexpr int kHistoLength = 30, kThLow = 50;  // ORBmatcher.cc:46-48
+constexpr int kHistoLength = 30, kThLow = 50, kThHigh = 100;  // ORBmatcher.cc:46-48
 
 struct OrbCell {
   int img_off, pitch;  // level image in the packed pyramid
@@ -480,45 +480,56 @@ __global__ __launch_bounds__(256) void k_orb_bf(const uint32_t *__restrict__ q, 
   }
 }
 
-struct SfiArgs {
-  const float *q;          // [n1][4] prev.x prev.y octave(as float bits: level) pad
-  const uint32_t *d1;      // [n1][8]
+// One GetFeaturesInArea query: window centre, half-size r, and the level
+// range packed as (minLevel & 0xffff) | (maxLevel << 16) (both int16);
+// kAreaSkip marks a query the caller skips before the area search.
+constexpr int kAreaSkip = (int)0x80008000;
+__host__ __device__ inline int area_levels(int min_level, int max_level) {
+  return (int)(((unsigned)min_level & 0xffffu) | ((unsigned)max_level << 16));
+}
+
+struct AreaArgs {
+  const float4 *q;         // [n1] x y r levels(int bits)
+  const uint32_t *d1;      // [n1][8] query descriptors
   const float *k2;         // [n2][4] x y octave pad
   const uint32_t *d2;      // [n2][8]
   const int *cell_ptr;     // [64*48+1] grid CSR (cell = ix*48 + iy)
   const int *cell_idx;     // keypoint indices in cell order
-  float min_x, min_y, wi, hi, r;
+  float min_x, min_y, wi, hi;
   int n1;
 };
 
-// GetFeaturesInArea (Frame.cc:1463-1552) + DescriptorDistance for one query:
-// pass 0 counts the candidates, pass 1 writes (i2, dist) in the reference's
-// iteration order (cells ix-major, then cell insertion order).
+// GetFeaturesInArea (Frame.cc:1463-1552) + DescriptorDistance for one query
+// per wave: pass 0 counts the candidates, pass 1 writes (i2, dist) in the
+// reference's iteration order (cells ix-major, then cell insertion order).
 template <int PASS>
-__global__ __launch_bounds__(256) void k_sfi_list(SfiArgs A, int *__restrict__ cnt, const int *__restrict__ off,
-                                                  int2 *__restrict__ pairs) {
+__global__ __launch_bounds__(256) void k_area_list(AreaArgs A, int *__restrict__ cnt, const int *__restrict__ off,
+                                                   int2 *__restrict__ pairs) {
   const int lane = threadIdx.x & 63;
   const int i1 = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i1 >= A.n1) return;
-  const float x = A.q[4 * i1], y = A.q[4 * i1 + 1];
-  const int level = __float_as_int(A.q[4 * i1 + 2]);
+  const float4 qv = A.q[i1];
+  const float x = qv.x, y = qv.y, r = qv.z;
+  const int lv = __float_as_int(qv.w);
+  const int minLevel = (int)(short)(lv & 0xffff), maxLevel = lv >> 16;
+  const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
   int run = 0;
-  bool ok = level <= 0;
+  bool ok = lv != kAreaSkip;
   int nMinCellX = 0, nMaxCellX = -1, nMinCellY = 0, nMaxCellY = -1;
   if (ok) {
-    nMinCellX = max(0, (int)floorf((x - A.min_x - A.r) * A.wi));
+    nMinCellX = max(0, (int)floorf((x - A.min_x - r) * A.wi));
     ok = nMinCellX < kGridCols;
   }
   if (ok) {
-    nMaxCellX = min(kGridCols - 1, (int)ceilf((x - A.min_x + A.r) * A.wi));
+    nMaxCellX = min(kGridCols - 1, (int)ceilf((x - A.min_x + r) * A.wi));
     ok = nMaxCellX >= 0;
   }
   if (ok) {
-    nMinCellY = max(0, (int)floorf((y - A.min_y - A.r) * A.hi));
+    nMinCellY = max(0, (int)floorf((y - A.min_y - r) * A.hi));
     ok = nMinCellY < kGridRows;
   }
   if (ok) {
-    nMaxCellY = min(kGridRows - 1, (int)ceilf((y - A.min_y + A.r) * A.hi));
+    nMaxCellY = min(kGridRows - 1, (int)ceilf((y - A.min_y + r) * A.hi));
     ok = nMaxCellY >= 0;
   }
   uint32_t my[8];
@@ -539,10 +550,9 @@ __global__ __launch_bounds__(256) void k_sfi_list(SfiArgs A, int *__restrict__ c
             i2 = A.cell_idx[j];
             const float kx = A.k2[4 * i2], ky = A.k2[4 * i2 + 1];
             const int oct = __float_as_int(A.k2[4 * i2 + 2]);
-            // bCheckLevels with minLevel = maxLevel = level1 (= 0)
-            hit = !(oct < level) && !(oct > level);
+            hit = !bCheckLevels || (!(oct < minLevel) && !(maxLevel >= 0 && oct > maxLevel));
             const float distx = kx - x, disty = ky - y;
-            hit = hit && fabsf(distx) < A.r && fabsf(disty) < A.r;
+            hit = hit && fabsf(distx) < r && fabsf(disty) < r;
           }
           const unsigned long long m = __ballot(hit);
           if (PASS == 1 && hit) {
@@ -1163,17 +1173,19 @@ int orb_match_bf(OrbEngine *e, const uint8_t *query, int nq, const uint8_t *trai
   return SQLM_OK;
 }
 
-int orb_search_for_init(OrbEngine *e, const sqlm_keypoint *k1, const uint8_t *d1, int n1, const sqlm_keypoint *k2,
-                        const uint8_t *d2, int n2, const sqlm_frame_bounds *f2, float *prev, int32_t *m12, int window,
-                        float nnratio, int check_ori, int *n_matches) {
-  if (n1 < 0 || n2 < 0 || !f2 || (n1 && (!k1 || !d1 || !prev || !m12)) || (n2 && (!k2 || !d2)))
-    return SQLM_ERR_INVALID_ARG;
-  for (int i = 0; i < n1; ++i) m12[i] = -1;
-  if (n_matches) *n_matches = 0;
+// The candidate lists of n_q GetFeaturesInArea queries over frame 2's grid
+// (AssignFeaturesToGrid, Frame.cc:1268-1285, with PosInGrid :1554-1565):
+// hoff [n_q + 1] offsets into hp = (keypoint index, Hamming distance to the
+// query's descriptor qdesc [n_q][32]) in the reference's candidate order.
+static int area_search(OrbEngine *e, const sqlm_keypoint *k2, const uint8_t *d2, int n2, const sqlm_frame_bounds *f2,
+                       const std::vector<float4> &hq, const uint8_t *qdesc, std::vector<int> &hoff,
+                       std::vector<int2> &hp) {
+  const int n1 = (int)hq.size();
+  hoff.assign(n1 + 1, 0);
+  hp.clear();
   if (n1 == 0) return SQLM_OK;
   const float wi = static_cast<float>(kGridCols) / static_cast<float>(f2->max_x - f2->min_x);
   const float hi = static_cast<float>(kGridRows) / static_cast<float>(f2->max_y - f2->min_y);
-  // Frame::AssignFeaturesToGrid (Frame.cc:1268-1285) with PosInGrid (:1554-1565)
   std::vector<int> cell_of(n2), ptr(kGridCols * kGridRows + 1, 0), idx;
   for (int i = 0; i < n2; ++i) {
     const int px = (int)std::round((k2[i].x - f2->min_x) * wi), py = (int)std::round((k2[i].y - f2->min_y) * hi);
@@ -1187,27 +1199,22 @@ int orb_search_for_init(OrbEngine *e, const sqlm_keypoint *k1, const uint8_t *d1
     for (int i = 0; i < n2; ++i)
       if (cell_of[i] >= 0) idx[fill[cell_of[i]]++] = i;
   }
-  std::vector<float> hq((size_t)4 * n1), hk2((size_t)4 * std::max(n2, 1));
-  for (int i = 0; i < n1; ++i) {
-    hq[4 * i] = prev[2 * i];
-    hq[4 * i + 1] = prev[2 * i + 1];
-    std::memcpy(&hq[4 * i + 2], &k1[i].octave, 4);
-  }
+  std::vector<float> hk2((size_t)4 * std::max(n2, 1));
   for (int i = 0; i < n2; ++i) {
     hk2[4 * i] = k2[i].x;
     hk2[4 * i + 1] = k2[i].y;
     std::memcpy(&hk2[4 * i + 2], &k2[i].octave, 4);
   }
-  SfiArgs A;
-  float *dq = e->get<float>(e->q, hq.size());
+  AreaArgs A;
+  float4 *dq = e->get<float4>(e->q, n1);
   uint32_t *dd1 = e->get<uint32_t>(e->qd, (size_t)8 * n1);
   float *dk2 = e->get<float>(e->t, hk2.size());
   uint32_t *dd2 = e->get<uint32_t>(e->td, (size_t)8 * std::max(n2, 1));
   int *dptr = e->get<int>(e->grid, ptr.size()), *didx = e->get<int>(e->gidx, idx.size());
   int *dcnt = e->get<int>(e->bidx, n1), *doff = e->get<int>(e->bd, n1 + 1);
   if (!dq || !dd1 || !dk2 || !dd2 || !dptr || !didx || !dcnt || !doff) return SQLM_ERR_OOM;
-  if (hipMemcpyAsync(dq, hq.data(), sizeof(float) * hq.size(), hipMemcpyHostToDevice, e->st) != hipSuccess ||
-      hipMemcpyAsync(dd1, d1, (size_t)32 * n1, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+  if (hipMemcpyAsync(dq, hq.data(), sizeof(float4) * n1, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(dd1, qdesc, (size_t)32 * n1, hipMemcpyHostToDevice, e->st) != hipSuccess ||
       hipMemcpyAsync(dk2, hk2.data(), sizeof(float) * hk2.size(), hipMemcpyHostToDevice, e->st) != hipSuccess ||
       (n2 && hipMemcpyAsync(dd2, d2, (size_t)32 * n2, hipMemcpyHostToDevice, e->st) != hipSuccess) ||
       hipMemcpyAsync(dptr, ptr.data(), sizeof(int) * ptr.size(), hipMemcpyHostToDevice, e->st) != hipSuccess ||
@@ -1223,23 +1230,49 @@ int orb_search_for_init(OrbEngine *e, const sqlm_keypoint *k1, const uint8_t *d1
   A.min_y = f2->min_y;
   A.wi = wi;
   A.hi = hi;
-  A.r = (float)window;
   A.n1 = n1;
   const dim3 g((n1 + 3) / 4);
-  hipLaunchKernelGGL(k_sfi_list<0>, g, dim3(256), 0, e->st, A, dcnt, (const int *)nullptr, (int2 *)nullptr);
+  hipLaunchKernelGGL(k_area_list<0>, g, dim3(256), 0, e->st, A, dcnt, (const int *)nullptr, (int2 *)nullptr);
   hipLaunchKernelGGL(k_orb_scan, dim3(1), dim3(1024), 0, e->st, dcnt, n1, doff);
-  std::vector<int> hoff(n1 + 1);
   if (hipMemcpyAsync(hoff.data(), doff, sizeof(int) * (n1 + 1), hipMemcpyDeviceToHost, e->st) != hipSuccess ||
       hipStreamSynchronize(e->st) != hipSuccess)
     return SQLM_ERR_HIP;
   const int total = hoff[n1];
   int2 *dpairs = e->get<int2>(e->pairs, std::max(total, 1));
   if (!dpairs) return SQLM_ERR_OOM;
-  hipLaunchKernelGGL(k_sfi_list<1>, g, dim3(256), 0, e->st, A, (int *)nullptr, (const int *)doff, dpairs);
-  std::vector<int2> hp(std::max(total, 1));
+  hipLaunchKernelGGL(k_area_list<1>, g, dim3(256), 0, e->st, A, (int *)nullptr, (const int *)doff, dpairs);
+  hp.resize(std::max(total, 1));
   if (total && hipMemcpyAsync(hp.data(), dpairs, sizeof(int2) * total, hipMemcpyDeviceToHost, e->st) != hipSuccess)
     return SQLM_ERR_HIP;
   if (hipStreamSynchronize(e->st) != hipSuccess) return SQLM_ERR_HIP;
+  return SQLM_OK;
+}
+
+static float4 area_query(float x, float y, float r, int lv) {
+  float4 q;
+  q.x = x;
+  q.y = y;
+  q.z = r;
+  std::memcpy(&q.w, &lv, 4);
+  return q;
+}
+
+int orb_search_for_init(OrbEngine *e, const sqlm_keypoint *k1, const uint8_t *d1, int n1, const sqlm_keypoint *k2,
+                        const uint8_t *d2, int n2, const sqlm_frame_bounds *f2, float *prev, int32_t *m12, int window,
+                        float nnratio, int check_ori, int *n_matches) {
+  if (n1 < 0 || n2 < 0 || !f2 || (n1 && (!k1 || !d1 || !prev || !m12)) || (n2 && (!k2 || !d2)))
+    return SQLM_ERR_INVALID_ARG;
+  for (int i = 0; i < n1; ++i) m12[i] = -1;
+  if (n_matches) *n_matches = 0;
+  if (n1 == 0) return SQLM_OK;
+  // GetFeaturesInArea(prev.x, prev.y, windowSize, level1, level1) for level1 == 0 (ORBmatcher.cc:594-612)
+  std::vector<float4> hq(n1);
+  for (int i = 0; i < n1; ++i)
+    hq[i] = area_query(prev[2 * i], prev[2 * i + 1], (float)window,
+                       k1[i].octave > 0 ? kAreaSkip : area_levels(k1[i].octave, k1[i].octave));
+  std::vector<int> hoff;
+  std::vector<int2> hp;
+  if (int rc = area_search(e, k2, d2, n2, f2, hq, d1, hoff, hp)) return rc;
   // acceptance loop (ORBmatcher.cc:594-682): order-dependent, over the GPU lists
   std::vector<int> vMatchedDistance(n2, INT_MAX), vnMatches21(n2, -1), rot_i, rot_bin;
   int hist[kHistoLength] = {0};
@@ -1314,6 +1347,193 @@ int orb_search_for_init(OrbEngine *e, const sqlm_keypoint *k1, const uint8_t *d1
       prev[2 * i1] = k2[m12[i1]].x;
       prev[2 * i1 + 1] = k2[m12[i1]].y;
     }
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+static bool frame_ok(const sqlm_orb_frame *F) {
+  return F && F->n >= 0 && F->n_levels > 0 && F->scale_factors && F->slot_mp && F->slot_obs &&
+         (F->n == 0 || (F->kps && F->desc));
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:2048-2090) over bin sizes.
+static void three_maxima(const int *hist, int &ind1, int &ind2, int &ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  ind1 = ind2 = ind3 = -1;
+  for (int i = 0; i < kHistoLength; i++) {
+    const int s = hist[i];
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s;
+      ind3 = i;
+    }
+  }
+  if (max2 < 0.1f * (float)max1) {
+    ind2 = -1;
+    ind3 = -1;
+  } else if (max3 < 0.1f * (float)max1) {
+    ind3 = -1;
+  }
+}
+
+int orb_search_by_projection_local(OrbEngine *e, sqlm_orb_frame *F, const sqlm_track_point *mps,
+                                   const uint8_t *mp_desc, int n_mp, float th, float nnratio, int *n_matches) {
+  if (!frame_ok(F) || n_mp < 0 || (n_mp && (!mps || !mp_desc))) return SQLM_ERR_INVALID_ARG;
+  if (n_matches) *n_matches = 0;
+  const bool bFactor = th != 1.0;
+  // ORBmatcher.cc:78-101: the window of every point still to be projected
+  std::vector<float4> hq(n_mp);
+  std::vector<float> rwin(n_mp);
+  for (int i = 0; i < n_mp; ++i) {
+    const sqlm_track_point &p = mps[i];
+    if (!p.in_view || p.bad || p.level < 0 || p.level >= F->n_levels) {
+      if (p.in_view && !p.bad) return SQLM_ERR_INVALID_ARG;  // mnTrackScaleLevel outside mvScaleFactors
+      hq[i] = area_query(0.f, 0.f, 0.f, kAreaSkip);
+      continue;
+    }
+    float r = p.view_cos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:183-190)
+    if (bFactor) r *= th;
+    rwin[i] = r * F->scale_factors[p.level];
+    hq[i] = area_query(p.proj_x, p.proj_y, rwin[i], area_levels(p.level - 1, p.level));
+  }
+  std::vector<int> hoff;
+  std::vector<int2> hp;
+  if (int rc = area_search(e, F->kps, F->desc, F->n, &F->bounds, hq, mp_desc, hoff, hp)) return rc;
+  int nmatches = 0;
+  for (int i = 0; i < n_mp; ++i) {  // :118-175, in point order over the GPU lists
+    if (hoff[i + 1] == hoff[i]) continue;
+    int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+    for (int q = hoff[i]; q < hoff[i + 1]; ++q) {
+      const int idx = hp[q].x, dist = hp[q].y;
+      if (F->slot_mp[idx] >= 0 && F->slot_obs[idx]) continue;
+      if (F->uright && F->uright[idx] > 0) {
+        const float er = fabsf(mps[i].proj_xr - F->uright[idx]);
+        if (er > rwin[i]) continue;
+      }
+      if (dist < bestDist) {
+        bestDist2 = bestDist;
+        bestDist = dist;
+        bestLevel2 = bestLevel;
+        bestLevel = F->kps[idx].octave;
+        bestIdx = idx;
+      } else if (dist < bestDist2) {
+        bestLevel2 = F->kps[idx].octave;
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist <= kThHigh) {
+      if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+      F->slot_mp[bestIdx] = mps[i].id;
+      F->slot_obs[bestIdx] = mps[i].has_obs;
+      nmatches++;
+    }
+  }
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+// cv::Mat 3x3 (optionally transposed) * 3x1 (+ 3x1) on CV_32F as OpenCV's
+// small-matrix gemm evaluates it: float dot left to right, then alpha * t +
+// beta * c in double (one float addition for alpha = beta = 1).
+static void mat3_mul_add(const float *T, bool transpose, const float *x, const float *c, double sign, float *out) {
+  for (int i = 0; i < 3; ++i) {
+    const float a0 = transpose ? T[i] : T[i * 4], a1 = transpose ? T[4 + i] : T[i * 4 + 1],
+                a2 = transpose ? T[8 + i] : T[i * 4 + 2];
+    const float t0 = a0 * x[0] + a1 * x[1] + a2 * x[2];
+    out[i] = c ? (float)((double)t0 * sign + (double)c[i]) : (float)((double)t0 * sign);
+  }
+}
+
+int orb_search_by_projection_last(OrbEngine *e, sqlm_orb_frame *F, const float *Tcw, const float *Tlw,
+                                  const sqlm_last_point *lp, const uint8_t *ldesc, int n_last, float th, int mono,
+                                  int check_ori, int *n_matches) {
+  if (!frame_ok(F) || !Tcw || !Tlw || n_last < 0 || (n_last && (!lp || !ldesc))) return SQLM_ERR_INVALID_ARG;
+  if (n_matches) *n_matches = 0;
+  const float tcw[3] = {Tcw[3], Tcw[7], Tcw[11]}, tlw[3] = {Tlw[3], Tlw[7], Tlw[11]};
+  float twc[3], tlc[3];
+  mat3_mul_add(Tcw, true, tcw, nullptr, -1.0, twc);  // twc = -Rcw.t()*tcw (ORBmatcher.cc:1730)
+  mat3_mul_add(Tlw, false, twc, tlw, 1.0, tlc);      // tlc = Rlw*twc+tlw (:1735)
+  const bool bForward = tlc[2] > F->mb && !mono, bBackward = -tlc[2] > F->mb && !mono;
+  // :1744-1790: projection and window of every slot (host, float as the reference)
+  std::vector<float4> hq(n_last);
+  std::vector<float> hu(n_last), hinvz(n_last), hrad(n_last);
+  for (int i = 0; i < n_last; i++) {
+    hq[i] = area_query(0.f, 0.f, 0.f, kAreaSkip);
+    const sqlm_last_point &p = lp[i];
+    if (p.id < 0 || p.outlier) continue;
+    if (p.octave < 0 || p.octave >= F->n_levels) return SQLM_ERR_INVALID_ARG;
+    const float x3Dw[3] = {p.x, p.y, p.z};
+    float x3Dc[3];
+    mat3_mul_add(Tcw, false, x3Dw, tcw, 1.0, x3Dc);
+    const float xc = x3Dc[0], yc = x3Dc[1];
+    const float invzc = (float)(1.0 / (double)x3Dc[2]);
+    if (invzc < 0) continue;
+    const float u = F->fx * xc * invzc + F->cx, v = F->fy * yc * invzc + F->cy;
+    if (u < F->bounds.min_x || u > F->bounds.max_x) continue;
+    if (v < F->bounds.min_y || v > F->bounds.max_y) continue;
+    const int o = p.octave;
+    const float radius = th * F->scale_factors[o];
+    const int lv = bForward ? area_levels(o, -1) : bBackward ? area_levels(0, o) : area_levels(o - 1, o + 1);
+    hq[i] = area_query(u, v, radius, lv);
+    hu[i] = u;
+    hinvz[i] = invzc;
+    hrad[i] = radius;
+  }
+  std::vector<int> hoff;
+  std::vector<int2> hp;
+  if (int rc = area_search(e, F->kps, F->desc, F->n, &F->bounds, hq, ldesc, hoff, hp)) return rc;
+  int nmatches = 0, hist[kHistoLength] = {0};
+  std::vector<int> rot_bin, rot_idx;
+  const float factor = kHistoLength / 360.0f;
+  for (int i = 0; i < n_last; i++) {  // :1806-1858
+    if (hoff[i + 1] == hoff[i]) continue;
+    int bestDist = 256, bestIdx2 = -1;
+    for (int q = hoff[i]; q < hoff[i + 1]; ++q) {
+      const int i2 = hp[q].x, dist = hp[q].y;
+      if (F->slot_mp[i2] >= 0 && F->slot_obs[i2]) continue;
+      if (F->uright && F->uright[i2] > 0) {
+        const float ur = hu[i] - F->bf * hinvz[i];
+        const float er = fabsf(ur - F->uright[i2]);
+        if (er > hrad[i]) continue;
+      }
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = i2;
+      }
+    }
+    if (bestDist <= kThHigh) {
+      F->slot_mp[bestIdx2] = lp[i].id;
+      F->slot_obs[bestIdx2] = lp[i].has_obs;
+      nmatches++;
+      if (check_ori) {
+        float rot = lp[i].angle - F->kps[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == kHistoLength) bin = 0;
+        rot_bin.push_back(bin);
+        rot_idx.push_back(bestIdx2);
+        hist[bin]++;
+      }
+    }
+  }
+  if (check_ori) {  // :1862-1880: every entry of a rejected bin is cleared, bin by bin
+    int ind1, ind2, ind3;
+    three_maxima(hist, ind1, ind2, ind3);
+    for (int b = 0; b < kHistoLength; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (size_t q = 0; q < rot_bin.size(); ++q)
+        if (rot_bin[q] == b) {
+          F->slot_mp[rot_idx[q]] = -1;
+          F->slot_obs[rot_idx[q]] = 0;
+          nmatches--;
+        }
+    }
+  }
   if (n_matches) *n_matches = nmatches;
   return SQLM_OK;
 }

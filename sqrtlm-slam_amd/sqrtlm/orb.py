@@ -19,6 +19,15 @@ KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4
 
 
 
+# MapPoint tracking fields of one local map point (sqlm_track_point)
+TRACK_POINT_DTYPE = np.dtype([("id", "<i4"), ("proj_x", "<f4"), ("proj_y", "<f4"), ("proj_xr", "<f4"),
+                              ("view_cos", "<f4"), ("level", "<i4"), ("in_view", "u1"), ("bad", "u1"),
+                              ("has_obs", "u1"), ("pad", "u1")])
+# one LastFrame keypoint slot (sqlm_last_point)
+LAST_POINT_DTYPE = np.dtype([("id", "<i4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("octave", "<i4"),
+                             ("angle", "<f4"), ("outlier", "u1"), ("has_obs", "u1"), ("pad", "u1", (2,))])
+
+
 class OrbParams(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
@@ -26,6 +35,65 @@ class OrbParams(C.Structure):
 
 class FrameBounds(C.Structure):
     _fields_ = [("min_x", C.c_float), ("max_x", C.c_float), ("min_y", C.c_float), ("max_y", C.c_float)]
+
+
+class _OrbFrame(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("uright", C.c_void_p), ("n", C.c_int32),
+                ("bounds", FrameBounds), ("scale_factors", C.c_void_p), ("n_levels", C.c_int32),
+                ("fx", C.c_float), ("fy", C.c_float), ("cx", C.c_float), ("cy", C.c_float), ("bf", C.c_float),
+                ("mb", C.c_float), ("slot_mp", C.c_void_p), ("slot_obs", C.c_void_p)]
+
+
+class Frame:
+    """The Frame fields ORBmatcher's projection searches read and write
+    (include/data_structure/Frame.h): mvKeysUn, mDescriptors, mvuRight (None:
+    monocular), the grid bounds (mnMinX, mnMaxX, mnMinY, mnMaxY),
+    mvScaleFactors, fx fy cx cy, mbf, mb, mTcw, and the keypoint slots
+    mvpMapPoints as map-point ids (-1 = NULL) with slot_obs = that point's
+    Observations() > 0; the searches update the last two in place."""
+
+    def __init__(self, mvKeysUn, mDescriptors, bounds, mvScaleFactors, fx, fy, cx, cy, mbf=0.0, mb=0.0,
+                 mvuRight=None, mTcw=None, mvpMapPoints=None, slot_obs=None):
+        self.mvKeysUn = np.ascontiguousarray(mvKeysUn, KP_DTYPE)
+        n = len(self.mvKeysUn)
+        self.N = n
+        self.mDescriptors = np.ascontiguousarray(mDescriptors, np.uint8).reshape(n, 32)
+        self.bounds = tuple(float(v) for v in bounds)
+        self.mvScaleFactors = np.ascontiguousarray(mvScaleFactors, np.float32)
+        self.fx, self.fy, self.cx, self.cy, self.mbf, self.mb = (float(v) for v in (fx, fy, cx, cy, mbf, mb))
+        self.mvuRight = None if mvuRight is None else np.ascontiguousarray(mvuRight, np.float32)
+        if self.mvuRight is not None and self.mvuRight.shape != (n,):
+            raise ValueError("mvuRight must hold one entry per keypoint")
+        self.mTcw = None if mTcw is None else np.ascontiguousarray(np.asarray(mTcw, np.float32)[:3, :4])
+        self.mvpMapPoints = np.full(n, -1, np.int32) if mvpMapPoints is None else np.ascontiguousarray(
+            mvpMapPoints, np.int32)
+        self.slot_obs = (self.mvpMapPoints >= 0).astype(np.uint8) if slot_obs is None else np.ascontiguousarray(
+            slot_obs, np.uint8)
+        if self.mvpMapPoints.shape != (n,) or self.slot_obs.shape != (n,):
+            raise ValueError("mvpMapPoints / slot_obs must hold one entry per keypoint")
+
+    def _struct(self) -> _OrbFrame:
+        f = _OrbFrame()
+        f.kps, f.desc = self.mvKeysUn.ctypes.data, self.mDescriptors.ctypes.data
+        f.uright = None if self.mvuRight is None else self.mvuRight.ctypes.data
+        f.n = self.N
+        f.bounds = FrameBounds(*self.bounds)
+        f.scale_factors, f.n_levels = self.mvScaleFactors.ctypes.data, len(self.mvScaleFactors)
+        f.fx, f.fy, f.cx, f.cy, f.bf, f.mb = self.fx, self.fy, self.cx, self.cy, self.mbf, self.mb
+        f.slot_mp, f.slot_obs = self.mvpMapPoints.ctypes.data, self.slot_obs.ctypes.data
+        return f
+
+
+class LastFrameSlots:
+    """LastFrame as SearchByProjection(CurrentFrame, LastFrame, ...) reads it:
+    mTcw and, per keypoint slot, LAST_POINT_DTYPE (mvpMapPoints id, world
+    position, mvKeys octave, mvKeysUn angle, mvbOutlier, Observations() > 0)
+    with the points' descriptors [N, 32]."""
+
+    def __init__(self, mTcw, slots, descriptors):
+        self.mTcw = np.ascontiguousarray(np.asarray(mTcw, np.float32)[:3, :4])
+        self.slots = np.ascontiguousarray(slots, LAST_POINT_DTYPE)
+        self.descriptors = np.ascontiguousarray(descriptors, np.uint8).reshape(len(self.slots), 32)
 
 
 class ORBextractor:
@@ -152,3 +220,37 @@ class ORBmatcher:
                                              C.c_float(self.mfNNratio), int(self.mbCheckOrientation), C.byref(n)),
               "sqlm_orb_search_for_init")
         return n.value, m12
+
+    def SearchByProjection(self, F: Frame, second, *args):
+        """The projection searches on the GPU candidate windows:
+
+        - ``SearchByProjection(F, vpMapPoints, descriptors, th=1.0)``
+          (ORBmatcher.cc:67-181): vpMapPoints TRACK_POINT_DTYPE [n] as
+          Tracking::SearchLocalPoints leaves them, descriptors [n, 32];
+        - ``SearchByProjection(CurrentFrame, LastFrame, th, bMono)``
+          (ORBmatcher.cc:1717-1883): LastFrame a LastFrameSlots, CurrentFrame.mTcw set.
+
+        F.mvpMapPoints / F.slot_obs are updated in place; returns nmatches."""
+        n = C.c_int(0)
+        fs = F._struct()
+        if isinstance(second, LastFrameSlots):
+            if len(args) != 2:
+                raise TypeError("SearchByProjection(CurrentFrame, LastFrame, th, bMono)")
+            th, bMono = args
+            if F.mTcw is None:
+                raise ValueError("CurrentFrame.mTcw is not set")
+            L = second
+            check(lib().sqlm_orb_search_by_projection_last(
+                self.ctx._h, C.byref(fs), ptr(F.mTcw), ptr(L.mTcw), ptr(L.slots), ptr(L.descriptors), len(L.slots),
+                C.c_float(th), int(bool(bMono)), int(self.mbCheckOrientation), C.byref(n)),
+                "sqlm_orb_search_by_projection_last")
+            return n.value
+        if len(args) not in (1, 2):
+            raise TypeError("SearchByProjection(F, vpMapPoints, descriptors, th=1.0)")
+        third, th = args[0], (args[1] if len(args) == 2 else 1.0)
+        mps = np.ascontiguousarray(second, TRACK_POINT_DTYPE)
+        desc = np.ascontiguousarray(third, np.uint8).reshape(len(mps), 32)
+        check(lib().sqlm_orb_search_by_projection_local(self.ctx._h, C.byref(fs), ptr(mps), ptr(desc), len(mps),
+                                                        C.c_float(th), C.c_float(self.mfNNratio), C.byref(n)),
+              "sqlm_orb_search_by_projection_local")
+        return n.value

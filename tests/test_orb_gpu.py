@@ -115,3 +115,87 @@ def test_search_for_initialization(gpu_ctx, extractor, orb_oracle, seed, shift, 
     np.testing.assert_array_equal(pg, pr)
     ok = mg >= 0
     assert np.median(k2["x"][mg[ok]] - k1["x"][ok]) == shift[0]
+
+
+# ---- projection searches (ORBmatcher.cc:67, :1717) vs the oracle, bit-exact slots ----
+@pytest.fixture(scope="module")
+def kitti_pair(extractor):
+    a, b = synth.make_image_pair(1241, 376, seed=17, shift=(9.0, 2.0))
+    k1, d1 = extractor(a)
+    k2, d2 = extractor(b)
+    return k1, d1, k2, d2, (0.0, 1241.0, 0.0, 376.0)
+
+
+def _gpu_frame(k2, d2, bounds, ur, sm, so, Tcw=None, w=1241, h=376):
+    import orb_scene as S
+    from sqrtlm.orb import Frame
+    fx, fy, cx, cy, bf, mb = S.camera(w, h)
+    return Frame(k2, d2, bounds, S.scale_factors(), fx, fy, cx, cy, bf, mb, mvuRight=ur, mTcw=Tcw,
+                 mvpMapPoints=sm.copy(), slot_obs=so.copy())
+
+
+@pytest.mark.parametrize("stereo,th,nnratio", [(False, 1.0, 0.8), (True, 1.0, 0.8), (True, 5.0, 0.9),
+                                               (False, 10.0, 0.6)])
+def test_search_by_projection_local(gpu_ctx, orb_oracle, kitti_pair, stereo, th, nnratio):
+    import orb_scene as S
+    from sqrtlm.orb import ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    mps, md = S.local_points(k1, d1, (9.0, 2.0), seed=3, stereo=stereo)
+    ur, sm, so = S.current_slots(k2, 3, stereo)
+    n_r, m_r, o_r = orb_oracle.search_by_projection_local(k2, d2, bounds, S.scale_factors(), ur, sm, so, mps, md, th,
+                                                          nnratio)
+    F = _gpu_frame(k2, d2, bounds, ur, sm, so)
+    n_g = ORBmatcher(nnratio, ctx=gpu_ctx).SearchByProjection(F, mps, md, th)
+    assert n_g == n_r and n_r > 100
+    np.testing.assert_array_equal(F.mvpMapPoints, m_r)
+    np.testing.assert_array_equal(F.slot_obs, o_r)
+
+
+@pytest.mark.parametrize("stereo,mono,tz,th,check_ori", [(False, True, 0.0, 7.0, True), (True, False, 1.0, 7.0, True),
+                                                         (True, False, -1.0, 15.0, True),
+                                                         (True, False, 0.0, 15.0, False)])
+def test_search_by_projection_last(gpu_ctx, orb_oracle, kitti_pair, stereo, mono, tz, th, check_ori):
+    import orb_scene as S
+    from sqrtlm.orb import LastFrameSlots, ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    Tcw, Tlw, lp, ld = S.last_frame(k1, d1, (9.0, 2.0), 1241, 376, seed=4, tz=tz)
+    ur, sm, so = S.current_slots(k2, 4, stereo)
+    n_r, m_r, o_r = orb_oracle.search_by_projection_last(k2, d2, bounds, S.scale_factors(), S.camera(1241, 376), ur,
+                                                         sm, so, Tcw, Tlw, lp, ld, th, mono, check_ori)
+    F = _gpu_frame(k2, d2, bounds, ur, sm, so, Tcw=Tcw)
+    n_g = ORBmatcher(0.9, check_ori, ctx=gpu_ctx).SearchByProjection(F, LastFrameSlots(Tlw, lp, ld), th, mono)
+    assert n_g == n_r and n_r > 100
+    np.testing.assert_array_equal(F.mvpMapPoints, m_r)
+    np.testing.assert_array_equal(F.slot_obs, o_r)
+
+
+def test_search_by_projection_edge_cases(gpu_ctx, orb_oracle, kitti_pair):
+    import orb_scene as S
+    from sqrtlm._lib import SqlmError
+    from sqrtlm.orb import LastFrameSlots, ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    m = ORBmatcher(0.8, ctx=gpu_ctx)
+    ur, sm, so = S.current_slots(k2, 1, False)
+    F = _gpu_frame(k2, d2, bounds, ur, sm, so, Tcw=np.eye(4)[:3])
+    mps, md = S.local_points(k1, d1, (9.0, 2.0), seed=1, stereo=False)
+    assert m.SearchByProjection(F, mps[:0], md[:0]) == 0  # no map points
+    off = mps.copy()
+    off["in_view"] = 0
+    assert m.SearchByProjection(F, off, md) == 0  # nothing to project
+    np.testing.assert_array_equal(F.mvpMapPoints, sm)
+    far = mps.copy()
+    far["proj_x"] += 5000.0  # every window outside the grid
+    assert m.SearchByProjection(F, far, md) == 0
+    bad = mps[:4].copy()
+    bad["level"] = 8  # mnTrackScaleLevel beyond mvScaleFactors
+    with pytest.raises(SqlmError):
+        m.SearchByProjection(F, bad, md[:4])
+    E = _gpu_frame(k2[:0], d2[:0], bounds, None, sm[:0], so[:0], Tcw=np.eye(4)[:3])  # frame without keypoints
+    assert m.SearchByProjection(E, mps, md) == 0
+    Tcw, Tlw, lp, ld = S.last_frame(k1, d1, (9.0, 2.0), 1241, 376, seed=2)
+    assert m.SearchByProjection(E, LastFrameSlots(Tlw, lp, ld), 7.0, True) == 0
+    n_r, m_r, _ = orb_oracle.search_by_projection_last(k2, d2, bounds, S.scale_factors(), S.camera(1241, 376), None,
+                                                       sm, so, np.eye(4)[:3], Tlw, lp, ld, 7.0, True)
+    F2 = _gpu_frame(k2, d2, bounds, None, sm, so, Tcw=np.eye(4)[:3])  # identity motion: the old positions
+    assert m.SearchByProjection(F2, LastFrameSlots(Tlw, lp, ld), 7.0, True) == n_r
+    np.testing.assert_array_equal(F2.mvpMapPoints, m_r)

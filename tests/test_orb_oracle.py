@@ -314,3 +314,220 @@ def test_golden_extract_and_match(OB):
     n, m12, _ = OB.search_for_init(k1, d1, k2, d2, (0.0, 640.0, 0.0, 300.0), prev, 100, 0.9, True)
     assert n == int(g["n_matches"])
     np.testing.assert_array_equal(m12, g["m12"])
+
+
+# ---- projection searches: the C oracle vs a second, pure-Python transliteration ----
+def _py_grid(kps, bounds):
+    import math
+    f32 = np.float32
+    minx, maxx, miny, maxy = (f32(v) for v in bounds)
+    wi, hi = f32(64) / (maxx - minx), f32(48) / (maxy - miny)
+    cells = [[[] for _ in range(48)] for _ in range(64)]
+    for i in range(len(kps)):
+        px = math.floor(float((f32(kps["x"][i]) - minx) * wi) + 0.5)
+        py = math.floor(float((f32(kps["y"][i]) - miny) * hi) + 0.5)
+        if 0 <= px < 64 and 0 <= py < 48:
+            cells[px][py].append(i)
+    return cells, minx, miny, wi, hi
+
+
+def _py_area(G, kps, x, y, r, minL, maxL):
+    """Frame::GetFeaturesInArea (Frame.cc:1463-1552)."""
+    import math
+    cells, minx, miny, wi, hi = G
+    x, y, r = np.float32(x), np.float32(y), np.float32(r)
+    x0 = max(0, math.floor((x - minx - r) * wi))
+    if x0 >= 64:
+        return []
+    x1 = min(63, math.ceil((x - minx + r) * wi))
+    if x1 < 0:
+        return []
+    y0 = max(0, math.floor((y - miny - r) * hi))
+    if y0 >= 48:
+        return []
+    y1 = min(47, math.ceil((y - miny + r) * hi))
+    if y1 < 0:
+        return []
+    check = minL > 0 or maxL >= 0
+    out = []
+    for ix in range(x0, x1 + 1):
+        for iy in range(y0, y1 + 1):
+            for j in cells[ix][iy]:
+                o = kps["octave"][j]
+                if check and (o < minL or (maxL >= 0 and o > maxL)):
+                    continue
+                if abs(kps["x"][j] - x) < r and abs(kps["y"][j] - y) < r:
+                    out.append(j)
+    return out
+
+
+def _py_sbp_local(kps, desc, bounds, scale, uright, slot_mp, slot_obs, mps, mp_desc, th, nnratio):
+    """ORBmatcher::SearchByProjection(F, vpMapPoints, th) (ORBmatcher.cc:67-181)."""
+    f32 = np.float32
+    G = _py_grid(kps, bounds)
+    sm, so = slot_mp.copy(), slot_obs.copy()
+    D = np.unpackbits(mp_desc[:, None, :] ^ desc[None, :, :], axis=2).sum(axis=2)
+    n = 0
+    for i, p in enumerate(mps):
+        if not p["in_view"] or p["bad"]:
+            continue
+        lvl = int(p["level"])
+        r = f32(2.5) if float(p["view_cos"]) > 0.998 else f32(4.0)
+        if f32(th) != 1.0:
+            r = r * f32(th)
+        rw = r * scale[lvl]
+        cand = _py_area(G, kps, p["proj_x"], p["proj_y"], rw, lvl - 1, lvl)
+        if not cand:
+            continue
+        b1, l1, b2, l2, bi = 256, -1, 256, -1, -1
+        for j in cand:
+            if sm[j] >= 0 and so[j]:
+                continue
+            if uright is not None and uright[j] > 0 and abs(p["proj_xr"] - uright[j]) > rw:
+                continue
+            d = int(D[i, j])
+            if d < b1:
+                b2, l2, b1, l1, bi = b1, l1, d, int(kps["octave"][j]), j
+            elif d < b2:
+                l2, b2 = int(kps["octave"][j]), d
+        if b1 <= 100:
+            if l1 == l2 and f32(b1) > f32(nnratio) * f32(b2):
+                continue
+            sm[bi], so[bi] = p["id"], p["has_obs"]
+            n += 1
+    return n, sm, so
+
+
+def _py_sbp_last(kps, desc, bounds, scale, cam, uright, slot_mp, slot_obs, Tcw, Tlw, lp, ldesc, th, mono, check_ori):
+    """ORBmatcher::SearchByProjection(CurrentFrame, LastFrame, th, bMono) (ORBmatcher.cc:1717-1883)."""
+    import math
+    f32 = np.float32
+    fx, fy, cx, cy, bf, mb = (f32(v) for v in cam)
+    G = _py_grid(kps, bounds)
+    sm, so = slot_mp.copy(), slot_obs.copy()
+    D = np.unpackbits(ldesc[:, None, :] ^ desc[None, :, :], axis=2).sum(axis=2)
+
+    def mul_add(A, x, c, sign):
+        out = []
+        for i in range(3):
+            t0 = f32(A[i][0]) * f32(x[0]) + f32(A[i][1]) * f32(x[1]) + f32(A[i][2]) * f32(x[2])
+            out.append(f32(float(t0) * sign + (float(c[i]) if c is not None else 0.0)))
+        return out
+    Tcw, Tlw = np.asarray(Tcw, f32), np.asarray(Tlw, f32)
+    tcw, tlw = Tcw[:, 3], Tlw[:, 3]
+    twc = mul_add(Tcw[:, :3].T, tcw, None, -1.0)
+    tlc = mul_add(Tlw[:, :3], twc, tlw, 1.0)
+    fwd = tlc[2] > mb and not mono
+    bwd = -tlc[2] > mb and not mono
+    n = 0
+    hist = [[] for _ in range(30)]
+    for i, p in enumerate(lp):
+        if p["id"] < 0 or p["outlier"]:
+            continue
+        xc, yc, zc = mul_add(Tcw[:, :3], (p["x"], p["y"], p["z"]), tcw, 1.0)
+        invz = f32(1.0 / float(zc))
+        if invz < 0:
+            continue
+        u = fx * xc * invz + cx
+        v = fy * yc * invz + cy
+        if u < f32(bounds[0]) or u > f32(bounds[1]) or v < f32(bounds[2]) or v > f32(bounds[3]):
+            continue
+        o = int(p["octave"])
+        rad = f32(th) * scale[o]
+        lv = (o, -1) if fwd else (0, o) if bwd else (o - 1, o + 1)
+        cand = _py_area(G, kps, u, v, rad, *lv)
+        if not cand:
+            continue
+        b1, bi = 256, -1
+        for j in cand:
+            if sm[j] >= 0 and so[j]:
+                continue
+            if uright is not None and uright[j] > 0:
+                ur = u - bf * invz
+                if abs(ur - uright[j]) > rad:
+                    continue
+            d = int(D[i, j])
+            if d < b1:
+                b1, bi = d, j
+        if b1 <= 100:
+            sm[bi], so[bi] = p["id"], p["has_obs"]
+            n += 1
+            if check_ori:
+                rot = f32(p["angle"]) - f32(kps["angle"][bi])
+                if rot < 0:
+                    rot = f32(rot + f32(360))
+                b = int(math.floor(float(rot * (f32(30) / f32(360))) + 0.5))
+                hist[0 if b == 30 else b].append(bi)
+    if check_ori:
+        sizes = [len(h) for h in hist]
+        m1 = m2 = m3 = 0
+        i1 = i2 = i3 = -1
+        for i, s in enumerate(sizes):
+            if s > m1:
+                m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, i
+            elif s > m2:
+                m3, m2, i3, i2 = m2, s, i2, i
+            elif s > m3:
+                m3, i3 = s, i
+        if f32(m2) < f32(0.1) * f32(m1):
+            i2 = i3 = -1
+        elif f32(m3) < f32(0.1) * f32(m1):
+            i3 = -1
+        for b in range(30):
+            if b in (i1, i2, i3):
+                continue
+            for j in hist[b]:
+                sm[j], so[j] = -1, 0
+                n -= 1
+    return n, sm, so
+
+
+@pytest.fixture(scope="module")
+def proj_scene(OB):
+    import orb_scene as S
+    a, b = synth.make_image_pair(640, 300, seed=21, shift=(6.0, -2.0))
+    p = OB.params(800)
+    k1, d1 = OB.extract(p, a)
+    k2, d2 = OB.extract(p, b)
+    return S, k1, d1, k2, d2, (0.0, 640.0, 0.0, 300.0)
+
+
+def test_features_in_area_matches_transliteration(OB, proj_scene):
+    S, k1, d1, k2, d2, bounds = proj_scene
+    G = _py_grid(k2, bounds)
+    rng = np.random.default_rng(3)
+    for _ in range(60):
+        x, y = rng.uniform(-20, 660), rng.uniform(-20, 320)
+        r = float(rng.choice([2.5, 4.0, 7.2, 30.0]))
+        lv = [(-1, -1), (0, -1), (2, -1), (-1, 0), (0, 3), (1, 1), (3, 5)][rng.integers(7)]
+        got = OB.features_in_area(k2, bounds, x, y, r, *lv)
+        assert list(got) == _py_area(G, k2, x, y, r, *lv)
+    assert len(OB.features_in_area(k2, bounds, 320, 150, 40)) > 0
+
+
+@pytest.mark.parametrize("stereo,th", [(False, 1.0), (True, 1.0), (True, 3.0)])
+def test_search_by_projection_local_matches_transliteration(OB, proj_scene, stereo, th):
+    S, k1, d1, k2, d2, bounds = proj_scene
+    mps, md = S.local_points(k1, d1, (6.0, -2.0), seed=5, stereo=stereo)
+    ur, sm, so = S.current_slots(k2, 5, stereo)
+    sf = S.scale_factors()
+    n, m, o = OB.search_by_projection_local(k2, d2, bounds, sf, ur, sm, so, mps, md, th, 0.8)
+    n_py, m_py, o_py = _py_sbp_local(k2, d2, bounds, sf, ur, sm, so, mps, md, th, 0.8)
+    assert n == n_py and n > 30
+    np.testing.assert_array_equal(m, m_py)
+    np.testing.assert_array_equal(o, o_py)
+
+
+@pytest.mark.parametrize("stereo,mono,tz,th,check_ori", [(False, True, 0.0, 7.0, True), (True, False, 1.0, 7.0, True),
+                                                         (True, False, -1.0, 15.0, False),
+                                                         (True, False, 0.0, 7.0, True)])
+def test_search_by_projection_last_matches_transliteration(OB, proj_scene, stereo, mono, tz, th, check_ori):
+    S, k1, d1, k2, d2, bounds = proj_scene
+    Tcw, Tlw, lp, ld = S.last_frame(k1, d1, (6.0, -2.0), 640, 300, seed=9, tz=tz)
+    ur, sm, so = S.current_slots(k2, 9, stereo)
+    sf, cam = S.scale_factors(), S.camera(640, 300)
+    n, m, o = OB.search_by_projection_last(k2, d2, bounds, sf, cam, ur, sm, so, Tcw, Tlw, lp, ld, th, mono, check_ori)
+    n_py, m_py, o_py = _py_sbp_last(k2, d2, bounds, sf, cam, ur, sm, so, Tcw, Tlw, lp, ld, th, mono, check_ori)
+    assert n == n_py and n > 20
+    np.testing.assert_array_equal(m, m_py)
+    np.testing.assert_array_equal(o, o_py)
