@@ -133,6 +133,76 @@ int sqlm_orb_search_by_projection_last(sqlm_ctx *ctx, sqlm_orb_frame *F, const f
                                        const sqlm_last_point *lp, const uint8_t *ldesc, int n_last, float th,
                                        int mono, int check_ori, int *n_matches);
 
+/* A map point as the keyframe searches read it (MapPoint.h): mnId,
+ * GetWorldPos(), GetNormal(), mfMinDistance / mfMaxDistance (the searches
+ * apply the 0.8 / 1.2 invariance factors themselves) and the caller's
+ * pre-filter `skip` (isBad(), or the point is already found / already in the
+ * keyframe — each search's own first test). */
+typedef struct sqlm_map_point {
+  int32_t id;
+  float x, y, z, nx, ny, nz, min_dist, max_dist;
+  uint8_t skip, pad[3];
+} sqlm_map_point;
+
+/* ORBmatcher::SearchByProjection(pKF, Scw, vpPoints, vpMatched, th)
+ * (ORBmatcher.cc:423-571): F = pKF with F->slot_mp = vpMatched (ids, updated);
+ * Scw = 3x4 rows of the Sim3 [sR | t]. */
+int sqlm_orb_search_by_projection_sim3(sqlm_ctx *ctx, sqlm_orb_frame *F, const float *Scw, const sqlm_map_point *mps,
+                                       const uint8_t *mp_desc, int n, int th, int *n_matches);
+
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th) (:1109-1294; sim3 = 0, T = pKF's
+ * 3x4 Tcw) and Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:1296-1446;
+ * sim3 = 1, T = Scw): fuse_idx [n] = the keypoint of pKF each point fuses
+ * into (-1: none). The map edit that follows (MapPoint::Replace /
+ * AddObservation / vpReplacePoint) is the caller's, in point order; it
+ * does not feed back into the searches of later points. *n_fused = nFused. */
+int sqlm_orb_fuse(sqlm_ctx *ctx, const sqlm_orb_frame *F, const float *T, int sim3, const sqlm_map_point *mps,
+                  const uint8_t *mp_desc, int n, float th, int32_t *fuse_idx, int *n_fused);
+
+/* ORBmatcher::SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th,
+ * ORBdist) (:1902-2046): F = CurrentFrame (slot_mp updated), Tcw its 3x4
+ * pose; mps / mp_desc / kf_angle = pKF's map-point slots
+ * (GetMapPointMatches; NULL, bad or already-found slots have skip set) and
+ * pKF->mvKeysUn[i].angle. */
+int sqlm_orb_search_by_projection_kf(sqlm_ctx *ctx, sqlm_orb_frame *F, const float *Tcw, const sqlm_map_point *mps,
+                                     const uint8_t *mp_desc, const float *kf_angle, int n, float th, int orb_dist,
+                                     int check_ori, int *n_matches);
+
+/* A keyframe (or Frame) as the BoW searches read it: mvKeysUn, mDescriptors
+ * [n][32], the DBoW2 FeatureVector as the node id of each feature (-1: the
+ * feature is not in mFeatVec), GetMapPointMatches() ids (-1: NULL), their
+ * isBad() (NULL: none bad) and mvuRight (NULL: monocular). */
+typedef struct sqlm_bow_frame {
+  const sqlm_keypoint *kps;
+  const uint8_t *desc;
+  const int32_t *node;
+  const int32_t *mp;
+  const uint8_t *mp_bad;
+  const float *uright;
+  int32_t n;
+} sqlm_bow_frame;
+
+/* ORBmatcher(nnratio, check_ori).SearchByBoW(pKF, F, vpMapPointMatches)
+ * (:246-403): matches [F->n] = map-point ids (-1: NULL). */
+int sqlm_orb_search_by_bow_kf_frame(sqlm_ctx *ctx, const sqlm_bow_frame *KF, const sqlm_bow_frame *F, float nnratio,
+                                    int check_ori, int32_t *matches, int *n_matches);
+
+/* SearchByBoW(pKF1, pKF2, vpMatches12) (:731-869): matches12 [K1->n] = ids
+ * of pKF2's map points (-1: NULL). */
+int sqlm_orb_search_by_bow_kf_kf(sqlm_ctx *ctx, const sqlm_bow_frame *K1, const sqlm_bow_frame *K2, float nnratio,
+                                 int check_ori, int32_t *matches12, int *n_matches);
+
+/* SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+ * (:887-1096): m12 [K1->n] = the matched pKF2 keypoint (-1: none; the
+ * reference's vMatchedPairs are the (i, m12[i]) with m12[i] >= 0, in i
+ * order). C1 = pKF1->GetCameraCenter(), T2w = pKF2's 3x4 pose, cam2 = pKF2's
+ * fx fy cx cy, scale_factors2 = pKF2->mvScaleFactors (mvLevelSigma2 = its
+ * squares), F12 row-major 3x3. */
+int sqlm_orb_search_for_triangulation(sqlm_ctx *ctx, const sqlm_bow_frame *K1, const sqlm_bow_frame *K2,
+                                      const float *C1, const float *T2w, const float *cam2,
+                                      const float *scale_factors2, int n_levels2, const float *F12, int only_stereo,
+                                      int check_ori, int32_t *m12, int *n_matches);
+
 /* Bench helper: time `reps` extractions of one image (input uploaded once;
  * timed region = the whole device pipeline incl. the host quadtree step).
  * ms_per_frame, and per-stage device milliseconds [6]: pyramid, fast,

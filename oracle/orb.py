@@ -212,3 +212,95 @@ def search_by_projection_last(kps, desc, bounds, scale, cam, uright, slot_mp, sl
     n = lib().orc_search_by_projection_last(C.byref(f), _p(Tcw), _p(Tlw), _p(lp), _p(ldesc), len(lp),
                                             C.c_float(th), int(bool(mono)), int(bool(check_ori)))
     return n, sm, so
+
+
+MAP_POINT_DTYPE = np.dtype([("id", "<i4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"),
+                            ("nz", "<f4"), ("min_dist", "<f4"), ("max_dist", "<f4"), ("skip", "u1"),
+                            ("pad", "u1", (3,))])
+
+
+def search_by_projection_sim3(kps, desc, bounds, scale, cam, slot_mp, Scw, mps, mp_desc, th):
+    """SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) -> (n, vpMatched)."""
+    n = len(kps)
+    f, keep, sm, _ = _frame(kps, desc, bounds, scale, cam, None, slot_mp, np.zeros(n))
+    S = np.ascontiguousarray(np.asarray(Scw, np.float32)[:3, :4])
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    r = lib().orc_search_by_projection_sim3(C.byref(f), _p(S), _p(mps), _p(np.ascontiguousarray(mp_desc, np.uint8)),
+                                            len(mps), int(th))
+    return r, sm
+
+
+def fuse(kps, desc, bounds, scale, cam, uright, T, sim3, mps, mp_desc, th):
+    """Fuse(pKF, vpMapPoints, th) (sim3 False, T = Tcw) / Fuse(pKF, Scw, ...) -> (nFused, fuse_idx)."""
+    n = len(kps)
+    f, keep, _, _ = _frame(kps, desc, bounds, scale, cam, uright, np.full(n, -1), np.zeros(n))
+    T = np.ascontiguousarray(np.asarray(T, np.float32)[:3, :4])
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    out = np.zeros(max(len(mps), 1), np.int32)
+    r = lib().orc_fuse(C.byref(f), _p(T), int(bool(sim3)), _p(mps), _p(np.ascontiguousarray(mp_desc, np.uint8)),
+                       len(mps), C.c_float(th), _p(out))
+    return r, out[:len(mps)]
+
+
+def search_by_projection_kf(kps, desc, bounds, scale, cam, slot_mp, Tcw, mps, mp_desc, kf_angle, th, orb_dist,
+                            check_ori=True):
+    """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) -> (n, mvpMapPoints)."""
+    n = len(kps)
+    f, keep, sm, _ = _frame(kps, desc, bounds, scale, cam, None, slot_mp, np.zeros(n))
+    T = np.ascontiguousarray(np.asarray(Tcw, np.float32)[:3, :4])
+    mps = np.ascontiguousarray(mps, MAP_POINT_DTYPE)
+    ang = np.ascontiguousarray(kf_angle, np.float32)
+    r = lib().orc_search_by_projection_kf(C.byref(f), _p(T), _p(mps), _p(np.ascontiguousarray(mp_desc, np.uint8)),
+                                          _p(ang), len(mps), C.c_float(th), int(orb_dist), int(bool(check_ori)))
+    return r, sm
+
+
+class _BowFrame(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("node", C.c_void_p), ("mp", C.c_void_p),
+                ("mp_bad", C.c_void_p), ("uright", C.c_void_p), ("n", C.c_int)]
+
+
+def _bow(kps, desc, node, mp, mp_bad=None, uright=None):
+    arrs = [np.ascontiguousarray(kps, KP_DTYPE), np.ascontiguousarray(desc, np.uint8),
+            np.ascontiguousarray(node, np.int32), np.ascontiguousarray(mp, np.int32),
+            None if mp_bad is None else np.ascontiguousarray(mp_bad, np.uint8),
+            None if uright is None else np.ascontiguousarray(uright, np.float32)]
+    b = _BowFrame()
+    b.kps, b.desc, b.node, b.mp = (a.ctypes.data for a in arrs[:4])
+    b.mp_bad = None if arrs[4] is None else arrs[4].ctypes.data
+    b.uright = None if arrs[5] is None else arrs[5].ctypes.data
+    b.n = len(arrs[0])
+    return b, arrs
+
+
+def search_by_bow_kf_frame(kf, f, nnratio=0.7, check_ori=True):
+    """SearchByBoW(pKF, F, vpMapPointMatches); kf / f = (kps, desc, node, mp[, mp_bad[, uright]])."""
+    a, ka = _bow(*kf)
+    b, kb = _bow(*f)
+    out = np.zeros(max(b.n, 1), np.int32)
+    r = lib().orc_search_by_bow_kf_frame(C.byref(a), C.byref(b), C.c_float(nnratio), int(bool(check_ori)), _p(out))
+    return r, out[:b.n]
+
+
+def search_by_bow_kf_kf(k1, k2, nnratio=0.75, check_ori=True):
+    """SearchByBoW(pKF1, pKF2, vpMatches12)."""
+    a, ka = _bow(*k1)
+    b, kb = _bow(*k2)
+    out = np.zeros(max(a.n, 1), np.int32)
+    r = lib().orc_search_by_bow_kf_kf(C.byref(a), C.byref(b), C.c_float(nnratio), int(bool(check_ori)), _p(out))
+    return r, out[:a.n]
+
+
+def search_for_triangulation(k1, k2, C1, T2w, cam2, scale2, F12, only_stereo, check_ori=False):
+    """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo) -> (n, m12)."""
+    a, ka = _bow(*k1)
+    b, kb = _bow(*k2)
+    C1 = np.ascontiguousarray(C1, np.float32)
+    T = np.ascontiguousarray(np.asarray(T2w, np.float32)[:3, :4])
+    cam2 = np.ascontiguousarray(cam2, np.float32)
+    s2 = np.ascontiguousarray(scale2, np.float32)
+    F = np.ascontiguousarray(F12, np.float32)
+    out = np.zeros(max(a.n, 1), np.int32)
+    r = lib().orc_search_for_triangulation(C.byref(a), C.byref(b), _p(C1), _p(T), _p(cam2), _p(s2), _p(F),
+                                           int(bool(only_stereo)), int(bool(check_ori)), _p(out))
+    return r, out[:a.n]

@@ -1133,3 +1133,529 @@ int orc_search_by_projection_last(orc_frame *F, const float *Tcw, const float *T
   grid_free(&G);
   return nmatches;
 }
+
+/* ---- keyframe projection searches ---- */
+typedef struct {
+  float T[12];  /* [R | t], rows */
+  float Ow[3];  /* -R^T t */
+} orc_pose;
+
+static void pose_finish(orc_pose *P) {
+  const float t[3] = {P->T[3], P->T[7], P->T[11]};
+  mat3_mul_add(P->T, 1, t, NULL, -1.0f, P->Ow);
+}
+
+/* pKF->GetRotation() / GetTranslation() / GetCameraCenter() of a 3x4 Tcw. */
+static void pose_from_T(const float *T, orc_pose *P) {
+  memcpy(P->T, T, sizeof(float) * 12);
+  pose_finish(P);
+}
+
+/* Scw -> s = sqrt(row0 . row0) (Mat::dot in double), R = sR / s, t = t / s
+ * (Mat / double: a float scale by (float)(1 / s)) — ORBmatcher.cc:434-441;
+ * OpenCV's convertTo scaling, "parity unpinned" with the other cv::Mat steps. */
+static void pose_from_sim3(const float *S, orc_pose *P) {
+  const double d = (double)S[0] * S[0] + (double)S[1] * S[1] + (double)S[2] * S[2];
+  const float scw = (float)sqrt(d);
+  const float inv = (float)(1.0 / (double)scw);
+  for (int i = 0; i < 12; ++i) P->T[i] = S[i] * inv;
+  pose_finish(P);
+}
+
+/* cv::norm of a 3x1 CV_32F (double sum of squares, sqrt) and Mat::dot (double). */
+static float norm3(const float *v) {
+  double s = 0;
+  for (int i = 0; i < 3; ++i) s += (double)v[i] * v[i];
+  return (float)sqrt(s);
+}
+static double dot3(const float *a, const float *b) {
+  double s = 0;
+  for (int i = 0; i < 3; ++i) s += (double)a[i] * b[i];
+  return s;
+}
+
+/* MapPoint::PredictScale (MapPoint.cc:610-650). */
+static int predict_scale(float max_dist, float dist, float log_scale, int n_levels) {
+  const float ratio = max_dist / dist;
+  int nScale = (int)ceilf(logf(ratio) / log_scale);
+  if (nScale < 0)
+    nScale = 0;
+  else if (nScale >= n_levels)
+    nScale = n_levels - 1;
+  return nScale;
+}
+
+/* The keyframe-side projection of ORBmatcher.cc:447-489 / :1132-1180 /
+ * :1327-1372: camera point, z >= 0, (u, v) = (fx x/z + cx, ...) inside
+ * IsInImage, distance invariance band, viewing angle within 60 degrees,
+ * predicted level. Returns 0 when the point is rejected. */
+static int project_kf(const orc_frame *F, const orc_pose *P, const orc_map_point *p, float *u, float *v, float *invz,
+                      int *level) {
+  const float X[3] = {p->x, p->y, p->z}, t[3] = {P->T[3], P->T[7], P->T[11]};
+  float Xc[3];
+  mat3_mul_add(P->T, 0, X, t, 1.0f, Xc);
+  if (Xc[2] < 0.0f) return 0;
+  *invz = 1 / Xc[2];
+  const float x = Xc[0] * *invz, y = Xc[1] * *invz;
+  *u = F->fx * x + F->cx;
+  *v = F->fy * y + F->cy;
+  if (!(*u >= F->bounds.min_x && *u < F->bounds.max_x && *v >= F->bounds.min_y && *v < F->bounds.max_y)) return 0;
+  const float maxDistance = 1.2f * p->max_dist, minDistance = 0.8f * p->min_dist;
+  const float PO[3] = {X[0] - P->Ow[0], X[1] - P->Ow[1], X[2] - P->Ow[2]};
+  const float dist = norm3(PO);
+  if (dist < minDistance || dist > maxDistance) return 0;
+  const float Pn[3] = {p->nx, p->ny, p->nz};
+  if (dot3(PO, Pn) < 0.5 * dist) return 0;
+  *level = predict_scale(p->max_dist, dist, logf(F->scale_factors[1]), F->n_levels);
+  return 1;
+}
+
+int orc_search_by_projection_sim3(orc_frame *F, const float *Scw, const orc_map_point *mps, const uint8_t *mp_desc,
+                                  int n, int th) {
+  orc_grid G;
+  grid_build(F, &G);
+  orc_pose P;
+  pose_from_sim3(Scw, &P);
+  int *vIndices = (int *)malloc(sizeof(int) * (F->n > 0 ? F->n : 1));
+  int nmatches = 0;
+  for (int iMP = 0; iMP < n; iMP++) {
+    const orc_map_point *p = &mps[iMP];
+    if (p->skip) continue;
+    float u, v, invz;
+    int pl;
+    if (!project_kf(F, &P, p, &u, &v, &invz, &pl)) continue;
+    const float radius = th * F->scale_factors[pl];
+    /* KeyFrame::GetFeaturesInArea (KeyFrame.cc:809-853) + the level test of :518-520 */
+    const int nI = area(F, &G, u, v, radius, pl - 1, pl, vIndices);
+    int bestDist = 256, bestIdx = -1;
+    for (int q = 0; q < nI; ++q) {
+      const int idx = vIndices[q];
+      if (F->slot_mp[idx] >= 0) continue;
+      const int dist = orc_hamming(mp_desc + 32 * (size_t)iMP, F->desc + 32 * (size_t)idx);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= TH_LOW) {
+      F->slot_mp[bestIdx] = p->id;
+      nmatches++;
+    }
+  }
+  free(vIndices);
+  grid_free(&G);
+  return nmatches;
+}
+
+int orc_fuse(const orc_frame *F, const float *T, int sim3, const orc_map_point *mps, const uint8_t *mp_desc, int n,
+             float th, int *fuse_idx) {
+  orc_grid G;
+  grid_build(F, &G);
+  orc_pose P;
+  if (sim3)
+    pose_from_sim3(T, &P);
+  else
+    pose_from_T(T, &P);
+  int *vIndices = (int *)malloc(sizeof(int) * (F->n > 0 ? F->n : 1));
+  int nFused = 0;
+  for (int i = 0; i < n; i++) {
+    fuse_idx[i] = -1;
+    const orc_map_point *p = &mps[i];
+    if (p->skip) continue;
+    float u, v, invz;
+    int pl;
+    if (!project_kf(F, &P, p, &u, &v, &invz, &pl)) continue;
+    const float ur = u - F->bf * invz;
+    const float radius = th * F->scale_factors[pl];
+    const int nI = area(F, &G, u, v, radius, pl - 1, pl, vIndices);
+    int bestDist = sim3 ? INT_MAX : 256, bestIdx = -1;
+    for (int q = 0; q < nI; ++q) {
+      const int idx = vIndices[q];
+      const orc_kp *kp = &F->kps[idx];
+      const int kpLevel = kp->octave;
+      if (!sim3) { /* :1209-1237: reprojection gate, 3 dof (stereo) or 2 dof */
+        const float s2 = F->scale_factors[kpLevel] * F->scale_factors[kpLevel];
+        const float inv_s2 = 1.0f / s2;
+        if (F->uright && F->uright[idx] >= 0) {
+          const float ex = u - kp->x, ey = v - kp->y, er = ur - F->uright[idx];
+          const float e2 = ex * ex + ey * ey + er * er;
+          if (e2 * inv_s2 > 7.8) continue;
+        } else {
+          const float ex = u - kp->x, ey = v - kp->y;
+          const float e2 = ex * ex + ey * ey;
+          if (e2 * inv_s2 > 5.99) continue;
+        }
+      }
+      const int dist = orc_hamming(mp_desc + 32 * (size_t)i, F->desc + 32 * (size_t)idx);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= TH_LOW) {
+      fuse_idx[i] = bestIdx;
+      nFused++;
+    }
+  }
+  free(vIndices);
+  grid_free(&G);
+  return nFused;
+}
+
+int orc_search_by_projection_kf(orc_frame *F, const float *Tcw, const orc_map_point *mps, const uint8_t *mp_desc,
+                                const float *kf_angle, int n, float th, int orb_dist, int check_ori) {
+  orc_grid G;
+  grid_build(F, &G);
+  orc_pose P;
+  pose_from_T(Tcw, &P);
+  int *vIndices2 = (int *)malloc(sizeof(int) * (F->n > 0 ? F->n : 1));
+  int *rot_bin = (int *)malloc(sizeof(int) * (n > 0 ? n : 1));
+  int *rot_idx = (int *)malloc(sizeof(int) * (n > 0 ? n : 1));
+  int nrot = 0, hist[HISTO_LENGTH] = {0}, nmatches = 0;
+  const float factor = HISTO_LENGTH / 360.0f;
+  const float t[3] = {P.T[3], P.T[7], P.T[11]};
+  for (int i = 0; i < n; i++) {
+    const orc_map_point *p = &mps[i];
+    if (p->skip) continue;
+    const float X[3] = {p->x, p->y, p->z};
+    float Xc[3];
+    mat3_mul_add(P.T, 0, X, t, 1.0f, Xc);
+    const float xc = Xc[0], yc = Xc[1];
+    const float invzc = (float)(1.0 / (double)Xc[2]);
+    const float u = F->fx * xc * invzc + F->cx, v = F->fy * yc * invzc + F->cy;
+    if (u < F->bounds.min_x || u > F->bounds.max_x) continue;
+    if (v < F->bounds.min_y || v > F->bounds.max_y) continue;
+    const float PO[3] = {X[0] - P.Ow[0], X[1] - P.Ow[1], X[2] - P.Ow[2]};
+    const float dist3D = norm3(PO);
+    const float maxDistance = 1.2f * p->max_dist, minDistance = 0.8f * p->min_dist;
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    const int pl = predict_scale(p->max_dist, dist3D, logf(F->scale_factors[1]), F->n_levels);
+    const float radius = th * F->scale_factors[pl];
+    const int nI = area(F, &G, u, v, radius, pl - 1, pl + 1, vIndices2);
+    int bestDist = 256, bestIdx2 = -1;
+    for (int q = 0; q < nI; ++q) {
+      const int i2 = vIndices2[q];
+      if (F->slot_mp[i2] >= 0) continue;
+      const int dist = orc_hamming(mp_desc + 32 * (size_t)i, F->desc + 32 * (size_t)i2);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = i2;
+      }
+    }
+    if (bestDist <= orb_dist) {
+      F->slot_mp[bestIdx2] = p->id;
+      nmatches++;
+      if (check_ori) {
+        float rot = kf_angle[i] - F->kps[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)roundf(rot * factor);
+        if (bin == HISTO_LENGTH) bin = 0;
+        rot_bin[nrot] = bin;
+        rot_idx[nrot++] = bestIdx2;
+        hist[bin]++;
+      }
+    }
+  }
+  if (check_ori) {
+    int ind1, ind2, ind3;
+    three_maxima(hist, &ind1, &ind2, &ind3);
+    for (int b = 0; b < HISTO_LENGTH; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (int q = 0; q < nrot; ++q)
+        if (rot_bin[q] == b) {
+          F->slot_mp[rot_idx[q]] = -1;
+          nmatches--;
+        }
+    }
+  }
+  free(vIndices2);
+  free(rot_bin);
+  free(rot_idx);
+  grid_free(&G);
+  return nmatches;
+}
+
+/* ---- BoW searches: DBoW2 FeatureVector (std::map<NodeId, vector<unsigned>>,
+ * features pushed in index order) as node-sorted index runs ---- */
+typedef struct {
+  int *idx; /* feature indices sorted by (node, index) */
+  int n;    /* features present */
+} orc_featvec;
+
+static const int *g_sort_node;
+static int cmp_node_idx(const void *a, const void *b) {
+  const int ia = *(const int *)a, ib = *(const int *)b;
+  if (g_sort_node[ia] != g_sort_node[ib]) return g_sort_node[ia] < g_sort_node[ib] ? -1 : 1;
+  return ia < ib ? -1 : ia > ib;
+}
+
+static void featvec_build(const orc_bow_frame *K, orc_featvec *V) {
+  V->idx = (int *)malloc(sizeof(int) * (K->n > 0 ? K->n : 1));
+  V->n = 0;
+  for (int i = 0; i < K->n; ++i)
+    if (K->node[i] >= 0) V->idx[V->n++] = i;
+  g_sort_node = K->node;
+  qsort(V->idx, V->n, sizeof(int), cmp_node_idx);
+}
+
+/* The common nodes in increasing order (the KFit / Fit merge with lower_bound,
+ * ORBmatcher.cc:280-382): calls visit(node run of side 1, node run of side 2). */
+typedef void (*orc_node_visit)(void *ctx, const int *r1, int n1, const int *r2, int n2);
+static void featvec_merge(const orc_bow_frame *K1, const orc_featvec *V1, const orc_bow_frame *K2,
+                          const orc_featvec *V2, orc_node_visit visit, void *ctx) {
+  int a = 0, b = 0;
+  while (a < V1->n && b < V2->n) {
+    const int na = K1->node[V1->idx[a]], nb = K2->node[V2->idx[b]];
+    if (na == nb) {
+      int ea = a, eb = b;
+      while (ea < V1->n && K1->node[V1->idx[ea]] == na) ea++;
+      while (eb < V2->n && K2->node[V2->idx[eb]] == nb) eb++;
+      visit(ctx, V1->idx + a, ea - a, V2->idx + b, eb - b);
+      a = ea;
+      b = eb;
+    } else if (na < nb) {
+      while (a < V1->n && K1->node[V1->idx[a]] < nb) a++;
+    } else {
+      while (b < V2->n && K2->node[V2->idx[b]] < na) b++;
+    }
+  }
+}
+
+typedef struct {
+  const orc_bow_frame *K1, *K2;
+  float nnratio;
+  int check_ori, nmatches, nrot, hist[HISTO_LENGTH];
+  int *out, *rot_bin, *rot_idx;
+  uint8_t *matched2;
+  /* SearchForTriangulation */
+  float ex, ey;
+  const float *F12, *sf2;
+  int only_stereo;
+} orc_bow_ctx;
+
+static void rot_push(orc_bow_ctx *c, float a1, float a2, int idx) {
+  const float factor = HISTO_LENGTH / 360.0f;
+  float rot = a1 - a2;
+  if (rot < 0.0) rot += 360.0f;
+  int bin = (int)roundf(rot * factor);
+  if (bin == HISTO_LENGTH) bin = 0;
+  c->rot_bin[c->nrot] = bin;
+  c->rot_idx[c->nrot++] = idx;
+  c->hist[bin]++;
+}
+
+/* the rejected bins' entries, bin by bin (ORBmatcher.cc:384-400 and alike);
+ * clear(ctx, idx) undoes one match. */
+static void rot_reject(orc_bow_ctx *c, void (*clear)(orc_bow_ctx *, int)) {
+  int ind1, ind2, ind3;
+  three_maxima(c->hist, &ind1, &ind2, &ind3);
+  for (int b = 0; b < HISTO_LENGTH; b++) {
+    if (b == ind1 || b == ind2 || b == ind3) continue;
+    for (int q = 0; q < c->nrot; ++q)
+      if (c->rot_bin[q] == b) {
+        clear(c, c->rot_idx[q]);
+        c->nmatches--;
+      }
+  }
+}
+
+static void visit_kf_frame(void *vc, const int *r1, int n1, const int *r2, int n2) {
+  orc_bow_ctx *c = (orc_bow_ctx *)vc;
+  for (int i = 0; i < n1; ++i) { /* :296-362 */
+    const int realIdxKF = r1[i];
+    if (c->K1->mp[realIdxKF] < 0) continue;
+    if (c->K1->mp_bad && c->K1->mp_bad[realIdxKF]) continue;
+    int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+    for (int j = 0; j < n2; ++j) {
+      const int realIdxF = r2[j];
+      if (c->out[realIdxF] >= 0) continue;
+      const int dist = orc_hamming(c->K1->desc + 32 * (size_t)realIdxKF, c->K2->desc + 32 * (size_t)realIdxF);
+      if (dist < bestDist1) {
+        bestDist2 = bestDist1;
+        bestDist1 = dist;
+        bestIdxF = realIdxF;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist1 <= TH_LOW) {
+      if ((float)bestDist1 < c->nnratio * (float)bestDist2) {
+        c->out[bestIdxF] = c->K1->mp[realIdxKF];
+        if (c->check_ori) rot_push(c, c->K1->kps[realIdxKF].angle, c->K2->kps[bestIdxF].angle, bestIdxF);
+        c->nmatches++;
+      }
+    }
+  }
+}
+
+static void clear_out(orc_bow_ctx *c, int idx) { c->out[idx] = -1; }
+
+int orc_search_by_bow_kf_frame(const orc_bow_frame *KF, const orc_bow_frame *F, float nnratio, int check_ori,
+                               int *matches) {
+  orc_bow_ctx c;
+  memset(&c, 0, sizeof(c));
+  c.K1 = KF;
+  c.K2 = F;
+  c.nnratio = nnratio;
+  c.check_ori = check_ori;
+  c.out = matches;
+  for (int i = 0; i < F->n; ++i) matches[i] = -1;
+  c.rot_bin = (int *)malloc(sizeof(int) * (KF->n > 0 ? KF->n : 1));
+  c.rot_idx = (int *)malloc(sizeof(int) * (KF->n > 0 ? KF->n : 1));
+  orc_featvec V1, V2;
+  featvec_build(KF, &V1);
+  featvec_build(F, &V2);
+  featvec_merge(KF, &V1, F, &V2, visit_kf_frame, &c);
+  if (check_ori) rot_reject(&c, clear_out);
+  free(V1.idx);
+  free(V2.idx);
+  free(c.rot_bin);
+  free(c.rot_idx);
+  return c.nmatches;
+}
+
+static void visit_kf_kf(void *vc, const int *r1, int n1, const int *r2, int n2) {
+  orc_bow_ctx *c = (orc_bow_ctx *)vc;
+  for (int i = 0; i < n1; ++i) { /* :775-845 */
+    const int idx1 = r1[i];
+    if (c->K1->mp[idx1] < 0) continue;
+    if (c->K1->mp_bad && c->K1->mp_bad[idx1]) continue;
+    int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+    for (int j = 0; j < n2; ++j) {
+      const int idx2 = r2[j];
+      if (c->matched2[idx2] || c->K2->mp[idx2] < 0) continue;
+      if (c->K2->mp_bad && c->K2->mp_bad[idx2]) continue;
+      const int dist = orc_hamming(c->K1->desc + 32 * (size_t)idx1, c->K2->desc + 32 * (size_t)idx2);
+      if (dist < bestDist1) {
+        bestDist2 = bestDist1;
+        bestDist1 = dist;
+        bestIdx2 = idx2;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist1 < TH_LOW) {
+      if ((float)bestDist1 < c->nnratio * (float)bestDist2) {
+        c->out[idx1] = c->K2->mp[bestIdx2];
+        c->matched2[bestIdx2] = 1;
+        if (c->check_ori) rot_push(c, c->K1->kps[idx1].angle, c->K2->kps[bestIdx2].angle, idx1);
+        c->nmatches++;
+      }
+    }
+  }
+}
+
+int orc_search_by_bow_kf_kf(const orc_bow_frame *K1, const orc_bow_frame *K2, float nnratio, int check_ori,
+                            int *matches12) {
+  orc_bow_ctx c;
+  memset(&c, 0, sizeof(c));
+  c.K1 = K1;
+  c.K2 = K2;
+  c.nnratio = nnratio;
+  c.check_ori = check_ori;
+  c.out = matches12;
+  for (int i = 0; i < K1->n; ++i) matches12[i] = -1;
+  c.matched2 = (uint8_t *)calloc(K2->n > 0 ? K2->n : 1, 1);
+  c.rot_bin = (int *)malloc(sizeof(int) * (K1->n > 0 ? K1->n : 1));
+  c.rot_idx = (int *)malloc(sizeof(int) * (K1->n > 0 ? K1->n : 1));
+  orc_featvec V1, V2;
+  featvec_build(K1, &V1);
+  featvec_build(K2, &V2);
+  featvec_merge(K1, &V1, K2, &V2, visit_kf_kf, &c);
+  if (check_ori) rot_reject(&c, clear_out); /* vbMatched2 is not reset (:855-866) */
+  free(V1.idx);
+  free(V2.idx);
+  free(c.matched2);
+  free(c.rot_bin);
+  free(c.rot_idx);
+  return c.nmatches;
+}
+
+/* CheckDistEpipolarLine (ORBmatcher.cc:203-229). */
+static int check_epipolar(const orc_kp *kp1, const orc_kp *kp2, const float *F, const float *sf2) {
+  const float a = kp1->x * F[0] + kp1->y * F[3] + F[6];
+  const float b = kp1->x * F[1] + kp1->y * F[4] + F[7];
+  const float c = kp1->x * F[2] + kp1->y * F[5] + F[8];
+  const float num = a * kp2->x + b * kp2->y + c;
+  const float den = a * a + b * b;
+  if (den == 0) return 0;
+  const float dsqr = num * num / den;
+  const float sigma2 = sf2[kp2->octave] * sf2[kp2->octave];
+  return dsqr < 3.84 * sigma2;
+}
+
+static void visit_triangulation(void *vc, const int *r1, int n1, const int *r2, int n2) {
+  orc_bow_ctx *c = (orc_bow_ctx *)vc;
+  for (int i = 0; i < n1; ++i) { /* :936-1030 */
+    const int idx1 = r1[i];
+    if (c->K1->mp[idx1] >= 0) continue;
+    const int bStereo1 = c->K1->uright && c->K1->uright[idx1] >= 0;
+    if (c->only_stereo && !bStereo1) continue;
+    const orc_kp *kp1 = &c->K1->kps[idx1];
+    int bestDist = TH_LOW, bestIdx2 = -1;
+    for (int j = 0; j < n2; ++j) {
+      const int idx2 = r2[j];
+      if (c->matched2[idx2] || c->K2->mp[idx2] >= 0) continue;
+      const int bStereo2 = c->K2->uright && c->K2->uright[idx2] >= 0;
+      if (c->only_stereo && !bStereo2) continue;
+      const int dist = orc_hamming(c->K1->desc + 32 * (size_t)idx1, c->K2->desc + 32 * (size_t)idx2);
+      if (dist > TH_LOW || dist > bestDist) continue;
+      const orc_kp *kp2 = &c->K2->kps[idx2];
+      if (!bStereo1 && !bStereo2) {
+        const float distex = c->ex - kp2->x, distey = c->ey - kp2->y;
+        if (distex * distex + distey * distey < 100 * c->sf2[kp2->octave]) continue;
+      }
+      if (check_epipolar(kp1, kp2, c->F12, c->sf2)) {
+        bestIdx2 = idx2;
+        bestDist = dist;
+      }
+    }
+    if (bestIdx2 >= 0) {
+      c->out[idx1] = bestIdx2;
+      c->matched2[bestIdx2] = 1;
+      c->nmatches++;
+      if (c->check_ori) rot_push(c, kp1->angle, c->K2->kps[bestIdx2].angle, idx1);
+    }
+  }
+}
+
+static void clear_tri(orc_bow_ctx *c, int idx1) {
+  c->matched2[c->out[idx1]] = 0; /* :1073 */
+  c->out[idx1] = -1;
+}
+
+int orc_search_for_triangulation(const orc_bow_frame *K1, const orc_bow_frame *K2, const float *C1, const float *T2w,
+                                 const float *cam2, const float *scale_factors2, const float *F12, int only_stereo,
+                                 int check_ori, int *m12) {
+  orc_bow_ctx c;
+  memset(&c, 0, sizeof(c));
+  c.K1 = K1;
+  c.K2 = K2;
+  c.check_ori = check_ori;
+  c.out = m12;
+  c.F12 = F12;
+  c.sf2 = scale_factors2;
+  c.only_stereo = only_stereo;
+  for (int i = 0; i < K1->n; ++i) m12[i] = -1;
+  /* epipole: C2 = R2w * Cw + t2w, (ex, ey) (:903-913) */
+  const float t2[3] = {T2w[3], T2w[7], T2w[11]};
+  float C2[3];
+  mat3_mul_add(T2w, 0, C1, t2, 1.0f, C2);
+  const float invz = 1.0f / C2[2];
+  c.ex = cam2[0] * C2[0] * invz + cam2[2];
+  c.ey = cam2[1] * C2[1] * invz + cam2[3];
+  c.matched2 = (uint8_t *)calloc(K2->n > 0 ? K2->n : 1, 1);
+  c.rot_bin = (int *)malloc(sizeof(int) * (K1->n > 0 ? K1->n : 1));
+  c.rot_idx = (int *)malloc(sizeof(int) * (K1->n > 0 ? K1->n : 1));
+  orc_featvec V1, V2;
+  featvec_build(K1, &V1);
+  featvec_build(K2, &V2);
+  featvec_merge(K1, &V1, K2, &V2, visit_triangulation, &c);
+  if (check_ori) rot_reject(&c, clear_tri);
+  free(V1.idx);
+  free(V2.idx);
+  free(c.matched2);
+  free(c.rot_bin);
+  free(c.rot_idx);
+  return c.nmatches;
+}

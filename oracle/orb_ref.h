@@ -128,4 +128,56 @@ int orc_search_by_projection_local(orc_frame *F, const orc_track_point *mps, con
  * CurrentFrame.mTcw / LastFrame.mTcw (float, row-major). */
 int orc_search_by_projection_last(orc_frame *F, const float *Tcw, const float *Tlw, const orc_last_point *lp,
                                   const uint8_t *ldesc, int n_last, float th, int mono, int check_ori);
+
+/* A map point as the keyframe searches read it (MapPoint.h): mnId,
+ * GetWorldPos(), GetNormal(), mfMinDistance / mfMaxDistance and the caller's
+ * pre-filter (isBad(), already found / already in the keyframe). Layout equal
+ * to sqlm_map_point. */
+typedef struct orc_map_point {
+  int id;
+  float x, y, z, nx, ny, nz, min_dist, max_dist;
+  uint8_t skip, pad[3];
+} orc_map_point;
+
+/* SearchByProjection(pKF, Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:423-571):
+ * F = pKF (slot_mp = vpMatched, updated). Returns nmatches. */
+int orc_search_by_projection_sim3(orc_frame *F, const float *Scw, const orc_map_point *mps, const uint8_t *mp_desc,
+                                  int n, int th);
+/* Fuse(pKF, vpMapPoints, th) (:1109-1294) and Fuse(pKF, Scw, vpPoints, th,
+ * vpReplacePoint) (:1296-1446): the keypoint each point fuses into (-1: none)
+ * in fuse_idx; the caller applies Replace / AddMapPoint in point order.
+ * Returns nFused. sim3 = 0: T is pKF's Tcw; 1: T is Scw. */
+int orc_fuse(const orc_frame *F, const float *T, int sim3, const orc_map_point *mps, const uint8_t *mp_desc, int n,
+             float th, int *fuse_idx);
+/* SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+ * (:1902-2046): F = CurrentFrame with Tcw; mps / kf_angle = pKF's slots. */
+int orc_search_by_projection_kf(orc_frame *F, const float *Tcw, const orc_map_point *mps, const uint8_t *mp_desc,
+                                const float *kf_angle, int n, float th, int orb_dist, int check_ori);
+
+/* A keyframe as the BoW searches read it: mvKeysUn, mDescriptors, the node of
+ * each feature in mFeatVec (DBoW2 FeatureVector; -1: not in it),
+ * GetMapPointMatches() ids (-1: NULL), their isBad() (NULL: none bad),
+ * mvuRight (NULL: monocular). Layout equal to sqlm_bow_frame. */
+typedef struct orc_bow_frame {
+  const orc_kp *kps;
+  const uint8_t *desc;
+  const int *node;
+  const int *mp;
+  const uint8_t *mp_bad;
+  const float *uright;
+  int n;
+} orc_bow_frame;
+
+/* SearchByBoW(pKF, F, vpMapPointMatches) (:246-403): matches [F.n] = map-point ids. */
+int orc_search_by_bow_kf_frame(const orc_bow_frame *KF, const orc_bow_frame *F, float nnratio, int check_ori,
+                               int *matches);
+/* SearchByBoW(pKF1, pKF2, vpMatches12) (:731-869): matches12 [KF1.n] = KF2 map-point ids. */
+int orc_search_by_bow_kf_kf(const orc_bow_frame *K1, const orc_bow_frame *K2, float nnratio, int check_ori,
+                            int *matches12);
+/* SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+ * (:887-1096): m12 [K1.n] = matched KF2 keypoint (-1: none); C1 = pKF1's
+ * camera centre, T2w = pKF2's 3x4 pose, cam2 = fx fy cx cy, F12 row-major. */
+int orc_search_for_triangulation(const orc_bow_frame *K1, const orc_bow_frame *K2, const float *C1, const float *T2w,
+                                 const float *cam2, const float *scale_factors2, const float *F12, int only_stereo,
+                                 int check_ori, int *m12);
 #endif

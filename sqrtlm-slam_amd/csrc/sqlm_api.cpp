@@ -1833,6 +1833,46 @@ int sqlm_orb_search_by_projection_last(sqlm_ctx *c, sqlm_orb_frame *F, const flo
   return orb_search_by_projection_last(c->orb, F, Tcw, Tlw, lp, ldesc, n_last, th, mono, check_ori, n_matches);
 }
 
+int sqlm_orb_search_by_projection_sim3(sqlm_ctx *c, sqlm_orb_frame *F, const float *Scw, const sqlm_map_point *mps,
+                                       const uint8_t *mp_desc, int n, int th, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_by_projection_sim3(c->orb, F, Scw, mps, mp_desc, n, th, n_matches);
+}
+
+int sqlm_orb_fuse(sqlm_ctx *c, const sqlm_orb_frame *F, const float *T, int sim3, const sqlm_map_point *mps,
+                  const uint8_t *mp_desc, int n, float th, int32_t *fuse_idx, int *n_fused) {
+  if (int r = orb_engine(c)) return r;
+  return orb_fuse(c->orb, F, T, sim3, mps, mp_desc, n, th, fuse_idx, n_fused);
+}
+
+int sqlm_orb_search_by_projection_kf(sqlm_ctx *c, sqlm_orb_frame *F, const float *Tcw, const sqlm_map_point *mps,
+                                     const uint8_t *mp_desc, const float *kf_angle, int n, float th, int orb_dist,
+                                     int check_ori, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_by_projection_kf(c->orb, F, Tcw, mps, mp_desc, kf_angle, n, th, orb_dist, check_ori, n_matches);
+}
+
+int sqlm_orb_search_by_bow_kf_frame(sqlm_ctx *c, const sqlm_bow_frame *KF, const sqlm_bow_frame *F, float nnratio,
+                                    int check_ori, int32_t *matches, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_by_bow_kf_frame(c->orb, KF, F, nnratio, check_ori, matches, n_matches);
+}
+
+int sqlm_orb_search_by_bow_kf_kf(sqlm_ctx *c, const sqlm_bow_frame *K1, const sqlm_bow_frame *K2, float nnratio,
+                                 int check_ori, int32_t *matches12, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_by_bow_kf_kf(c->orb, K1, K2, nnratio, check_ori, matches12, n_matches);
+}
+
+int sqlm_orb_search_for_triangulation(sqlm_ctx *c, const sqlm_bow_frame *K1, const sqlm_bow_frame *K2,
+                                      const float *C1, const float *T2w, const float *cam2,
+                                      const float *scale_factors2, int n_levels2, const float *F12, int only_stereo,
+                                      int check_ori, int32_t *m12, int *n_matches) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_for_triangulation(c->orb, K1, K2, C1, T2w, cam2, scale_factors2, n_levels2, F12, only_stereo,
+                                      check_ori, m12, n_matches);
+}
+
 int sqlm_orb_bench_extract(sqlm_ctx *c, const sqlm_orb_params *p, const uint8_t *image, int w, int h, int stride,
                            int reps, double *ms_per_frame, double *stage_ms) {
   if (int r = orb_engine(c)) return r;

@@ -291,5 +291,21 @@ int orb_search_by_projection_local(OrbEngine *e, struct sqlm_orb_frame *F, const
 int orb_search_by_projection_last(OrbEngine *e, struct sqlm_orb_frame *F, const float *Tcw, const float *Tlw,
                                   const struct sqlm_last_point *lp, const uint8_t *ldesc, int n_last, float th,
                                   int mono, int check_ori, int *n_matches);
+int orb_search_by_projection_sim3(OrbEngine *e, struct sqlm_orb_frame *F, const float *Scw,
+                                  const struct sqlm_map_point *mps, const uint8_t *mp_desc, int n, int th,
+                                  int *n_matches);
+int orb_fuse(OrbEngine *e, const struct sqlm_orb_frame *F, const float *T, int sim3, const struct sqlm_map_point *mps,
+             const uint8_t *mp_desc, int n, float th, int32_t *fuse_idx, int *n_fused);
+int orb_search_by_projection_kf(OrbEngine *e, struct sqlm_orb_frame *F, const float *Tcw,
+                                const struct sqlm_map_point *mps, const uint8_t *mp_desc, const float *kf_angle, int n,
+                                float th, int orb_dist, int check_ori, int *n_matches);
+int orb_search_by_bow_kf_frame(OrbEngine *e, const struct sqlm_bow_frame *KF, const struct sqlm_bow_frame *F,
+                               float nnratio, int check_ori, int32_t *matches, int *n_matches);
+int orb_search_by_bow_kf_kf(OrbEngine *e, const struct sqlm_bow_frame *K1, const struct sqlm_bow_frame *K2,
+                            float nnratio, int check_ori, int32_t *matches12, int *n_matches);
+int orb_search_for_triangulation(OrbEngine *e, const struct sqlm_bow_frame *K1, const struct sqlm_bow_frame *K2,
+                                 const float *C1, const float *T2w, const float *cam2, const float *sf2,
+                                 int n_levels2, const float *F12, int only_stereo, int check_ori, int32_t *m12,
+                                 int *n_matches);
 
 }  // namespace sqlm

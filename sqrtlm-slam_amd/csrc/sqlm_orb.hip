@@ -568,6 +568,28 @@ __global__ __launch_bounds__(256) void k_area_list(AreaArgs A, int *__restrict__
   if (PASS == 0 && lane == 0) cnt[i1] = run;
 }
 
+// BoW node runs (SearchByBoW / SearchForTriangulation): query q = (feature
+// of side 1, run [b, e) of side-2 features in cand, output offset); one wave
+// per query, one candidate per lane: dist[off + j] = Hamming(d1[f], d2[cand[b + j]]).
+__global__ __launch_bounds__(256) void k_cand_dist(const int4 *__restrict__ q, int nq, const uint32_t *__restrict__ d1,
+                                                   const uint32_t *__restrict__ d2, const int *__restrict__ cand,
+                                                   int *__restrict__ dist) {
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= nq) return;
+  const int4 Q = q[w];
+  uint32_t my[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) my[k] = d1[(size_t)8 * Q.x + k];
+  for (int j = Q.y + lane; j < Q.z; j += 64) {
+    const int i2 = cand[j];
+    int d = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d += __builtin_popcount(my[k] ^ d2[(size_t)8 * i2 + k]);
+    dist[Q.w + (j - Q.y)] = d;
+  }
+}
+
 // ---- host: DistributeOctTree (ORBextractor.cc:606-1043) -----------------------------
 struct Cand {
   float x, y, response;
@@ -1534,6 +1556,488 @@ int orb_search_by_projection_last(OrbEngine *e, sqlm_orb_frame *F, const float *
         }
     }
   }
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+// ---- keyframe projection searches (ORBmatcher.cc:423, :1109, :1296, :1902) ----
+// [R | t] rows and Ow = -R^T t, as pKF->GetRotation() / GetTranslation() /
+// GetCameraCenter() hold them.
+struct ProjPose {
+  float T[12];
+  float Ow[3];
+  void finish() {
+    const float t[3] = {T[3], T[7], T[11]};
+    mat3_mul_add(T, true, t, nullptr, -1.0, Ow);
+  }
+  explicit ProjPose(const float *Tcw) {
+    std::memcpy(T, Tcw, sizeof(T));
+    finish();
+  }
+  // Scw -> s = sqrt(row0 . row0) (Mat::dot in double), [R | t] = [sR | t] / s
+  // (a float scale by (float)(1 / s)) (ORBmatcher.cc:434-441)
+  ProjPose(const float *S, bool) {
+    const double d = (double)S[0] * S[0] + (double)S[1] * S[1] + (double)S[2] * S[2];
+    const float scw = (float)std::sqrt(d);
+    const float inv = (float)(1.0 / (double)scw);
+    for (int i = 0; i < 12; ++i) T[i] = S[i] * inv;
+    finish();
+  }
+};
+
+// cv::norm (double sum of squares) and Mat::dot (double) of 3x1 CV_32F
+static float norm3(const float *v) {
+  double s = 0;
+  for (int i = 0; i < 3; ++i) s += (double)v[i] * v[i];
+  return (float)std::sqrt(s);
+}
+static double dot3(const float *a, const float *b) {
+  double s = 0;
+  for (int i = 0; i < 3; ++i) s += (double)a[i] * b[i];
+  return s;
+}
+
+// MapPoint::PredictScale (MapPoint.cc:610-650)
+static int predict_scale(float max_dist, float dist, float log_scale, int n_levels) {
+  const float ratio = max_dist / dist;
+  int nScale = (int)std::ceil(std::log(ratio) / log_scale);
+  if (nScale < 0)
+    nScale = 0;
+  else if (nScale >= n_levels)
+    nScale = n_levels - 1;
+  return nScale;
+}
+
+// The keyframe-side projection (ORBmatcher.cc:447-489, :1132-1180, :1327-1372):
+// z >= 0, IsInImage, distance invariance band, viewing angle, predicted level.
+static bool project_kf(const sqlm_orb_frame *F, const ProjPose &P, const sqlm_map_point &p, float &u, float &v,
+                       float &invz, int &level) {
+  const float X[3] = {p.x, p.y, p.z}, t[3] = {P.T[3], P.T[7], P.T[11]};
+  float Xc[3];
+  mat3_mul_add(P.T, false, X, t, 1.0, Xc);
+  if (Xc[2] < 0.0f) return false;
+  invz = 1 / Xc[2];
+  const float x = Xc[0] * invz, y = Xc[1] * invz;
+  u = F->fx * x + F->cx;
+  v = F->fy * y + F->cy;
+  if (!(u >= F->bounds.min_x && u < F->bounds.max_x && v >= F->bounds.min_y && v < F->bounds.max_y)) return false;
+  const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+  const float PO[3] = {X[0] - P.Ow[0], X[1] - P.Ow[1], X[2] - P.Ow[2]};
+  const float dist = norm3(PO);
+  if (dist < minDistance || dist > maxDistance) return false;
+  const float Pn[3] = {p.nx, p.ny, p.nz};
+  if (dot3(PO, Pn) < 0.5 * dist) return false;
+  level = predict_scale(p.max_dist, dist, std::log(F->scale_factors[1]), F->n_levels);
+  return true;
+}
+
+static bool kf_frame_ok(const sqlm_orb_frame *F) {
+  return F && F->n >= 0 && F->n_levels >= 2 && F->scale_factors && (F->n == 0 || (F->kps && F->desc));
+}
+
+int orb_search_by_projection_sim3(OrbEngine *e, sqlm_orb_frame *F, const float *Scw, const sqlm_map_point *mps,
+                                  const uint8_t *mp_desc, int n, int th, int *n_matches) {
+  if (!kf_frame_ok(F) || !F->slot_mp || !Scw || n < 0 || (n && (!mps || !mp_desc))) return SQLM_ERR_INVALID_ARG;
+  if (n_matches) *n_matches = 0;
+  const ProjPose P(Scw, true);
+  std::vector<float4> hq(n);
+  for (int i = 0; i < n; ++i) {
+    hq[i] = area_query(0.f, 0.f, 0.f, kAreaSkip);
+    float u, v, invz;
+    int pl;
+    if (mps[i].skip || !project_kf(F, P, mps[i], u, v, invz, pl)) continue;
+    // KeyFrame::GetFeaturesInArea (KeyFrame.cc:809-853) + the level test (ORBmatcher.cc:518-520)
+    hq[i] = area_query(u, v, th * F->scale_factors[pl], area_levels(pl - 1, pl));
+  }
+  std::vector<int> hoff;
+  std::vector<int2> hp;
+  if (int rc = area_search(e, F->kps, F->desc, F->n, &F->bounds, hq, mp_desc, hoff, hp)) return rc;
+  int nmatches = 0;
+  for (int i = 0; i < n; ++i) {  // :505-541
+    int bestDist = 256, bestIdx = -1;
+    for (int q = hoff[i]; q < hoff[i + 1]; ++q) {
+      const int idx = hp[q].x, dist = hp[q].y;
+      if (F->slot_mp[idx] >= 0) continue;
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= kThLow) {
+      F->slot_mp[bestIdx] = mps[i].id;
+      nmatches++;
+    }
+  }
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+int orb_fuse(OrbEngine *e, const sqlm_orb_frame *F, const float *T, int sim3, const sqlm_map_point *mps,
+             const uint8_t *mp_desc, int n, float th, int32_t *fuse_idx, int *n_fused) {
+  if (!kf_frame_ok(F) || !T || n < 0 || (n && (!mps || !mp_desc || !fuse_idx))) return SQLM_ERR_INVALID_ARG;
+  if (n_fused) *n_fused = 0;
+  const ProjPose P = sim3 ? ProjPose(T, true) : ProjPose(T);
+  std::vector<float4> hq(n);
+  std::vector<float> hu(n), hv(n), hur(n);
+  for (int i = 0; i < n; ++i) {
+    fuse_idx[i] = -1;
+    hq[i] = area_query(0.f, 0.f, 0.f, kAreaSkip);
+    float u, v, invz;
+    int pl;
+    if (mps[i].skip || !project_kf(F, P, mps[i], u, v, invz, pl)) continue;
+    hu[i] = u;
+    hv[i] = v;
+    hur[i] = u - F->bf * invz;
+    hq[i] = area_query(u, v, th * F->scale_factors[pl], area_levels(pl - 1, pl));
+  }
+  std::vector<int> hoff;
+  std::vector<int2> hp;
+  if (int rc = area_search(e, F->kps, F->desc, F->n, &F->bounds, hq, mp_desc, hoff, hp)) return rc;
+  int nFused = 0;
+  for (int i = 0; i < n; ++i) {
+    int bestDist = sim3 ? INT_MAX : 256, bestIdx = -1;
+    for (int q = hoff[i]; q < hoff[i + 1]; ++q) {
+      const int idx = hp[q].x, dist = hp[q].y;
+      const sqlm_keypoint &kp = F->kps[idx];
+      if (!sim3) {  // :1209-1237: reprojection gate, stereo (3 dof) or monocular (2 dof)
+        const float s2 = F->scale_factors[kp.octave] * F->scale_factors[kp.octave];
+        const float inv_s2 = 1.0f / s2;
+        if (F->uright && F->uright[idx] >= 0) {
+          const float ex = hu[i] - kp.x, ey = hv[i] - kp.y, er = hur[i] - F->uright[idx];
+          const float e2 = ex * ex + ey * ey + er * er;
+          if (e2 * inv_s2 > 7.8) continue;
+        } else {
+          const float ex = hu[i] - kp.x, ey = hv[i] - kp.y;
+          const float e2 = ex * ex + ey * ey;
+          if (e2 * inv_s2 > 5.99) continue;
+        }
+      }
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= kThLow) {
+      fuse_idx[i] = bestIdx;
+      nFused++;
+    }
+  }
+  if (n_fused) *n_fused = nFused;
+  return SQLM_OK;
+}
+
+int orb_search_by_projection_kf(OrbEngine *e, sqlm_orb_frame *F, const float *Tcw, const sqlm_map_point *mps,
+                                const uint8_t *mp_desc, const float *kf_angle, int n, float th, int orb_dist,
+                                int check_ori, int *n_matches) {
+  if (!kf_frame_ok(F) || !F->slot_mp || !Tcw || n < 0 || (n && (!mps || !mp_desc || !kf_angle)))
+    return SQLM_ERR_INVALID_ARG;
+  if (n_matches) *n_matches = 0;
+  const ProjPose P(Tcw);
+  const float t[3] = {P.T[3], P.T[7], P.T[11]};
+  const float log_scale = std::log(F->scale_factors[1]);
+  std::vector<float4> hq(n);
+  for (int i = 0; i < n; ++i) {  // :1932-1968
+    hq[i] = area_query(0.f, 0.f, 0.f, kAreaSkip);
+    const sqlm_map_point &p = mps[i];
+    if (p.skip) continue;
+    const float X[3] = {p.x, p.y, p.z};
+    float Xc[3];
+    mat3_mul_add(P.T, false, X, t, 1.0, Xc);
+    const float xc = Xc[0], yc = Xc[1];
+    const float invzc = (float)(1.0 / (double)Xc[2]);
+    const float u = F->fx * xc * invzc + F->cx, v = F->fy * yc * invzc + F->cy;
+    if (u < F->bounds.min_x || u > F->bounds.max_x) continue;
+    if (v < F->bounds.min_y || v > F->bounds.max_y) continue;
+    const float PO[3] = {X[0] - P.Ow[0], X[1] - P.Ow[1], X[2] - P.Ow[2]};
+    const float dist3D = norm3(PO);
+    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    const int pl = predict_scale(p.max_dist, dist3D, log_scale, F->n_levels);
+    hq[i] = area_query(u, v, th * F->scale_factors[pl], area_levels(pl - 1, pl + 1));
+  }
+  std::vector<int> hoff;
+  std::vector<int2> hp;
+  if (int rc = area_search(e, F->kps, F->desc, F->n, &F->bounds, hq, mp_desc, hoff, hp)) return rc;
+  int nmatches = 0, hist[kHistoLength] = {0};
+  std::vector<int> rot_bin, rot_idx;
+  const float factor = kHistoLength / 360.0f;
+  for (int i = 0; i < n; ++i) {  // :1975-2013
+    int bestDist = 256, bestIdx2 = -1;
+    for (int q = hoff[i]; q < hoff[i + 1]; ++q) {
+      const int i2 = hp[q].x, dist = hp[q].y;
+      if (F->slot_mp[i2] >= 0) continue;
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = i2;
+      }
+    }
+    if (bestDist <= orb_dist) {
+      F->slot_mp[bestIdx2] = mps[i].id;
+      nmatches++;
+      if (check_ori) {
+        float rot = kf_angle[i] - F->kps[bestIdx2].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == kHistoLength) bin = 0;
+        rot_bin.push_back(bin);
+        rot_idx.push_back(bestIdx2);
+        hist[bin]++;
+      }
+    }
+  }
+  if (check_ori) {  // :2017-2039
+    int ind1, ind2, ind3;
+    three_maxima(hist, ind1, ind2, ind3);
+    for (int b = 0; b < kHistoLength; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (size_t q = 0; q < rot_bin.size(); ++q)
+        if (rot_bin[q] == b) {
+          F->slot_mp[rot_idx[q]] = -1;
+          nmatches--;
+        }
+    }
+  }
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+// ---- BoW searches (ORBmatcher.cc:246, :731, :887) ----
+// One query per side-1 feature of every common FeatureVector node, in the
+// reference's visiting order (common nodes ascending — the lower_bound merge
+// of :280-382 — then the node's features in index order); its candidates are
+// the node's side-2 run. The GPU fills every (query, candidate) distance; the
+// order-dependent acceptance replays the visit on the host.
+struct BowPlan {
+  std::vector<int4> q;    // (side-1 feature, run begin, run end, distance offset)
+  std::vector<int> cand;  // side-2 features, node-sorted
+  std::vector<int> dist;
+};
+
+static bool bow_ok(const sqlm_bow_frame *K) {
+  return K && K->n >= 0 && (K->n == 0 || (K->kps && K->desc && K->node && K->mp));
+}
+
+static std::vector<int> node_sorted(const sqlm_bow_frame *K) {
+  std::vector<int> v;
+  v.reserve(K->n);
+  for (int i = 0; i < K->n; ++i)
+    if (K->node[i] >= 0) v.push_back(i);
+  std::stable_sort(v.begin(), v.end(), [K](int a, int b) { return K->node[a] < K->node[b]; });
+  return v;
+}
+
+static int bow_plan(OrbEngine *e, const sqlm_bow_frame *K1, const sqlm_bow_frame *K2, BowPlan &B) {
+  const std::vector<int> v1 = node_sorted(K1);
+  B.cand = node_sorted(K2);
+  const std::vector<int> &v2 = B.cand;
+  B.q.clear();
+  int total = 0;
+  size_t a = 0, b = 0;
+  while (a < v1.size() && b < v2.size()) {
+    const int na = K1->node[v1[a]], nb = K2->node[v2[b]];
+    if (na == nb) {
+      size_t ea = a, eb = b;
+      while (ea < v1.size() && K1->node[v1[ea]] == na) ea++;
+      while (eb < v2.size() && K2->node[v2[eb]] == nb) eb++;
+      for (size_t i = a; i < ea; ++i) {
+        B.q.push_back(make_int4(v1[i], (int)b, (int)eb, total));
+        total += (int)(eb - b);
+      }
+      a = ea;
+      b = eb;
+    } else if (na < nb) {
+      while (a < v1.size() && K1->node[v1[a]] < nb) a++;
+    } else {
+      while (b < v2.size() && K2->node[v2[b]] < na) b++;
+    }
+  }
+  B.dist.assign(std::max(total, 1), 0);
+  const int nq = (int)B.q.size();
+  if (nq == 0 || total == 0) return SQLM_OK;
+  int4 *dq = e->get<int4>(e->q, nq);
+  uint32_t *dd1 = e->get<uint32_t>(e->qd, (size_t)8 * K1->n);
+  uint32_t *dd2 = e->get<uint32_t>(e->td, (size_t)8 * K2->n);
+  int *dc = e->get<int>(e->gidx, B.cand.size()), *dd = e->get<int>(e->pairs, total);
+  if (!dq || !dd1 || !dd2 || !dc || !dd) return SQLM_ERR_OOM;
+  if (hipMemcpyAsync(dq, B.q.data(), sizeof(int4) * nq, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(dd1, K1->desc, (size_t)32 * K1->n, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(dd2, K2->desc, (size_t)32 * K2->n, hipMemcpyHostToDevice, e->st) != hipSuccess ||
+      hipMemcpyAsync(dc, B.cand.data(), sizeof(int) * B.cand.size(), hipMemcpyHostToDevice, e->st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  hipLaunchKernelGGL(k_cand_dist, dim3((nq + 3) / 4), dim3(256), 0, e->st, dq, nq, dd1, dd2, dc, dd);
+  if (hipMemcpyAsync(B.dist.data(), dd, sizeof(int) * total, hipMemcpyDeviceToHost, e->st) != hipSuccess ||
+      hipStreamSynchronize(e->st) != hipSuccess)
+    return SQLM_ERR_HIP;
+  return SQLM_OK;
+}
+
+struct RotHist {
+  int hist[kHistoLength] = {0};
+  std::vector<int> bin, idx;
+  void push(float a1, float a2, int i) {
+    const float factor = kHistoLength / 360.0f;
+    float rot = a1 - a2;
+    if (rot < 0.0) rot += 360.0f;
+    int b = (int)std::round(rot * factor);
+    if (b == kHistoLength) b = 0;
+    bin.push_back(b);
+    idx.push_back(i);
+    hist[b]++;
+  }
+  // every entry of a rejected bin, bin by bin
+  template <class F>
+  void reject(int &nmatches, F clear) {
+    int ind1, ind2, ind3;
+    three_maxima(hist, ind1, ind2, ind3);
+    for (int b = 0; b < kHistoLength; b++) {
+      if (b == ind1 || b == ind2 || b == ind3) continue;
+      for (size_t q = 0; q < bin.size(); ++q)
+        if (bin[q] == b) {
+          clear(idx[q]);
+          nmatches--;
+        }
+    }
+  }
+};
+
+int orb_search_by_bow_kf_frame(OrbEngine *e, const sqlm_bow_frame *KF, const sqlm_bow_frame *F, float nnratio,
+                               int check_ori, int32_t *matches, int *n_matches) {
+  if (!bow_ok(KF) || !bow_ok(F) || (F->n && !matches)) return SQLM_ERR_INVALID_ARG;
+  for (int i = 0; i < F->n; ++i) matches[i] = -1;
+  if (n_matches) *n_matches = 0;
+  BowPlan B;
+  if (int rc = bow_plan(e, KF, F, B)) return rc;
+  int nmatches = 0;
+  RotHist R;
+  for (const int4 &Q : B.q) {  // :296-362
+    const int realIdxKF = Q.x;
+    if (KF->mp[realIdxKF] < 0 || (KF->mp_bad && KF->mp_bad[realIdxKF])) continue;
+    int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+    for (int j = Q.y; j < Q.z; ++j) {
+      const int realIdxF = B.cand[j];
+      if (matches[realIdxF] >= 0) continue;
+      const int dist = B.dist[Q.w + j - Q.y];
+      if (dist < bestDist1) {
+        bestDist2 = bestDist1;
+        bestDist1 = dist;
+        bestIdxF = realIdxF;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist1 <= kThLow && (float)bestDist1 < nnratio * (float)bestDist2) {
+      matches[bestIdxF] = KF->mp[realIdxKF];
+      if (check_ori) R.push(KF->kps[realIdxKF].angle, F->kps[bestIdxF].angle, bestIdxF);
+      nmatches++;
+    }
+  }
+  if (check_ori) R.reject(nmatches, [&](int i) { matches[i] = -1; });
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+int orb_search_by_bow_kf_kf(OrbEngine *e, const sqlm_bow_frame *K1, const sqlm_bow_frame *K2, float nnratio,
+                            int check_ori, int32_t *matches12, int *n_matches) {
+  if (!bow_ok(K1) || !bow_ok(K2) || (K1->n && !matches12)) return SQLM_ERR_INVALID_ARG;
+  for (int i = 0; i < K1->n; ++i) matches12[i] = -1;
+  if (n_matches) *n_matches = 0;
+  BowPlan B;
+  if (int rc = bow_plan(e, K1, K2, B)) return rc;
+  std::vector<uint8_t> matched2(K2->n, 0);
+  int nmatches = 0;
+  RotHist R;
+  for (const int4 &Q : B.q) {  // :775-845
+    const int idx1 = Q.x;
+    if (K1->mp[idx1] < 0 || (K1->mp_bad && K1->mp_bad[idx1])) continue;
+    int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+    for (int j = Q.y; j < Q.z; ++j) {
+      const int idx2 = B.cand[j];
+      if (matched2[idx2] || K2->mp[idx2] < 0 || (K2->mp_bad && K2->mp_bad[idx2])) continue;
+      const int dist = B.dist[Q.w + j - Q.y];
+      if (dist < bestDist1) {
+        bestDist2 = bestDist1;
+        bestDist1 = dist;
+        bestIdx2 = idx2;
+      } else if (dist < bestDist2) {
+        bestDist2 = dist;
+      }
+    }
+    if (bestDist1 < kThLow && (float)bestDist1 < nnratio * (float)bestDist2) {
+      matches12[idx1] = K2->mp[bestIdx2];
+      matched2[bestIdx2] = 1;
+      if (check_ori) R.push(K1->kps[idx1].angle, K2->kps[bestIdx2].angle, idx1);
+      nmatches++;
+    }
+  }
+  if (check_ori) R.reject(nmatches, [&](int i) { matches12[i] = -1; });
+  if (n_matches) *n_matches = nmatches;
+  return SQLM_OK;
+}
+
+int orb_search_for_triangulation(OrbEngine *e, const sqlm_bow_frame *K1, const sqlm_bow_frame *K2, const float *C1,
+                                 const float *T2w, const float *cam2, const float *sf2, int n_levels2, const float *F12,
+                                 int only_stereo, int check_ori, int32_t *m12, int *n_matches) {
+  if (!bow_ok(K1) || !bow_ok(K2) || !C1 || !T2w || !cam2 || !sf2 || n_levels2 < 1 || !F12 || (K1->n && !m12))
+    return SQLM_ERR_INVALID_ARG;
+  for (int i = 0; i < K2->n; ++i)
+    if (K2->kps[i].octave < 0 || K2->kps[i].octave >= n_levels2) return SQLM_ERR_INVALID_ARG;
+  for (int i = 0; i < K1->n; ++i) m12[i] = -1;
+  if (n_matches) *n_matches = 0;
+  // epipole of pKF1's centre in pKF2 (:903-913)
+  const float t2[3] = {T2w[3], T2w[7], T2w[11]};
+  float C2[3];
+  mat3_mul_add(T2w, false, C1, t2, 1.0, C2);
+  const float invz = 1.0f / C2[2];
+  const float ex = cam2[0] * C2[0] * invz + cam2[2], ey = cam2[1] * C2[1] * invz + cam2[3];
+  BowPlan B;
+  if (int rc = bow_plan(e, K1, K2, B)) return rc;
+  std::vector<uint8_t> matched2(K2->n, 0);
+  int nmatches = 0;
+  RotHist R;
+  for (const int4 &Q : B.q) {  // :936-1030
+    const int idx1 = Q.x;
+    if (K1->mp[idx1] >= 0) continue;
+    const bool bStereo1 = K1->uright && K1->uright[idx1] >= 0;
+    if (only_stereo && !bStereo1) continue;
+    const sqlm_keypoint &kp1 = K1->kps[idx1];
+    int bestDist = kThLow, bestIdx2 = -1;
+    for (int j = Q.y; j < Q.z; ++j) {
+      const int idx2 = B.cand[j];
+      if (matched2[idx2] || K2->mp[idx2] >= 0) continue;
+      const bool bStereo2 = K2->uright && K2->uright[idx2] >= 0;
+      if (only_stereo && !bStereo2) continue;
+      const int dist = B.dist[Q.w + j - Q.y];
+      if (dist > kThLow || dist > bestDist) continue;
+      const sqlm_keypoint &kp2 = K2->kps[idx2];
+      if (!bStereo1 && !bStereo2) {
+        const float distex = ex - kp2.x, distey = ey - kp2.y;
+        if (distex * distex + distey * distey < 100 * sf2[kp2.octave]) continue;
+      }
+      // CheckDistEpipolarLine (:203-229)
+      const float a = kp1.x * F12[0] + kp1.y * F12[3] + F12[6];
+      const float b = kp1.x * F12[1] + kp1.y * F12[4] + F12[7];
+      const float c = kp1.x * F12[2] + kp1.y * F12[5] + F12[8];
+      const float num = a * kp2.x + b * kp2.y + c;
+      const float den = a * a + b * b;
+      if (den == 0) continue;
+      const float dsqr = num * num / den;
+      if (dsqr < 3.84 * (sf2[kp2.octave] * sf2[kp2.octave])) {
+        bestIdx2 = idx2;
+        bestDist = dist;
+      }
+    }
+    if (bestIdx2 >= 0) {
+      m12[idx1] = bestIdx2;
+      matched2[bestIdx2] = 1;
+      nmatches++;
+      if (check_ori) R.push(kp1.angle, K2->kps[bestIdx2].angle, idx1);
+    }
+  }
+  if (check_ori)
+    R.reject(nmatches, [&](int i) {
+      matched2[m12[i]] = 0;
+      m12[i] = -1;
+    });
   if (n_matches) *n_matches = nmatches;
   return SQLM_OK;
 }

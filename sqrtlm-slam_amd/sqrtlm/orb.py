@@ -28,6 +28,12 @@ LAST_POINT_DTYPE = np.dtype([("id", "<i4"), ("x", "<f4"), ("y", "<f4"), ("z", "<
                              ("angle", "<f4"), ("outlier", "u1"), ("has_obs", "u1"), ("pad", "u1", (2,))])
 
 
+# a map point as the keyframe searches read it (sqlm_map_point)
+MAP_POINT_DTYPE = np.dtype([("id", "<i4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"),
+                            ("nz", "<f4"), ("min_dist", "<f4"), ("max_dist", "<f4"), ("skip", "u1"),
+                            ("pad", "u1", (3,))])
+
+
 class OrbParams(C.Structure):
     _fields_ = [("nfeatures", C.c_int32), ("scale_factor", C.c_float), ("nlevels", C.c_int32),
                 ("ini_th_fast", C.c_int32), ("min_th_fast", C.c_int32)]
@@ -94,6 +100,66 @@ class LastFrameSlots:
         self.mTcw = np.ascontiguousarray(np.asarray(mTcw, np.float32)[:3, :4])
         self.slots = np.ascontiguousarray(slots, LAST_POINT_DTYPE)
         self.descriptors = np.ascontiguousarray(descriptors, np.uint8).reshape(len(self.slots), 32)
+
+
+class KeyFrameSlots:
+    """pKF as SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist)
+    reads it: its map-point slots MAP_POINT_DTYPE [N] (skip set for NULL, bad
+    and already-found slots), their descriptors and mvKeysUn[i].angle."""
+
+    def __init__(self, slots, descriptors, angles):
+        self.slots = np.ascontiguousarray(slots, MAP_POINT_DTYPE)
+        self.descriptors = np.ascontiguousarray(descriptors, np.uint8).reshape(len(self.slots), 32)
+        self.angles = np.ascontiguousarray(angles, np.float32)
+
+
+class _BowFrame(C.Structure):
+    _fields_ = [("kps", C.c_void_p), ("desc", C.c_void_p), ("node", C.c_void_p), ("mp", C.c_void_p),
+                ("mp_bad", C.c_void_p), ("uright", C.c_void_p), ("n", C.c_int32)]
+
+
+def _f32_mat3_mul(R, x):
+    """cv::Mat 3x3 * 3x1 on CV_32F: float products summed left to right."""
+    f32 = np.float32
+    return [f32(f32(R[i][0]) * f32(x[0]) + f32(R[i][1]) * f32(x[1]) + f32(R[i][2]) * f32(x[2])) for i in range(3)]
+
+
+class BowFrame:
+    """A KeyFrame (keyframe=True) or Frame as the BoW searches read it:
+    mvKeysUn, mDescriptors, the DBoW2 FeatureVector as one node id per feature
+    (-1: not in mFeatVec), GetMapPointMatches() ids (-1: NULL) with isBad(),
+    mvuRight, and for SearchForTriangulation the pose Tcw (3x4), fx fy cx cy and
+    mvScaleFactors."""
+
+    def __init__(self, mvKeysUn, mDescriptors, node, mapPoints=None, mapPointBad=None, mvuRight=None,
+                 keyframe=True, Tcw=None, cam=None, mvScaleFactors=None):
+        self.mvKeysUn = np.ascontiguousarray(mvKeysUn, KP_DTYPE)
+        n = self.N = len(self.mvKeysUn)
+        self.mDescriptors = np.ascontiguousarray(mDescriptors, np.uint8).reshape(n, 32)
+        self.node = np.ascontiguousarray(node, np.int32)
+        self.mp = np.full(n, -1, np.int32) if mapPoints is None else np.ascontiguousarray(mapPoints, np.int32)
+        self.mp_bad = None if mapPointBad is None else np.ascontiguousarray(mapPointBad, np.uint8)
+        self.mvuRight = None if mvuRight is None else np.ascontiguousarray(mvuRight, np.float32)
+        for a in (self.node, self.mp, self.mp_bad, self.mvuRight):
+            if a is not None and a.shape != (n,):
+                raise ValueError("per-feature arrays must hold one entry per keypoint")
+        self.keyframe = bool(keyframe)
+        self.Tcw = None if Tcw is None else np.ascontiguousarray(np.asarray(Tcw, np.float32)[:3, :4])
+        self.cam = None if cam is None else np.ascontiguousarray(cam, np.float32)[:4]
+        self.mvScaleFactors = None if mvScaleFactors is None else np.ascontiguousarray(mvScaleFactors, np.float32)
+
+    def GetCameraCenter(self):
+        """Ow = -R^T t (KeyFrame::SetPose), float as cv::Mat computes it."""
+        t = self.Tcw[:, 3]
+        return np.array([-v for v in _f32_mat3_mul(self.Tcw[:, :3].T, t)], np.float32)
+
+    def _struct(self) -> _BowFrame:
+        b = _BowFrame()
+        b.kps, b.desc, b.node, b.mp = (a.ctypes.data for a in (self.mvKeysUn, self.mDescriptors, self.node, self.mp))
+        b.mp_bad = None if self.mp_bad is None else self.mp_bad.ctypes.data
+        b.uright = None if self.mvuRight is None else self.mvuRight.ctypes.data
+        b.n = self.N
+        return b
 
 
 class ORBextractor:
@@ -222,15 +288,19 @@ class ORBmatcher:
         return n.value, m12
 
     def SearchByProjection(self, F: Frame, second, *args):
-        """The projection searches on the GPU candidate windows:
+        """The projection searches on the GPU candidate windows (F.mvpMapPoints
+        / F.slot_obs updated in place; returns nmatches):
 
         - ``SearchByProjection(F, vpMapPoints, descriptors, th=1.0)``
           (ORBmatcher.cc:67-181): vpMapPoints TRACK_POINT_DTYPE [n] as
           Tracking::SearchLocalPoints leaves them, descriptors [n, 32];
         - ``SearchByProjection(CurrentFrame, LastFrame, th, bMono)``
-          (ORBmatcher.cc:1717-1883): LastFrame a LastFrameSlots, CurrentFrame.mTcw set.
-
-        F.mvpMapPoints / F.slot_obs are updated in place; returns nmatches."""
+          (ORBmatcher.cc:1717-1883): LastFrame a LastFrameSlots, CurrentFrame.mTcw set;
+        - ``SearchByProjection(pKF, Scw, vpPoints, descriptors, th)``
+          (ORBmatcher.cc:423-571): vpMatched = pKF.mvpMapPoints, vpPoints
+          MAP_POINT_DTYPE (skip = isBad() or already in vpMatched);
+        - ``SearchByProjection(CurrentFrame, pKF, th, ORBdist)``
+          (ORBmatcher.cc:1902-2046): pKF a KeyFrameSlots, CurrentFrame.mTcw set."""
         n = C.c_int(0)
         fs = F._struct()
         if isinstance(second, LastFrameSlots):
@@ -245,6 +315,28 @@ class ORBmatcher:
                 C.c_float(th), int(bool(bMono)), int(self.mbCheckOrientation), C.byref(n)),
                 "sqlm_orb_search_by_projection_last")
             return n.value
+        if isinstance(second, KeyFrameSlots):
+            if len(args) != 2:
+                raise TypeError("SearchByProjection(CurrentFrame, pKF, th, ORBdist)")
+            if F.mTcw is None:
+                raise ValueError("CurrentFrame.mTcw is not set")
+            th, orb_dist = args
+            K = second
+            check(lib().sqlm_orb_search_by_projection_kf(
+                self.ctx._h, C.byref(fs), ptr(F.mTcw), ptr(K.slots), ptr(K.descriptors), ptr(K.angles), len(K.slots),
+                C.c_float(th), int(orb_dist), int(self.mbCheckOrientation), C.byref(n)),
+                "sqlm_orb_search_by_projection_kf")
+            return n.value
+        if isinstance(second, np.ndarray) and second.dtype.kind == "f" and second.shape in ((3, 4), (4, 4)):
+            if len(args) != 3:
+                raise TypeError("SearchByProjection(pKF, Scw, vpPoints, descriptors, th)")
+            Scw = np.ascontiguousarray(second[:3, :4], np.float32)
+            pts = np.ascontiguousarray(args[0], MAP_POINT_DTYPE)
+            desc = np.ascontiguousarray(args[1], np.uint8).reshape(len(pts), 32)
+            check(lib().sqlm_orb_search_by_projection_sim3(self.ctx._h, C.byref(fs), ptr(Scw), ptr(pts), ptr(desc),
+                                                           len(pts), int(args[2]), C.byref(n)),
+                  "sqlm_orb_search_by_projection_sim3")
+            return n.value
         if len(args) not in (1, 2):
             raise TypeError("SearchByProjection(F, vpMapPoints, descriptors, th=1.0)")
         third, th = args[0], (args[1] if len(args) == 2 else 1.0)
@@ -254,3 +346,66 @@ class ORBmatcher:
                                                         C.c_float(th), C.c_float(self.mfNNratio), C.byref(n)),
               "sqlm_orb_search_by_projection_local")
         return n.value
+
+    def Fuse(self, pKF: Frame, *args):
+        """Fuse(pKF, vpMapPoints, descriptors, th=3.0) (ORBmatcher.cc:1109-1294,
+        pKF.mTcw set) or Fuse(pKF, Scw, vpPoints, descriptors, th)
+        (:1296-1446). Points MAP_POINT_DTYPE (skip = isBad() or already in
+        pKF). Returns (nFused, fuse_idx): the keypoint each point fuses into
+        (-1: none); MapPoint::Replace / AddObservation are the caller's."""
+        if args and isinstance(args[0], np.ndarray) and args[0].dtype.kind == "f" and args[0].shape in ((3, 4),
+                                                                                                       (4, 4)):
+            T, sim3, rest = np.ascontiguousarray(args[0][:3, :4], np.float32), 1, args[1:]
+            if len(rest) != 3:
+                raise TypeError("Fuse(pKF, Scw, vpPoints, descriptors, th)")
+        else:
+            if pKF.mTcw is None:
+                raise ValueError("pKF.mTcw is not set")
+            T, sim3, rest = pKF.mTcw, 0, args
+            if len(rest) == 2:
+                rest = (*rest, 3.0)
+            if len(rest) != 3:
+                raise TypeError("Fuse(pKF, vpMapPoints, descriptors, th=3.0)")
+        pts = np.ascontiguousarray(rest[0], MAP_POINT_DTYPE)
+        desc = np.ascontiguousarray(rest[1], np.uint8).reshape(len(pts), 32)
+        idx = np.zeros(len(pts), np.int32)
+        n = C.c_int(0)
+        fs = pKF._struct()
+        check(lib().sqlm_orb_fuse(self.ctx._h, C.byref(fs), ptr(T), int(sim3), ptr(pts), ptr(desc), len(pts),
+                                  C.c_float(rest[2]), ptr(idx), C.byref(n)), "sqlm_orb_fuse")
+        return n.value, idx
+
+    def SearchByBoW(self, pKF: BowFrame, second: BowFrame):
+        """SearchByBoW(pKF, F) (ORBmatcher.cc:246-403; second.keyframe False):
+        (nmatches, vpMapPointMatches [F.N] ids); SearchByBoW(pKF1, pKF2)
+        (:731-869): (nmatches, vpMatches12 [pKF1.N] ids of pKF2's points)."""
+        n = C.c_int(0)
+        a, b = pKF._struct(), second._struct()
+        if second.keyframe:
+            out = np.zeros(pKF.N, np.int32)
+            check(lib().sqlm_orb_search_by_bow_kf_kf(self.ctx._h, C.byref(a), C.byref(b), C.c_float(self.mfNNratio),
+                                                     int(self.mbCheckOrientation), ptr(out), C.byref(n)),
+                  "sqlm_orb_search_by_bow_kf_kf")
+        else:
+            out = np.zeros(second.N, np.int32)
+            check(lib().sqlm_orb_search_by_bow_kf_frame(self.ctx._h, C.byref(a), C.byref(b),
+                                                        C.c_float(self.mfNNratio), int(self.mbCheckOrientation),
+                                                        ptr(out), C.byref(n)), "sqlm_orb_search_by_bow_kf_frame")
+        return n.value, out
+
+    def SearchForTriangulation(self, pKF1: BowFrame, pKF2: BowFrame, F12, bOnlyStereo: bool):
+        """SearchForTriangulation(pKF1, pKF2, F12, vMatchedPairs, bOnlyStereo)
+        (ORBmatcher.cc:887-1096) -> (nmatches, vMatchedPairs as [(i1, i2)])."""
+        if pKF1.Tcw is None or pKF2.Tcw is None or pKF2.cam is None or pKF2.mvScaleFactors is None:
+            raise ValueError("pKF1.Tcw, pKF2.Tcw, pKF2.cam and pKF2.mvScaleFactors are required")
+        F = np.ascontiguousarray(F12, np.float32).reshape(3, 3)
+        C1 = pKF1.GetCameraCenter()
+        m12 = np.zeros(pKF1.N, np.int32)
+        n = C.c_int(0)
+        a, b = pKF1._struct(), pKF2._struct()
+        check(lib().sqlm_orb_search_for_triangulation(
+            self.ctx._h, C.byref(a), C.byref(b), ptr(C1), ptr(pKF2.Tcw), ptr(pKF2.cam), ptr(pKF2.mvScaleFactors),
+            len(pKF2.mvScaleFactors), ptr(F), int(bool(bOnlyStereo)), int(self.mbCheckOrientation), ptr(m12),
+            C.byref(n)), "sqlm_orb_search_for_triangulation")
+        i1 = np.nonzero(m12 >= 0)[0]
+        return n.value, [(int(i), int(m12[i])) for i in i1]

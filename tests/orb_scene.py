@@ -110,3 +110,75 @@ def last_frame(k1, d1, shift, w, h, seed, tz=0.0):
     Tlw = np.zeros((3, 4), np.float32)
     Tlw[:, :3] = np.eye(3)
     return Tcw, Tlw, lp, np.ascontiguousarray(d1)
+
+
+MAP_POINT_DTYPE = np.dtype([("id", "<i4"), ("x", "<f4"), ("y", "<f4"), ("z", "<f4"), ("nx", "<f4"), ("ny", "<f4"),
+                            ("nz", "<f4"), ("min_dist", "<f4"), ("max_dist", "<f4"), ("skip", "u1"),
+                            ("pad", "u1", (3,))])
+
+
+def keyframe_pose(shift, w, h, t=(0.0, 0.0, 0.0)):
+    """3x4 Tcw of a keyframe that sees frame-1 content about `shift` pixels on."""
+    R = _rot(-shift[1] / FY, shift[0] / FX)
+    T = np.zeros((3, 4), np.float32)
+    T[:, :3] = R
+    T[:, 3] = t
+    return T
+
+
+def sim3_of(T, s):
+    """Scw = [sR | s t] of a 3x4 Tcw."""
+    return (np.asarray(T, np.float64) * s).astype(np.float32)
+
+
+def map_points(k1, d1, w, h, seed, n_levels=8):
+    """(MAP_POINT_DTYPE [n], descriptors): frame-1 keypoints back-projected at
+    random depths from the origin, normals along the viewing ray (noisy),
+    mfMaxDistance = dist * scale[octave], mfMinDistance = max / scale[n-1]
+    (MapPoint ctor, MapPoint.cc:95-106); a few skipped (bad / already found)."""
+    rng = np.random.default_rng(seed + 31)
+    n = len(k1)
+    fx, fy, cx, cy, _, _ = camera(w, h)
+    z = rng.uniform(3.0, 40.0, n)
+    X = np.stack([(k1["x"] - cx) / fx * z, (k1["y"] - cy) / fy * z, z], 1)
+    dist = np.linalg.norm(X, axis=1)
+    nrm = X / dist[:, None] + rng.normal(0, 0.2, (n, 3))
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    sf = scale_factors(n_levels)
+    mp = np.zeros(n, MAP_POINT_DTYPE)
+    mp["id"] = np.arange(n) + 7000
+    mp["x"], mp["y"], mp["z"] = X[:, 0], X[:, 1], X[:, 2]
+    mp["nx"], mp["ny"], mp["nz"] = nrm[:, 0], nrm[:, 1], nrm[:, 2]
+    mx = (dist * sf[np.clip(k1["octave"], 0, n_levels - 1)]).astype(np.float32)
+    mp["max_dist"] = mx
+    mp["min_dist"] = (mx / sf[-1]).astype(np.float32)
+    mp["skip"] = rng.random(n) < 0.05
+    return mp, np.ascontiguousarray(d1)
+
+
+def bow_nodes(desc, seed, absent=0.08):
+    """A stand-in DBoW2 FeatureVector: the node of a feature from its first
+    descriptor byte (similar descriptors share nodes), some features absent."""
+    rng = np.random.default_rng(seed + 57)
+    node = (desc[:, 0].astype(np.int32) >> 3) * 37 + 1000
+    node[rng.random(len(desc)) < absent] = -1
+    return node
+
+
+def bow_points(n, seed, frac=0.7, bad=0.05, base=0):
+    """GetMapPointMatches ids (-1: NULL) and isBad() flags."""
+    rng = np.random.default_rng(seed + 91)
+    mp = np.where(rng.random(n) < frac, np.arange(n) + base, -1).astype(np.int32)
+    return mp, (rng.random(n) < bad).astype(np.uint8)
+
+
+def fundamental_12(T1w, T2w, cam1, cam2):
+    """F12 (ComputeF12, LocalMapping.cc): K1^-T [t12]x R12 K2^-1 from 3x4 poses (float32)."""
+    def K(c):
+        return np.array([[c[0], 0, c[2]], [0, c[1], c[3]], [0, 0, 1.0]])
+    R1, t1 = np.asarray(T1w[:, :3], np.float64), np.asarray(T1w[:, 3], np.float64)
+    R2, t2 = np.asarray(T2w[:, :3], np.float64), np.asarray(T2w[:, 3], np.float64)
+    R12 = R1 @ R2.T
+    t12 = -R1 @ R2.T @ t2 + t1
+    tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
+    return (np.linalg.inv(K(cam1)).T @ tx @ R12 @ np.linalg.inv(K(cam2))).astype(np.float32)

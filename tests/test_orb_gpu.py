@@ -199,3 +199,114 @@ def test_search_by_projection_edge_cases(gpu_ctx, orb_oracle, kitti_pair):
     F2 = _gpu_frame(k2, d2, bounds, None, sm, so, Tcw=np.eye(4)[:3])  # identity motion: the old positions
     assert m.SearchByProjection(F2, LastFrameSlots(Tlw, lp, ld), 7.0, True) == n_r
     np.testing.assert_array_equal(F2.mvpMapPoints, m_r)
+
+
+# ---- keyframe projection searches (ORBmatcher.cc:423, :1109, :1296, :1902) ----
+@pytest.mark.parametrize("s,th", [(1.0, 10), (1.3, 10), (0.8, 4)])
+def test_search_by_projection_sim3(gpu_ctx, orb_oracle, kitti_pair, s, th):
+    import orb_scene as S
+    from sqrtlm.orb import ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    cam = S.camera(1241, 376)
+    mps, md = S.map_points(k1, d1, 1241, 376, seed=3)
+    Scw = S.sim3_of(S.keyframe_pose((9.0, 2.0), 1241, 376, (0.02, 0.0, 0.1)), s)
+    _, sm, so = S.current_slots(k2, 3, False)
+    n_r, m_r = orb_oracle.search_by_projection_sim3(k2, d2, bounds, S.scale_factors(), cam, sm, Scw, mps, md, th)
+    F = _gpu_frame(k2, d2, bounds, None, sm, so)
+    n_g = ORBmatcher(0.75, ctx=gpu_ctx).SearchByProjection(F, Scw, mps, md, th)
+    assert n_g == n_r and n_r > 100
+    np.testing.assert_array_equal(F.mvpMapPoints, m_r)
+
+
+@pytest.mark.parametrize("sim3,stereo,th", [(False, False, 3.0), (False, True, 5.0), (True, False, 4.0)])
+def test_fuse(gpu_ctx, orb_oracle, kitti_pair, sim3, stereo, th):
+    import orb_scene as S
+    from sqrtlm.orb import ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    cam = S.camera(1241, 376)
+    mps, md = S.map_points(k1, d1, 1241, 376, seed=4)
+    T = S.keyframe_pose((9.0, 2.0), 1241, 376, (0.0, 0.01, 0.05))
+    ur, sm, so = S.current_slots(k2, 4, stereo)
+    Tq = S.sim3_of(T, 1.2) if sim3 else T
+    n_r, idx_r = orb_oracle.fuse(k2, d2, bounds, S.scale_factors(), cam, ur, Tq, sim3, mps, md, th)
+    F = _gpu_frame(k2, d2, bounds, ur, sm, so, Tcw=T)
+    m = ORBmatcher(0.6, ctx=gpu_ctx)
+    n_g, idx_g = m.Fuse(F, Tq, mps, md, th) if sim3 else m.Fuse(F, mps, md, th)
+    assert n_g == n_r and n_r > 50
+    np.testing.assert_array_equal(idx_g, idx_r)
+
+
+@pytest.mark.parametrize("th,orb_dist,check_ori", [(10.0, 100, True), (3.0, 64, False)])
+def test_search_by_projection_kf(gpu_ctx, orb_oracle, kitti_pair, th, orb_dist, check_ori):
+    import orb_scene as S
+    from sqrtlm.orb import KeyFrameSlots, ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    cam = S.camera(1241, 376)
+    mps, md = S.map_points(k1, d1, 1241, 376, seed=5)
+    Tcw = S.keyframe_pose((9.0, 2.0), 1241, 376, (0.01, 0.0, -0.1))
+    _, sm, so = S.current_slots(k2, 5, False)
+    n_r, m_r = orb_oracle.search_by_projection_kf(k2, d2, bounds, S.scale_factors(), cam, sm, Tcw, mps, md,
+                                                  k1["angle"], th, orb_dist, check_ori)
+    F = _gpu_frame(k2, d2, bounds, None, sm, so, Tcw=Tcw)
+    n_g = ORBmatcher(0.75, check_ori, ctx=gpu_ctx).SearchByProjection(F, KeyFrameSlots(mps, md, k1["angle"]), th,
+                                                                      orb_dist)
+    assert n_g == n_r and n_r > 100
+    np.testing.assert_array_equal(F.mvpMapPoints, m_r)
+
+
+# ---- BoW searches (ORBmatcher.cc:246, :731, :887) ----
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_by_bow(gpu_ctx, orb_oracle, kitti_pair, check_ori):
+    import orb_scene as S
+    from sqrtlm.orb import BowFrame, ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    n1, n2 = S.bow_nodes(d1, 1), S.bow_nodes(d2, 2)
+    mp1, bad1 = S.bow_points(len(k1), 1)
+    mp2, bad2 = S.bow_points(len(k2), 2, base=10000)
+    a = (k1, d1, n1, mp1, bad1)
+    n_r, out_r = orb_oracle.search_by_bow_kf_frame(a, (k2, d2, n2, mp2), 0.7, check_ori)
+    KF = BowFrame(k1, d1, n1, mp1, bad1)
+    n_g, out_g = ORBmatcher(0.7, check_ori, ctx=gpu_ctx).SearchByBoW(KF, BowFrame(k2, d2, n2, keyframe=False))
+    assert n_g == n_r and n_r > 100
+    np.testing.assert_array_equal(out_g, out_r)
+    n_r, out_r = orb_oracle.search_by_bow_kf_kf(a, (k2, d2, n2, mp2, bad2), 0.75, check_ori)
+    n_g, out_g = ORBmatcher(0.75, check_ori, ctx=gpu_ctx).SearchByBoW(KF, BowFrame(k2, d2, n2, mp2, bad2))
+    assert n_g == n_r and n_r > 100
+    np.testing.assert_array_equal(out_g, out_r)
+
+
+@pytest.mark.parametrize("stereo,only_stereo,check_ori", [(False, False, False), (True, False, True),
+                                                          (True, True, False)])
+def test_search_for_triangulation(gpu_ctx, orb_oracle, kitti_pair, stereo, only_stereo, check_ori):
+    import orb_scene as S
+    from sqrtlm.orb import BowFrame, ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    cam = S.camera(1241, 376)
+    T1 = S.keyframe_pose((0.0, 0.0), 1241, 376)
+    T2 = S.keyframe_pose((9.0, 2.0), 1241, 376, (0.3, 0.0, 0.05))
+    F12 = S.fundamental_12(T1, T2, cam, cam)
+    n1, n2 = S.bow_nodes(d1, 5), S.bow_nodes(d2, 6)
+    mp1, _ = S.bow_points(len(k1), 5, frac=0.3)
+    mp2, _ = S.bow_points(len(k2), 6, frac=0.3)
+    ur1, _, _ = S.current_slots(k1, 5, stereo)
+    ur2, _, _ = S.current_slots(k2, 6, stereo)
+    sf = S.scale_factors()
+    K1 = BowFrame(k1, d1, n1, mp1, None, ur1, Tcw=T1, cam=cam[:4], mvScaleFactors=sf)
+    K2 = BowFrame(k2, d2, n2, mp2, None, ur2, Tcw=T2, cam=cam[:4], mvScaleFactors=sf)
+    n_r, m_r = orb_oracle.search_for_triangulation((k1, d1, n1, mp1, None, ur1), (k2, d2, n2, mp2, None, ur2),
+                                                   K1.GetCameraCenter(), T2, cam[:4], sf, F12, only_stereo, check_ori)
+    n_g, pairs = ORBmatcher(0.6, check_ori, ctx=gpu_ctx).SearchForTriangulation(K1, K2, F12, only_stereo)
+    assert n_g == n_r and n_r > 10
+    assert pairs == [(int(i), int(m_r[i])) for i in np.nonzero(m_r >= 0)[0]]
+
+
+def test_bow_edge_cases(gpu_ctx, kitti_pair):
+    from sqrtlm.orb import BowFrame, ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    m = ORBmatcher(0.7, True, ctx=gpu_ctx)
+    none = np.full(len(k1), -1, np.int32)
+    n, out = m.SearchByBoW(BowFrame(k1, d1, none, np.arange(len(k1))), BowFrame(k2, d2, np.zeros(len(k2)),
+                                                                                keyframe=False))
+    assert n == 0 and (out == -1).all()  # no feature in the vocabulary: no common node
+    n, out = m.SearchByBoW(BowFrame(k1[:0], d1[:0], none[:0]), BowFrame(k2, d2, np.zeros(len(k2))))
+    assert n == 0 and len(out) == 0

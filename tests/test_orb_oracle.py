@@ -10,6 +10,7 @@ implements itself (IC_Angle, steered BRIEF, Hamming distance, quadtree,
 SearchForInitialization) are checked against direct numpy / Python
 transliterations of the reference source, and the whole extractor output is
 frozen in tests/golden/orb/orb_golden.npz."""
+import math
 import os
 
 import numpy as np
@@ -531,3 +532,410 @@ def test_search_by_projection_last_matches_transliteration(OB, proj_scene, stere
     assert n == n_py and n > 20
     np.testing.assert_array_equal(m, m_py)
     np.testing.assert_array_equal(o, o_py)
+
+
+# ---- keyframe projection and BoW searches vs pure-Python transliterations ----
+def _f32_mul_add(A, x, c, sign=1.0):
+    f32 = np.float32
+    out = []
+    for i in range(3):
+        t0 = f32(A[i][0]) * f32(x[0]) + f32(A[i][1]) * f32(x[1]) + f32(A[i][2]) * f32(x[2])
+        out.append(f32(float(t0) * sign + (float(c[i]) if c is not None else 0.0)))
+    return out
+
+
+def _py_pose(T, sim3):
+    f32 = np.float32
+    T = np.asarray(T, f32)[:3, :4]
+    if sim3:
+        s = f32(math.sqrt(sum(float(T[0, j]) * float(T[0, j]) for j in range(3))))
+        inv = f32(1.0 / float(s))
+        T = (T * inv).astype(f32)
+    Ow = _f32_mul_add(T[:, :3].T, T[:, 3], None, -1.0)
+    return T, Ow
+
+
+def _py_norm_dot(PO, Pn):
+    n = np.float32(math.sqrt(sum(float(v) * float(v) for v in PO)))
+    d = sum(float(a) * float(b) for a, b in zip(PO, Pn))
+    return n, d
+
+
+def _py_predict(max_dist, dist, sf):
+    f32 = np.float32
+    ratio = f32(max_dist) / f32(dist)
+    ls = f32(math.log(float(sf[1])))
+    v = f32(f32(math.log(float(ratio))) / ls)
+    s = math.ceil(float(v))
+    return 0 if s < 0 else min(s, len(sf) - 1)
+
+
+def _py_project_kf(T, Ow, p, cam, bounds, sf):
+    f32 = np.float32
+    X = (p["x"], p["y"], p["z"])
+    Xc = _f32_mul_add(T[:, :3], X, T[:, 3])
+    if Xc[2] < 0:
+        return None
+    invz = f32(1) / Xc[2]
+    u = f32(cam[0]) * (Xc[0] * invz) + f32(cam[2])
+    v = f32(cam[1]) * (Xc[1] * invz) + f32(cam[3])
+    if not (u >= f32(bounds[0]) and u < f32(bounds[1]) and v >= f32(bounds[2]) and v < f32(bounds[3])):
+        return None
+    PO = [f32(X[i]) - Ow[i] for i in range(3)]
+    dist, dot = _py_norm_dot(PO, (p["nx"], p["ny"], p["nz"]))
+    if dist < f32(1.2) * p["max_dist"] and dist >= f32(0.8) * p["min_dist"] and not dot < 0.5 * float(dist):
+        return u, v, invz, _py_predict(p["max_dist"], dist, sf)
+    return None
+
+
+def _py_sbp_sim3(kps, desc, bounds, sf, cam, slot_mp, Scw, mps, md, th):
+    T, Ow = _py_pose(Scw, True)
+    G = _py_grid(kps, bounds)
+    D = np.unpackbits(md[:, None, :] ^ desc[None, :, :], axis=2).sum(axis=2)
+    sm = slot_mp.copy()
+    n = 0
+    for i, p in enumerate(mps):
+        if p["skip"]:
+            continue
+        r = _py_project_kf(T, Ow, p, cam, bounds, sf)
+        if r is None:
+            continue
+        u, v, _, pl = r
+        bd, bi = 256, -1
+        for j in _py_area(G, kps, u, v, np.float32(th) * sf[pl], -1, -1):
+            if sm[j] >= 0 or kps["octave"][j] < pl - 1 or kps["octave"][j] > pl:
+                continue
+            if D[i, j] < bd:
+                bd, bi = int(D[i, j]), j
+        if bd <= 50:
+            sm[bi] = p["id"]
+            n += 1
+    return n, sm
+
+
+def _py_fuse(kps, desc, bounds, sf, cam, uright, T, sim3, mps, md, th):
+    f32 = np.float32
+    T, Ow = _py_pose(T, sim3)
+    G = _py_grid(kps, bounds)
+    D = np.unpackbits(md[:, None, :] ^ desc[None, :, :], axis=2).sum(axis=2)
+    out = np.full(len(mps), -1, np.int32)
+    n = 0
+    for i, p in enumerate(mps):
+        if p["skip"]:
+            continue
+        r = _py_project_kf(T, Ow, p, cam, bounds, sf)
+        if r is None:
+            continue
+        u, v, invz, pl = r
+        ur = u - f32(cam[4]) * invz
+        bd, bi = (2 ** 31 - 1) if sim3 else 256, -1
+        for j in _py_area(G, kps, u, v, f32(th) * sf[pl], -1, -1):
+            lv = int(kps["octave"][j])
+            if lv < pl - 1 or lv > pl:
+                continue
+            if not sim3:
+                inv = f32(1.0) / (sf[lv] * sf[lv])
+                ex, ey = u - kps["x"][j], v - kps["y"][j]
+                if uright is not None and uright[j] >= 0:
+                    er = ur - uright[j]
+                    if float((ex * ex + ey * ey + er * er) * inv) > 7.8:
+                        continue
+                elif float((ex * ex + ey * ey) * inv) > 5.99:
+                    continue
+            if D[i, j] < bd:
+                bd, bi = int(D[i, j]), j
+        if bd <= 50:
+            out[i] = bi
+            n += 1
+    return n, out
+
+
+def _py_hist_reject(hist_entries, clear):
+    """ComputeThreeMaxima + removal; hist_entries: list of (bin, payload). Returns removed count."""
+    f32 = np.float32
+    sizes = [0] * 30
+    for b, _ in hist_entries:
+        sizes[b] += 1
+    m1 = m2 = m3 = 0
+    i1 = i2 = i3 = -1
+    for i, s in enumerate(sizes):
+        if s > m1:
+            m3, m2, m1, i3, i2, i1 = m2, m1, s, i2, i1, i
+        elif s > m2:
+            m3, m2, i3, i2 = m2, s, i2, i
+        elif s > m3:
+            m3, i3 = s, i
+    if f32(m2) < f32(0.1) * f32(m1):
+        i2 = i3 = -1
+    elif f32(m3) < f32(0.1) * f32(m1):
+        i3 = -1
+    removed = 0
+    for b in range(30):
+        if b in (i1, i2, i3):
+            continue
+        for bb, pay in hist_entries:
+            if bb == b:
+                clear(pay)
+                removed += 1
+    return removed
+
+
+def _py_bin(a1, a2):
+    f32 = np.float32
+    rot = f32(a1) - f32(a2)
+    if rot < 0:
+        rot = f32(rot + f32(360))
+    b = int(math.floor(float(rot * (f32(30) / f32(360))) + 0.5))
+    return 0 if b == 30 else b
+
+
+def _py_sbp_kf(kps, desc, bounds, sf, cam, slot_mp, Tcw, mps, md, ang, th, orb_dist, check_ori):
+    f32 = np.float32
+    T, Ow = _py_pose(Tcw, False)
+    G = _py_grid(kps, bounds)
+    D = np.unpackbits(md[:, None, :] ^ desc[None, :, :], axis=2).sum(axis=2)
+    sm = slot_mp.copy()
+    n = 0
+    hist = []
+    for i, p in enumerate(mps):
+        if p["skip"]:
+            continue
+        X = (p["x"], p["y"], p["z"])
+        Xc = _f32_mul_add(T[:, :3], X, T[:, 3])
+        invz = f32(1.0 / float(Xc[2]))
+        u = f32(cam[0]) * Xc[0] * invz + f32(cam[2])
+        v = f32(cam[1]) * Xc[1] * invz + f32(cam[3])
+        if u < f32(bounds[0]) or u > f32(bounds[1]) or v < f32(bounds[2]) or v > f32(bounds[3]):
+            continue
+        dist, _ = _py_norm_dot([f32(X[k]) - Ow[k] for k in range(3)], (0, 0, 0))
+        if dist < f32(0.8) * p["min_dist"] or dist > f32(1.2) * p["max_dist"]:
+            continue
+        pl = _py_predict(p["max_dist"], dist, sf)
+        bd, bi = 256, -1
+        for j in _py_area(G, kps, u, v, f32(th) * sf[pl], pl - 1, pl + 1):
+            if sm[j] >= 0:
+                continue
+            if D[i, j] < bd:
+                bd, bi = int(D[i, j]), j
+        if bd <= orb_dist:
+            sm[bi] = p["id"]
+            n += 1
+            if check_ori:
+                hist.append((_py_bin(ang[i], kps["angle"][bi]), bi))
+    if check_ori:
+        n -= _py_hist_reject(hist, lambda j: sm.__setitem__(j, -1))
+    return n, sm
+
+
+def _py_common_nodes(node1, node2):
+    nodes = sorted(set(int(v) for v in node1 if v >= 0) & set(int(v) for v in node2 if v >= 0))
+    for nd in nodes:
+        yield [i for i in range(len(node1)) if node1[i] == nd], [j for j in range(len(node2)) if node2[j] == nd]
+
+
+def _py_bow_kf_frame(kf, f, nnratio, check_ori):
+    k1, d1, n1, mp1, bad1 = kf
+    k2, d2, n2 = f[:3]
+    D = np.unpackbits(d1[:, None, :] ^ d2[None, :, :], axis=2).sum(axis=2)
+    out = np.full(len(k2), -1, np.int32)
+    n, hist = 0, []
+    for r1, r2 in _py_common_nodes(n1, n2):
+        for i in r1:
+            if mp1[i] < 0 or bad1[i]:
+                continue
+            b1, b2, bi = 256, 256, -1
+            for j in r2:
+                if out[j] >= 0:
+                    continue
+                d = int(D[i, j])
+                if d < b1:
+                    b2, b1, bi = b1, d, j
+                elif d < b2:
+                    b2 = d
+            if b1 <= 50 and np.float32(b1) < np.float32(nnratio) * np.float32(b2):
+                out[bi] = mp1[i]
+                if check_ori:
+                    hist.append((_py_bin(k1["angle"][i], k2["angle"][bi]), bi))
+                n += 1
+    if check_ori:
+        n -= _py_hist_reject(hist, lambda j: out.__setitem__(j, -1))
+    return n, out
+
+
+def _py_bow_kf_kf(a, b, nnratio, check_ori):
+    k1, d1, n1, mp1, bad1 = a
+    k2, d2, n2, mp2, bad2 = b
+    D = np.unpackbits(d1[:, None, :] ^ d2[None, :, :], axis=2).sum(axis=2)
+    out = np.full(len(k1), -1, np.int32)
+    matched = np.zeros(len(k2), bool)
+    n, hist = 0, []
+    for r1, r2 in _py_common_nodes(n1, n2):
+        for i in r1:
+            if mp1[i] < 0 or bad1[i]:
+                continue
+            b1, b2, bi = 256, 256, -1
+            for j in r2:
+                if matched[j] or mp2[j] < 0 or bad2[j]:
+                    continue
+                d = int(D[i, j])
+                if d < b1:
+                    b2, b1, bi = b1, d, j
+                elif d < b2:
+                    b2 = d
+            if b1 < 50 and np.float32(b1) < np.float32(nnratio) * np.float32(b2):
+                out[i] = mp2[bi]
+                matched[bi] = True
+                if check_ori:
+                    hist.append((_py_bin(k1["angle"][i], k2["angle"][bi]), i))
+                n += 1
+    if check_ori:
+        n -= _py_hist_reject(hist, lambda i: out.__setitem__(i, -1))
+    return n, out
+
+
+def _py_triangulation(a, b, C1, T2w, cam2, sf2, F12, only_stereo, check_ori):
+    f32 = np.float32
+    k1, d1, n1, mp1, _, ur1 = a
+    k2, d2, n2, mp2, _, ur2 = b
+    C2 = _f32_mul_add(T2w[:, :3], C1, T2w[:, 3])
+    invz = f32(1.0) / C2[2]
+    ex = f32(cam2[0]) * C2[0] * invz + f32(cam2[2])
+    ey = f32(cam2[1]) * C2[1] * invz + f32(cam2[3])
+    D = np.unpackbits(d1[:, None, :] ^ d2[None, :, :], axis=2).sum(axis=2)
+    m12 = np.full(len(k1), -1, np.int32)
+    matched = np.zeros(len(k2), bool)
+    n, hist = 0, []
+    F = np.asarray(F12, f32)
+    for r1, r2 in _py_common_nodes(n1, n2):
+        for i in r1:
+            if mp1[i] >= 0:
+                continue
+            s1 = ur1 is not None and ur1[i] >= 0
+            if only_stereo and not s1:
+                continue
+            x1, y1 = k1["x"][i], k1["y"][i]
+            bd, bi = 50, -1
+            for j in r2:
+                if matched[j] or mp2[j] >= 0:
+                    continue
+                s2 = ur2 is not None and ur2[j] >= 0
+                if only_stereo and not s2:
+                    continue
+                d = int(D[i, j])
+                if d > 50 or d > bd:
+                    continue
+                x2, y2, o2 = k2["x"][j], k2["y"][j], int(k2["octave"][j])
+                if not s1 and not s2:
+                    dx, dy = ex - x2, ey - y2
+                    if dx * dx + dy * dy < f32(100) * sf2[o2]:
+                        continue
+                la = x1 * F[0, 0] + y1 * F[1, 0] + F[2, 0]
+                lb = x1 * F[0, 1] + y1 * F[1, 1] + F[2, 1]
+                lc = x1 * F[0, 2] + y1 * F[1, 2] + F[2, 2]
+                num = la * x2 + lb * y2 + lc
+                den = la * la + lb * lb
+                if den == 0:
+                    continue
+                if float(num * num / den) < 3.84 * float(sf2[o2] * sf2[o2]):
+                    bi, bd = j, d
+            if bi >= 0:
+                m12[i] = bi
+                matched[bi] = True
+                n += 1
+                if check_ori:
+                    hist.append((_py_bin(k1["angle"][i], k2["angle"][bi]), i))
+
+    def clear(i):
+        matched[m12[i]] = False
+        m12[i] = -1
+    if check_ori:
+        n -= _py_hist_reject(hist, clear)
+    return n, m12
+
+
+@pytest.fixture(scope="module")
+def kf_scene(OB, proj_scene):
+    S, k1, d1, k2, d2, bounds = proj_scene
+    cam = S.camera(640, 300)
+    mps, md = S.map_points(k1, d1, 640, 300, seed=2)
+    return S, k1, d1, k2, d2, bounds, cam, mps, md
+
+
+@pytest.mark.parametrize("s,th", [(1.0, 10), (1.3, 10), (0.8, 4)])
+def test_search_by_projection_sim3_matches_transliteration(OB, kf_scene, s, th):
+    S, k1, d1, k2, d2, bounds, cam, mps, md = kf_scene
+    Scw = S.sim3_of(S.keyframe_pose((6.0, -2.0), 640, 300, (0.02, 0.0, 0.1)), s)
+    _, sm, _ = S.current_slots(k2, 2, False)
+    sf = S.scale_factors()
+    n, m = OB.search_by_projection_sim3(k2, d2, bounds, sf, cam, sm, Scw, mps, md, th)
+    n_py, m_py = _py_sbp_sim3(k2, d2, bounds, sf, cam, sm, Scw, mps, md, th)
+    assert n == n_py and n > 20
+    np.testing.assert_array_equal(m, m_py)
+
+
+@pytest.mark.parametrize("sim3,stereo,th", [(False, False, 3.0), (False, True, 5.0), (True, False, 4.0)])
+def test_fuse_matches_transliteration(OB, kf_scene, sim3, stereo, th):
+    S, k1, d1, k2, d2, bounds, cam, mps, md = kf_scene
+    T = S.keyframe_pose((6.0, -2.0), 640, 300, (0.0, 0.01, 0.05))
+    if sim3:
+        T = S.sim3_of(T, 1.2)
+    ur, _, _ = S.current_slots(k2, 3, stereo)
+    sf = S.scale_factors()
+    n, idx = OB.fuse(k2, d2, bounds, sf, cam, ur, T, sim3, mps, md, th)
+    n_py, idx_py = _py_fuse(k2, d2, bounds, sf, cam, ur, T, sim3, mps, md, th)
+    assert n == n_py and n > 10
+    np.testing.assert_array_equal(idx, idx_py)
+
+
+@pytest.mark.parametrize("th,orb_dist,check_ori", [(10.0, 100, True), (3.0, 64, False)])
+def test_search_by_projection_kf_matches_transliteration(OB, kf_scene, th, orb_dist, check_ori):
+    S, k1, d1, k2, d2, bounds, cam, mps, md = kf_scene
+    Tcw = S.keyframe_pose((6.0, -2.0), 640, 300, (0.01, 0.0, -0.1))
+    _, sm, _ = S.current_slots(k2, 4, False)
+    sf = S.scale_factors()
+    n, m = OB.search_by_projection_kf(k2, d2, bounds, sf, cam, sm, Tcw, mps, md, k1["angle"], th, orb_dist,
+                                      check_ori)
+    n_py, m_py = _py_sbp_kf(k2, d2, bounds, sf, cam, sm, Tcw, mps, md, k1["angle"], th, orb_dist, check_ori)
+    assert n == n_py and n > 20
+    np.testing.assert_array_equal(m, m_py)
+
+
+@pytest.mark.parametrize("check_ori", [True, False])
+def test_search_by_bow_matches_transliteration(OB, proj_scene, check_ori):
+    S, k1, d1, k2, d2, bounds = proj_scene
+    n1, n2 = S.bow_nodes(d1, 1), S.bow_nodes(d2, 2)
+    mp1, bad1 = S.bow_points(len(k1), 1)
+    mp2, bad2 = S.bow_points(len(k2), 2, base=10000)
+    a = (k1, d1, n1, mp1, bad1)
+    n, out = OB.search_by_bow_kf_frame(a, (k2, d2, n2, mp2), 0.7, check_ori)
+    n_py, out_py = _py_bow_kf_frame(a, (k2, d2, n2), 0.7, check_ori)
+    assert n == n_py and n > 20
+    np.testing.assert_array_equal(out, out_py)
+    b = (k2, d2, n2, mp2, bad2)
+    n, out = OB.search_by_bow_kf_kf(a, b, 0.75, check_ori)
+    n_py, out_py = _py_bow_kf_kf(a, b, 0.75, check_ori)
+    assert n == n_py and n > 20
+    np.testing.assert_array_equal(out, out_py)
+
+
+@pytest.mark.parametrize("stereo,only_stereo,check_ori", [(False, False, False), (True, False, True),
+                                                          (True, True, False)])
+def test_search_for_triangulation_matches_transliteration(OB, proj_scene, stereo, only_stereo, check_ori):
+    S, k1, d1, k2, d2, bounds = proj_scene
+    cam = S.camera(640, 300)
+    T1 = S.keyframe_pose((0.0, 0.0), 640, 300)
+    T2 = S.keyframe_pose((6.0, -2.0), 640, 300, (0.3, 0.0, 0.05))
+    F12 = S.fundamental_12(T1, T2, cam, cam)
+    n1, n2 = S.bow_nodes(d1, 5), S.bow_nodes(d2, 6)
+    mp1, _ = S.bow_points(len(k1), 5, frac=0.3)
+    mp2, _ = S.bow_points(len(k2), 6, frac=0.3)
+    ur1, _, _ = S.current_slots(k1, 5, stereo)
+    ur2, _, _ = S.current_slots(k2, 6, stereo)
+    C1 = np.zeros(3, np.float32)
+    a = (k1, d1, n1, mp1, None, ur1)
+    b = (k2, d2, n2, mp2, None, ur2)
+    sf = S.scale_factors()
+    n, m12 = OB.search_for_triangulation(a, b, C1, T2, cam[:4], sf, F12, only_stereo, check_ori)
+    n_py, m_py = _py_triangulation(a, b, C1, T2, cam[:4], sf, F12, only_stereo, check_ori)
+    assert n == n_py and n > 5
+    np.testing.assert_array_equal(m12, m_py)
