@@ -168,6 +168,17 @@ int sqlm_orb_search_by_projection_kf(sqlm_ctx *ctx, sqlm_orb_frame *F, const flo
                                      const uint8_t *mp_desc, const float *kf_angle, int n, float th, int orb_dist,
                                      int check_ori, int *n_matches);
 
+/* ORBmatcher::SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+ * (ORBmatcher.cc:1448-1608): K1 / K2 the two keyframes (K1's fx fy cx cy
+ * project both ways, as the reference does), T1w / T2w their 3x4 poses,
+ * mp1 / mp2 their map-point slots (id -1: NULL, skip: isBad()) with
+ * descriptors; R12 row-major, t12 [3]. matches12 [K1->n]: in = vpMatches12
+ * as ids (-1: NULL), out = with the mutual matches added. *n_found = nFound. */
+int sqlm_orb_search_by_sim3(sqlm_ctx *ctx, const sqlm_orb_frame *K1, const sqlm_orb_frame *K2, const float *T1w,
+                            const float *T2w, const sqlm_map_point *mp1, const uint8_t *md1, const sqlm_map_point *mp2,
+                            const uint8_t *md2, float s12, const float *R12, const float *t12, float th,
+                            int32_t *matches12, int *n_found);
+
 /* A keyframe (or Frame) as the BoW searches read it: mvKeysUn, mDescriptors
  * [n][32], the DBoW2 FeatureVector as the node id of each feature (-1: the
  * feature is not in mFeatVec), GetMapPointMatches() ids (-1: NULL), their

@@ -304,3 +304,21 @@ def search_for_triangulation(k1, k2, C1, T2w, cam2, scale2, F12, only_stereo, ch
     r = lib().orc_search_for_triangulation(C.byref(a), C.byref(b), _p(C1), _p(T), _p(cam2), _p(s2), _p(F),
                                            int(bool(only_stereo)), int(bool(check_ori)), _p(out))
     return r, out[:a.n]
+
+
+def search_by_sim3(k1, d1, k2, d2, bounds, scale, cam, T1w, T2w, mp1, md1, mp2, md2, s12, R12, t12, th, matches12):
+    """SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th) -> (nFound, vpMatches12)."""
+    n1, n2 = len(k1), len(k2)
+    f1, keep1, _, _ = _frame(k1, d1, bounds, scale, cam, None, np.full(n1, -1), np.zeros(n1))
+    f2, keep2, _, _ = _frame(k2, d2, bounds, scale, cam, None, np.full(n2, -1), np.zeros(n2))
+    arr = [np.ascontiguousarray(np.asarray(T, np.float32)[:3, :4]) for T in (T1w, T2w)]
+    mp1 = np.ascontiguousarray(mp1, MAP_POINT_DTYPE)
+    mp2 = np.ascontiguousarray(mp2, MAP_POINT_DTYPE)
+    md1 = np.ascontiguousarray(md1, np.uint8)
+    md2 = np.ascontiguousarray(md2, np.uint8)
+    R = np.ascontiguousarray(R12, np.float32)
+    t = np.ascontiguousarray(t12, np.float32)
+    m = np.array(matches12, np.int32)
+    r = lib().orc_search_by_sim3(C.byref(f1), C.byref(f2), _p(arr[0]), _p(arr[1]), _p(mp1), _p(md1), _p(mp2),
+                                 _p(md2), C.c_float(s12), _p(R), _p(t), C.c_float(th), _p(m))
+    return r, m

@@ -1659,3 +1659,101 @@ int orc_search_for_triangulation(const orc_bow_frame *K1, const orc_bow_frame *K
   free(c.rot_idx);
   return c.nmatches;
 }
+
+/* ---- SearchBySim3 (ORBmatcher.cc:1448-1608) ---- */
+/* One direction: points of `src` (in src's camera via Tsw, then by [sR | t]
+ * into dst's camera) searched in dst (fx.. of pKF1 for both, :1455-1458). */
+static void sim3_direction(const orc_frame *cam, const orc_frame *dst, const float *Tsw, const float *sR,
+                           const float *t, const orc_map_point *mp, const uint8_t *md, int n, const uint8_t *already,
+                           float th, int *vnMatch) {
+  orc_grid G;
+  grid_build(dst, &G);
+  int *vIndices = (int *)malloc(sizeof(int) * (dst->n > 0 ? dst->n : 1));
+  const float ts[3] = {Tsw[3], Tsw[7], Tsw[11]};
+  float sRT[12];
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) sRT[r * 4 + c] = sR[r * 3 + c];
+    sRT[r * 4 + 3] = 0.f;
+  }
+  for (int i = 0; i < n; i++) {
+    vnMatch[i] = -1;
+    const orc_map_point *p = &mp[i];
+    if (p->id < 0 || already[i] || p->skip) continue;
+    const float X[3] = {p->x, p->y, p->z};
+    float Xs[3], Xd[3];
+    mat3_mul_add(Tsw, 0, X, ts, 1.0f, Xs);
+    mat3_mul_add(sRT, 0, Xs, t, 1.0f, Xd);
+    if (Xd[2] < 0.0) continue;
+    const float invz = (float)(1.0 / (double)Xd[2]);
+    const float x = Xd[0] * invz, y = Xd[1] * invz;
+    const float u = cam->fx * x + cam->cx, v = cam->fy * y + cam->cy;
+    if (!(u >= dst->bounds.min_x && u < dst->bounds.max_x && v >= dst->bounds.min_y && v < dst->bounds.max_y))
+      continue;
+    const float maxDistance = 1.2f * p->max_dist, minDistance = 0.8f * p->min_dist;
+    const float dist3D = norm3(Xd);
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    const int pl = predict_scale(p->max_dist, dist3D, logf(dst->scale_factors[1]), dst->n_levels);
+    const float radius = th * dst->scale_factors[pl];
+    const int nI = area(dst, &G, u, v, radius, pl - 1, pl, vIndices);
+    int bestDist = INT_MAX, bestIdx = -1;
+    for (int q = 0; q < nI; ++q) {
+      const int idx = vIndices[q];
+      const int dist = orc_hamming(md + 32 * (size_t)i, dst->desc + 32 * (size_t)idx);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx = idx;
+      }
+    }
+    if (bestDist <= TH_HIGH) vnMatch[i] = bestIdx;
+  }
+  free(vIndices);
+  grid_free(&G);
+}
+
+int orc_search_by_sim3(const orc_frame *K1, const orc_frame *K2, const float *T1w, const float *T2w,
+                       const orc_map_point *mp1, const uint8_t *md1, const orc_map_point *mp2, const uint8_t *md2,
+                       float s12, const float *R12, const float *t12, float th, int *matches12) {
+  const int N1 = K1->n, N2 = K2->n;
+  /* sR12 = s12 * R12, sR21 = (1 / s12) * R12^T, t21 = -sR21 * t12 (:1466-1469) */
+  float sR12[9], sR21[9], t21[3];
+  const float inv_s = (float)(1.0 / (double)s12);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      sR12[r * 3 + c] = R12[r * 3 + c] * s12;
+      sR21[r * 3 + c] = R12[c * 3 + r] * inv_s;
+    }
+  {
+    float sR21T[12];
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) sR21T[r * 4 + c] = sR21[r * 3 + c];
+      sR21T[r * 4 + 3] = 0.f;
+    }
+    mat3_mul_add(sR21T, 0, t12, NULL, -1.0f, t21);
+  }
+  /* vbAlreadyMatched1 / 2 (:1480-1494): pMP->GetIndexInKeyFrame(pKF2) is the
+   * slot of pKF2 holding the same point */
+  uint8_t *am1 = (uint8_t *)calloc(N1 > 0 ? N1 : 1, 1), *am2 = (uint8_t *)calloc(N2 > 0 ? N2 : 1, 1);
+  for (int i = 0; i < N1; i++)
+    if (matches12[i] >= 0) {
+      am1[i] = 1;
+      for (int j = 0; j < N2; ++j)
+        if (mp2[j].id == matches12[i]) am2[j] = 1;
+    }
+  int *vnMatch1 = (int *)malloc(sizeof(int) * (N1 > 0 ? N1 : 1));
+  int *vnMatch2 = (int *)malloc(sizeof(int) * (N2 > 0 ? N2 : 1));
+  sim3_direction(K1, K2, T1w, sR21, t21, mp1, md1, N1, am1, th, vnMatch1);
+  sim3_direction(K1, K1, T2w, sR12, t12, mp2, md2, N2, am2, th, vnMatch2);
+  int nFound = 0;
+  for (int i1 = 0; i1 < N1; i1++) { /* :1592-1606 */
+    const int idx2 = vnMatch1[i1];
+    if (idx2 >= 0 && vnMatch2[idx2] == i1) {
+      matches12[i1] = mp2[idx2].id;
+      nFound++;
+    }
+  }
+  free(am1);
+  free(am2);
+  free(vnMatch1);
+  free(vnMatch2);
+  return nFound;
+}

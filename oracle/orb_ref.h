@@ -180,4 +180,12 @@ int orc_search_by_bow_kf_kf(const orc_bow_frame *K1, const orc_bow_frame *K2, fl
 int orc_search_for_triangulation(const orc_bow_frame *K1, const orc_bow_frame *K2, const float *C1, const float *T2w,
                                  const float *cam2, const float *scale_factors2, const float *F12, int only_stereo,
                                  int check_ori, int *m12);
+
+/* SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+ * (ORBmatcher.cc:1448-1608): K1 / K2 with their 3x4 poses T1w / T2w and
+ * map-point slots mp1 / mp2 (id -1: NULL; skip: isBad()); matches12 [K1.n]
+ * in: vpMatches12 as ids, out: with the mutual matches added. R12 row-major. */
+int orc_search_by_sim3(const orc_frame *K1, const orc_frame *K2, const float *T1w, const float *T2w,
+                       const orc_map_point *mp1, const uint8_t *md1, const orc_map_point *mp2, const uint8_t *md2,
+                       float s12, const float *R12, const float *t12, float th, int *matches12);
 #endif

@@ -1852,6 +1852,14 @@ int sqlm_orb_search_by_projection_kf(sqlm_ctx *c, sqlm_orb_frame *F, const float
   return orb_search_by_projection_kf(c->orb, F, Tcw, mps, mp_desc, kf_angle, n, th, orb_dist, check_ori, n_matches);
 }
 
+int sqlm_orb_search_by_sim3(sqlm_ctx *c, const sqlm_orb_frame *K1, const sqlm_orb_frame *K2, const float *T1w,
+                            const float *T2w, const sqlm_map_point *mp1, const uint8_t *md1, const sqlm_map_point *mp2,
+                            const uint8_t *md2, float s12, const float *R12, const float *t12, float th,
+                            int32_t *matches12, int *n_found) {
+  if (int r = orb_engine(c)) return r;
+  return orb_search_by_sim3(c->orb, K1, K2, T1w, T2w, mp1, md1, mp2, md2, s12, R12, t12, th, matches12, n_found);
+}
+
 int sqlm_orb_search_by_bow_kf_frame(sqlm_ctx *c, const sqlm_bow_frame *KF, const sqlm_bow_frame *F, float nnratio,
                                     int check_ori, int32_t *matches, int *n_matches) {
   if (int r = orb_engine(c)) return r;

@@ -299,6 +299,10 @@ int orb_fuse(OrbEngine *e, const struct sqlm_orb_frame *F, const float *T, int s
 int orb_search_by_projection_kf(OrbEngine *e, struct sqlm_orb_frame *F, const float *Tcw,
                                 const struct sqlm_map_point *mps, const uint8_t *mp_desc, const float *kf_angle, int n,
                                 float th, int orb_dist, int check_ori, int *n_matches);
+int orb_search_by_sim3(OrbEngine *e, const struct sqlm_orb_frame *K1, const struct sqlm_orb_frame *K2, const float *T1w,
+                       const float *T2w, const struct sqlm_map_point *mp1, const uint8_t *md1,
+                       const struct sqlm_map_point *mp2, const uint8_t *md2, float s12, const float *R12,
+                       const float *t12, float th, int32_t *matches12, int *n_found);
 int orb_search_by_bow_kf_frame(OrbEngine *e, const struct sqlm_bow_frame *KF, const struct sqlm_bow_frame *F,
                                float nnratio, int check_ori, int32_t *matches, int *n_matches);
 int orb_search_by_bow_kf_kf(OrbEngine *e, const struct sqlm_bow_frame *K1, const struct sqlm_bow_frame *K2,

@@ -2042,4 +2042,101 @@ int orb_search_for_triangulation(OrbEngine *e, const sqlm_bow_frame *K1, const s
   return SQLM_OK;
 }
 
+// ---- SearchBySim3 (ORBmatcher.cc:1448-1608): two independent directions,
+// then the mutual check — no order dependence, every window on the GPU ----
+static int sim3_direction(OrbEngine *e, const sqlm_orb_frame *cam, const sqlm_orb_frame *dst, const float *Tsw,
+                          const float *sR, const float *t, const sqlm_map_point *mp, const uint8_t *md, int n,
+                          const std::vector<uint8_t> &already, float th, std::vector<int> &vnMatch) {
+  float sRT[12];
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) sRT[r * 4 + c] = sR[r * 3 + c];
+    sRT[r * 4 + 3] = 0.f;
+  }
+  const float ts[3] = {Tsw[3], Tsw[7], Tsw[11]};
+  const float log_scale = std::log(dst->scale_factors[1]);
+  std::vector<float4> hq(n);
+  for (int i = 0; i < n; i++) {  // :1499-1540 / :1545-1586
+    hq[i] = area_query(0.f, 0.f, 0.f, kAreaSkip);
+    const sqlm_map_point &p = mp[i];
+    if (p.id < 0 || already[i] || p.skip) continue;
+    const float X[3] = {p.x, p.y, p.z};
+    float Xs[3], Xd[3];
+    mat3_mul_add(Tsw, false, X, ts, 1.0, Xs);
+    mat3_mul_add(sRT, false, Xs, t, 1.0, Xd);
+    if (Xd[2] < 0.0) continue;
+    const float invz = (float)(1.0 / (double)Xd[2]);
+    const float x = Xd[0] * invz, y = Xd[1] * invz;
+    const float u = cam->fx * x + cam->cx, v = cam->fy * y + cam->cy;
+    if (!(u >= dst->bounds.min_x && u < dst->bounds.max_x && v >= dst->bounds.min_y && v < dst->bounds.max_y))
+      continue;
+    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+    const float dist3D = norm3(Xd);
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    const int pl = predict_scale(p.max_dist, dist3D, log_scale, dst->n_levels);
+    hq[i] = area_query(u, v, th * dst->scale_factors[pl], area_levels(pl - 1, pl));
+  }
+  std::vector<int> hoff;
+  std::vector<int2> hp;
+  if (int rc = area_search(e, dst->kps, dst->desc, dst->n, &dst->bounds, hq, md, hoff, hp)) return rc;
+  vnMatch.assign(n, -1);
+  for (int i = 0; i < n; ++i) {
+    int bestDist = INT_MAX, bestIdx = -1;
+    for (int q = hoff[i]; q < hoff[i + 1]; ++q)
+      if (hp[q].y < bestDist) {
+        bestDist = hp[q].y;
+        bestIdx = hp[q].x;
+      }
+    if (bestDist <= kThHigh) vnMatch[i] = bestIdx;
+  }
+  return SQLM_OK;
+}
+
+int orb_search_by_sim3(OrbEngine *e, const sqlm_orb_frame *K1, const sqlm_orb_frame *K2, const float *T1w,
+                       const float *T2w, const sqlm_map_point *mp1, const uint8_t *md1, const sqlm_map_point *mp2,
+                       const uint8_t *md2, float s12, const float *R12, const float *t12, float th, int32_t *matches12,
+                       int *n_found) {
+  if (!kf_frame_ok(K1) || !kf_frame_ok(K2) || !T1w || !T2w || !R12 || !t12 ||
+      (K1->n && (!mp1 || !md1 || !matches12)) || (K2->n && (!mp2 || !md2)))
+    return SQLM_ERR_INVALID_ARG;
+  if (n_found) *n_found = 0;
+  const int N1 = K1->n, N2 = K2->n;
+  // sR12 = s12 R12, sR21 = (1 / s12) R12^T, t21 = -sR21 t12 (:1466-1469)
+  float sR12[9], sR21[9], t21[3], sR21T[12];
+  const float inv_s = (float)(1.0 / (double)s12);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      sR12[r * 3 + c] = R12[r * 3 + c] * s12;
+      sR21[r * 3 + c] = R12[c * 3 + r] * inv_s;
+      sR21T[r * 4 + c] = sR21[r * 3 + c];
+    }
+  for (int r = 0; r < 3; ++r) sR21T[r * 4 + 3] = 0.f;
+  mat3_mul_add(sR21T, false, t12, nullptr, -1.0, t21);
+  // vbAlreadyMatched1 / 2 (:1480-1494): GetIndexInKeyFrame(pKF2) = pKF2's slot of the same point
+  std::vector<uint8_t> am1(N1, 0), am2(N2, 0);
+  {
+    std::vector<int32_t> ids;
+    for (int i = 0; i < N1; i++)
+      if (matches12[i] >= 0) {
+        am1[i] = 1;
+        ids.push_back(matches12[i]);
+      }
+    std::sort(ids.begin(), ids.end());
+    for (int j = 0; j < N2; ++j)
+      if (std::binary_search(ids.begin(), ids.end(), mp2[j].id)) am2[j] = 1;
+  }
+  std::vector<int> vnMatch1, vnMatch2;
+  if (int rc = sim3_direction(e, K1, K2, T1w, sR21, t21, mp1, md1, N1, am1, th, vnMatch1)) return rc;
+  if (int rc = sim3_direction(e, K1, K1, T2w, sR12, t12, mp2, md2, N2, am2, th, vnMatch2)) return rc;
+  int nFound = 0;
+  for (int i1 = 0; i1 < N1; i1++) {  // :1592-1606
+    const int idx2 = vnMatch1[i1];
+    if (idx2 >= 0 && vnMatch2[idx2] == i1) {
+      matches12[i1] = mp2[idx2].id;
+      nFound++;
+    }
+  }
+  if (n_found) *n_found = nFound;
+  return SQLM_OK;
+}
+
 }  // namespace sqlm

@@ -41,7 +41,7 @@ CAPTURE_EXPORTS = ["sqlm_capture_write", "sqlm_capture_read", "sqlm_capture_free
 ORB_EXPORTS = ["sqlm_orb_extract", "sqlm_orb_get_level", "sqlm_orb_match_bf", "sqlm_orb_search_for_init",
                "sqlm_orb_search_by_projection_local", "sqlm_orb_search_by_projection_last",
                "sqlm_orb_search_by_projection_sim3", "sqlm_orb_fuse", "sqlm_orb_search_by_projection_kf",
-               "sqlm_orb_search_by_bow_kf_frame", "sqlm_orb_search_by_bow_kf_kf", "sqlm_orb_search_for_triangulation",
+               "sqlm_orb_search_by_sim3", "sqlm_orb_search_by_bow_kf_frame", "sqlm_orb_search_by_bow_kf_kf", "sqlm_orb_search_for_triangulation",
                "sqlm_orb_bench_extract"]
 
 

@@ -409,3 +409,28 @@ class ORBmatcher:
             C.byref(n)), "sqlm_orb_search_for_triangulation")
         i1 = np.nonzero(m12 >= 0)[0]
         return n.value, [(int(i), int(m12[i])) for i in i1]
+
+    def SearchBySim3(self, pKF1: Frame, pKF2: Frame, mapPoints1, descriptors1, mapPoints2, descriptors2,
+                     vpMatches12, s12: float, R12, t12, th: float):
+        """SearchBySim3(pKF1, pKF2, vpMatches12, s12, R12, t12, th)
+        (ORBmatcher.cc:1448-1608). pKF1 / pKF2 Frames with mTcw; mapPoints1 /
+        mapPoints2 their slots MAP_POINT_DTYPE [N] (id -1: NULL, skip: isBad());
+        vpMatches12 int32 [pKF1.N] ids, updated in place. Returns nFound."""
+        if pKF1.mTcw is None or pKF2.mTcw is None:
+            raise ValueError("pKF1.mTcw and pKF2.mTcw are required")
+        m1 = np.ascontiguousarray(mapPoints1, MAP_POINT_DTYPE)
+        m2 = np.ascontiguousarray(mapPoints2, MAP_POINT_DTYPE)
+        if len(m1) != pKF1.N or len(m2) != pKF2.N:
+            raise ValueError("one map-point slot per keypoint")
+        d1 = np.ascontiguousarray(descriptors1, np.uint8).reshape(len(m1), 32)
+        d2 = np.ascontiguousarray(descriptors2, np.uint8).reshape(len(m2), 32)
+        if vpMatches12.dtype != np.int32 or not vpMatches12.flags.c_contiguous or vpMatches12.shape != (pKF1.N,):
+            raise ValueError("vpMatches12 must be a C-contiguous int32 [pKF1.N] array (updated in place)")
+        R = np.ascontiguousarray(R12, np.float32).reshape(3, 3)
+        t = np.ascontiguousarray(t12, np.float32).reshape(3)
+        n = C.c_int(0)
+        a, b = pKF1._struct(), pKF2._struct()
+        check(lib().sqlm_orb_search_by_sim3(self.ctx._h, C.byref(a), C.byref(b), ptr(pKF1.mTcw), ptr(pKF2.mTcw),
+                                            ptr(m1), ptr(d1), ptr(m2), ptr(d2), C.c_float(s12), ptr(R), ptr(t),
+                                            C.c_float(th), ptr(vpMatches12), C.byref(n)), "sqlm_orb_search_by_sim3")
+        return n.value

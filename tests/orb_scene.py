@@ -182,3 +182,37 @@ def fundamental_12(T1w, T2w, cam1, cam2):
     t12 = -R1 @ R2.T @ t2 + t1
     tx = np.array([[0, -t12[2], t12[1]], [t12[2], 0, -t12[0]], [-t12[1], t12[0], 0]])
     return (np.linalg.inv(K(cam1)).T @ tx @ R12 @ np.linalg.inv(K(cam2))).astype(np.float32)
+
+
+def keyframe_points(k, d, T, w, h, seed, n_levels=8):
+    """map_points for a keyframe with pose T (3x4 Tcw): its keypoints
+    back-projected at random depths into the world."""
+    mp, desc = map_points(k, d, w, h, seed, n_levels)
+    R, t = np.asarray(T[:, :3], np.float64), np.asarray(T[:, 3], np.float64)
+    Xc = np.stack([mp["x"], mp["y"], mp["z"]], 1).astype(np.float64)
+    Xw = (Xc - t) @ R  # R^T (Xc - t)
+    nw = np.stack([mp["nx"], mp["ny"], mp["nz"]], 1).astype(np.float64) @ R
+    mp["x"], mp["y"], mp["z"] = Xw[:, 0], Xw[:, 1], Xw[:, 2]
+    mp["nx"], mp["ny"], mp["nz"] = nw[:, 0], nw[:, 1], nw[:, 2]
+    return mp, desc
+
+
+def sim3_scene(k1, d1, k2, d2, shift, w, h, seed):
+    """Two keyframes for SearchBySim3: T1w = I, T2w from the image shift plus a
+    small translation, both map-point slot sets (a quarter NULL), S12 = their
+    relative pose, and vpMatches12 with a few matches already in."""
+    rng = np.random.default_rng(seed + 13)
+    T1 = keyframe_pose((0.0, 0.0), w, h)
+    T2 = keyframe_pose(shift, w, h, (0.05, 0.0, 0.02))
+    mp1, md1 = map_points(k1, d1, w, h, seed)
+    mp2, md2 = keyframe_points(k2, d2, T2, w, h, seed + 1)
+    mp2["id"] = np.arange(len(mp2)) + 20000
+    mp1["id"][rng.random(len(mp1)) < 0.25] = -1
+    mp2["id"][rng.random(len(mp2)) < 0.25] = -1
+    R2, t2 = T2[:, :3].astype(np.float64), T2[:, 3].astype(np.float64)
+    R12 = R2.T.astype(np.float32)
+    t12 = (-R2.T @ t2).astype(np.float32)
+    m12 = np.full(len(k1), -1, np.int32)
+    pick = rng.choice(len(k1), 20, replace=False)
+    m12[pick] = rng.choice(mp2["id"][mp2["id"] >= 0], 20, replace=False)
+    return T1, T2, mp1, md1, mp2, md2, R12, t12, m12

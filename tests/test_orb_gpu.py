@@ -310,3 +310,21 @@ def test_bow_edge_cases(gpu_ctx, kitti_pair):
     assert n == 0 and (out == -1).all()  # no feature in the vocabulary: no common node
     n, out = m.SearchByBoW(BowFrame(k1[:0], d1[:0], none[:0]), BowFrame(k2, d2, np.zeros(len(k2))))
     assert n == 0 and len(out) == 0
+
+
+@pytest.mark.parametrize("s12,th", [(1.0, 7.5), (1.03, 10.0)])
+def test_search_by_sim3(gpu_ctx, orb_oracle, kitti_pair, s12, th):
+    import orb_scene as S
+    from sqrtlm.orb import Frame, ORBmatcher
+    k1, d1, k2, d2, bounds = kitti_pair
+    cam = S.camera(1241, 376)
+    T1, T2, mp1, md1, mp2, md2, R12, t12, m12 = S.sim3_scene(k1, d1, k2, d2, (9.0, 2.0), 1241, 376, 7)
+    sf = S.scale_factors()
+    n_r, m_r = orb_oracle.search_by_sim3(k1, d1, k2, d2, bounds, sf, cam, T1, T2, mp1, md1, mp2, md2, s12, R12, t12,
+                                         th, m12)
+    K1 = Frame(k1, d1, bounds, sf, *cam[:4], mTcw=T1)
+    K2 = Frame(k2, d2, bounds, sf, *cam[:4], mTcw=T2)
+    m = m12.copy()
+    n_g = ORBmatcher(0.75, ctx=gpu_ctx).SearchBySim3(K1, K2, mp1, md1, mp2, md2, m, s12, R12, t12, th)
+    assert n_g == n_r and n_r > 100
+    np.testing.assert_array_equal(m, m_r)

@@ -939,3 +939,70 @@ def test_search_for_triangulation_matches_transliteration(OB, proj_scene, stereo
     n_py, m_py = _py_triangulation(a, b, C1, T2, cam[:4], sf, F12, only_stereo, check_ori)
     assert n == n_py and n > 5
     np.testing.assert_array_equal(m12, m_py)
+
+
+def _py_sim3_dir(cam, kd, bounds, sf, Tsw, sR, t, mps, md, already, th):
+    f32 = np.float32
+    G = _py_grid(kd[0], bounds)
+    D = np.unpackbits(md[:, None, :] ^ kd[1][None, :, :], axis=2).sum(axis=2)
+    out = np.full(len(mps), -1, np.int32)
+    for i, p in enumerate(mps):
+        if p["id"] < 0 or already[i] or p["skip"]:
+            continue
+        Xs = _f32_mul_add(Tsw[:, :3], (p["x"], p["y"], p["z"]), Tsw[:, 3])
+        Xd = _f32_mul_add(sR, Xs, t)
+        if Xd[2] < 0:
+            continue
+        invz = f32(1.0 / float(Xd[2]))
+        u = f32(cam[0]) * (Xd[0] * invz) + f32(cam[2])
+        v = f32(cam[1]) * (Xd[1] * invz) + f32(cam[3])
+        if not (u >= f32(bounds[0]) and u < f32(bounds[1]) and v >= f32(bounds[2]) and v < f32(bounds[3])):
+            continue
+        dist, _ = _py_norm_dot(Xd, (0, 0, 0))
+        if dist < f32(0.8) * p["min_dist"] or dist > f32(1.2) * p["max_dist"]:
+            continue
+        pl = _py_predict(p["max_dist"], dist, sf)
+        bd, bi = 2 ** 31 - 1, -1
+        for j in _py_area(G, kd[0], u, v, f32(th) * sf[pl], -1, -1):
+            o = kd[0]["octave"][j]
+            if o < pl - 1 or o > pl:
+                continue
+            if D[i, j] < bd:
+                bd, bi = int(D[i, j]), j
+        if bd <= 100:
+            out[i] = bi
+    return out
+
+
+def _py_search_by_sim3(k1, d1, k2, d2, bounds, sf, cam, T1, T2, mp1, md1, mp2, md2, s12, R12, t12, th, m12):
+    f32 = np.float32
+    R12 = np.asarray(R12, f32)
+    sR12 = (R12 * f32(s12)).astype(f32)
+    sR21 = (R12.T * f32(1.0 / float(f32(s12)))).astype(f32)
+    t21 = _f32_mul_add(sR21, t12, None, -1.0)
+    am1 = m12 >= 0
+    ids = set(int(v) for v in m12 if v >= 0)
+    am2 = np.array([int(v) in ids for v in mp2["id"]])
+    v1 = _py_sim3_dir(cam, (k2, d2), bounds, sf, np.asarray(T1, f32), sR21, t21, mp1, md1, am1, th)
+    v2 = _py_sim3_dir(cam, (k1, d1), bounds, sf, np.asarray(T2, f32), sR12, np.asarray(t12, f32), mp2, md2, am2, th)
+    out = m12.copy()
+    n = 0
+    for i1 in range(len(k1)):
+        j = v1[i1]
+        if j >= 0 and v2[j] == i1:
+            out[i1] = mp2["id"][j]
+            n += 1
+    return n, out
+
+
+@pytest.mark.parametrize("s12,th", [(1.0, 7.5), (1.03, 10.0)])
+def test_search_by_sim3_matches_transliteration(OB, proj_scene, s12, th):
+    S, k1, d1, k2, d2, bounds = proj_scene
+    cam = S.camera(640, 300)
+    T1, T2, mp1, md1, mp2, md2, R12, t12, m12 = S.sim3_scene(k1, d1, k2, d2, (6.0, -2.0), 640, 300, 3)
+    sf = S.scale_factors()
+    n, m = OB.search_by_sim3(k1, d1, k2, d2, bounds, sf, cam, T1, T2, mp1, md1, mp2, md2, s12, R12, t12, th, m12)
+    n_py, m_py = _py_search_by_sim3(k1, d1, k2, d2, bounds, sf, cam, T1, T2, mp1, md1, mp2, md2, s12, R12, t12, th,
+                                    m12)
+    assert n == n_py and n > 20
+    np.testing.assert_array_equal(m, m_py)
