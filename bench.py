@@ -314,6 +314,68 @@ def bench_eg(args, world):
         dist.destroy_process_group()
 
 
+def bench_matchers(ctx, ex, reps, cpu):
+    """ORBmatcher's searches on a KITTI-size scene (sqrtlm.orb_scene, two
+    2000-feature frames 9 px apart): ms per call through the C ABI (host
+    arrays in and out, windows / node runs and Hamming distances on the GPU,
+    acceptance on the host), and the single-thread oracle beside it."""
+    from sqrtlm import orb_scene as S
+    from sqrtlm import synth
+    from sqrtlm.orb import BowFrame, Frame, KeyFrameSlots, LastFrameSlots, ORBmatcher
+    a, b = synth.make_image_pair(1241, 376, seed=17, shift=(9.0, 2.0))
+    k1, d1 = ex(a)
+    k2, d2 = ex(b)
+    bounds, cam, sf = (0.0, 1241.0, 0.0, 376.0), S.camera(1241, 376), S.scale_factors()
+    mps, md = S.local_points(k1, d1, (9.0, 2.0), seed=3, stereo=True)
+    ur, sm, so = S.current_slots(k2, 3, True)
+    Tcw, Tlw, lp, ld = S.last_frame(k1, d1, (9.0, 2.0), 1241, 376, seed=4, tz=1.0)
+    kmp, kmd = S.map_points(k1, d1, 1241, 376, seed=5)
+    Tk = S.keyframe_pose((9.0, 2.0), 1241, 376, (0.0, 0.01, 0.05))
+    n1, n2 = S.bow_nodes(d1, 1), S.bow_nodes(d2, 2)
+    mp1, bad1 = S.bow_points(len(k1), 1)
+    mp2, bad2 = S.bow_points(len(k2), 2, base=10000)
+    m = ORBmatcher(0.8, True, ctx=ctx)
+
+    def frame(Tc=None):
+        return Frame(k2, d2, bounds, sf, *cam, mvuRight=ur, mTcw=Tc, mvpMapPoints=sm.copy(), slot_obs=so.copy())
+    gpu = {
+        "SearchByProjection_local": lambda: m.SearchByProjection(frame(), mps, md, 1.0),
+        "SearchByProjection_last": lambda: m.SearchByProjection(frame(Tcw), LastFrameSlots(Tlw, lp, ld), 7.0, False),
+        "SearchByProjection_kf": lambda: m.SearchByProjection(frame(Tk), KeyFrameSlots(kmp, kmd, k1["angle"]), 10.0,
+                                                              100),
+        "Fuse": lambda: m.Fuse(frame(Tk), kmp, kmd, 3.0),
+        "SearchByBoW_kf_frame": lambda: m.SearchByBoW(BowFrame(k1, d1, n1, mp1, bad1),
+                                                      BowFrame(k2, d2, n2, keyframe=False)),
+    }
+    out = {}
+    for name, fn in gpu.items():
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        out[name] = {"gpu_ms": (time.perf_counter() - t0) * 1e3 / reps}
+    if cpu:
+        from oracle import orb as OB
+        oracle = {
+            "SearchByProjection_local": lambda: OB.search_by_projection_local(k2, d2, bounds, sf, ur, sm, so, mps, md,
+                                                                              1.0, 0.8),
+            "SearchByProjection_last": lambda: OB.search_by_projection_last(k2, d2, bounds, sf, cam, ur, sm, so, Tcw,
+                                                                            Tlw, lp, ld, 7.0, False),
+            "SearchByProjection_kf": lambda: OB.search_by_projection_kf(k2, d2, bounds, sf, cam, sm, Tk, kmp, kmd,
+                                                                        k1["angle"], 10.0, 100),
+            "Fuse": lambda: OB.fuse(k2, d2, bounds, sf, cam, ur, Tk, False, kmp, kmd, 3.0),
+            "SearchByBoW_kf_frame": lambda: OB.search_by_bow_kf_frame((k1, d1, n1, mp1, bad1), (k2, d2, n2, mp2),
+                                                                      0.8),
+        }
+        for name, fn in oracle.items():
+            fn()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            out[name]["cpu_port_ms"] = (time.perf_counter() - t0) * 1e3 / reps
+    return out
+
+
 def bench_orb(args, world):
     """ORB front end (SURVEY.md §8 f3): ORBextractor::operator() on a
     KITTI-00-size synthetic grey frame (1241x376, cfg/KITTI00-02.yaml: 2000
@@ -375,6 +437,7 @@ def bench_orb(args, world):
         OB.build()
         _k, _d, pyr = OB.extract(OB.params(), img, with_levels=True)
         ncand = sum(len(OB.level_candidates(OB.params(), lev)) for lev in pyr)
+        matchers = bench_matchers(ctx, ex, reps=max(20, args.steps * 4), cpu=not args.no_cpu_baseline and world == 1)
     if world > 1:
         import torch
         tt = torch.tensor([ms], dtype=torch.float64)
@@ -391,6 +454,7 @@ def bench_orb(args, world):
                           "parallelism": f"replicas x{world}"},
                "stage_ms": dict(zip(["pyramid", "fast", "compact", "blur", "describe", "host_quadtree"], stages)),
                "stereo_two_extractors_frames_per_s": stereo_fps,
+               "matchers_ms_per_call": matchers,
                "roofline": {"bound": "hbm", "kernel": "k_orb_fast", "algorithmic_bytes": alg,
                             "achieved": alg / (t_fast * 1e-3) / 1e9 if t_fast > 0 else 0.0, "peak": HBM_PEAK_GBPS,
                             "unit": "GB/s", "traffic": None, "launch_ms": t_fast,

@@ -127,7 +127,7 @@ def kitti_pair(extractor):
 
 
 def _gpu_frame(k2, d2, bounds, ur, sm, so, Tcw=None, w=1241, h=376):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import Frame
     fx, fy, cx, cy, bf, mb = S.camera(w, h)
     return Frame(k2, d2, bounds, S.scale_factors(), fx, fy, cx, cy, bf, mb, mvuRight=ur, mTcw=Tcw,
@@ -137,7 +137,7 @@ def _gpu_frame(k2, d2, bounds, ur, sm, so, Tcw=None, w=1241, h=376):
 @pytest.mark.parametrize("stereo,th,nnratio", [(False, 1.0, 0.8), (True, 1.0, 0.8), (True, 5.0, 0.9),
                                                (False, 10.0, 0.6)])
 def test_search_by_projection_local(gpu_ctx, orb_oracle, kitti_pair, stereo, th, nnratio):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     mps, md = S.local_points(k1, d1, (9.0, 2.0), seed=3, stereo=stereo)
@@ -155,7 +155,7 @@ def test_search_by_projection_local(gpu_ctx, orb_oracle, kitti_pair, stereo, th,
                                                          (True, False, -1.0, 15.0, True),
                                                          (True, False, 0.0, 15.0, False)])
 def test_search_by_projection_last(gpu_ctx, orb_oracle, kitti_pair, stereo, mono, tz, th, check_ori):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import LastFrameSlots, ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     Tcw, Tlw, lp, ld = S.last_frame(k1, d1, (9.0, 2.0), 1241, 376, seed=4, tz=tz)
@@ -170,7 +170,7 @@ def test_search_by_projection_last(gpu_ctx, orb_oracle, kitti_pair, stereo, mono
 
 
 def test_search_by_projection_edge_cases(gpu_ctx, orb_oracle, kitti_pair):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm._lib import SqlmError
     from sqrtlm.orb import LastFrameSlots, ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
@@ -204,7 +204,7 @@ def test_search_by_projection_edge_cases(gpu_ctx, orb_oracle, kitti_pair):
 # ---- keyframe projection searches (ORBmatcher.cc:423, :1109, :1296, :1902) ----
 @pytest.mark.parametrize("s,th", [(1.0, 10), (1.3, 10), (0.8, 4)])
 def test_search_by_projection_sim3(gpu_ctx, orb_oracle, kitti_pair, s, th):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     cam = S.camera(1241, 376)
@@ -220,7 +220,7 @@ def test_search_by_projection_sim3(gpu_ctx, orb_oracle, kitti_pair, s, th):
 
 @pytest.mark.parametrize("sim3,stereo,th", [(False, False, 3.0), (False, True, 5.0), (True, False, 4.0)])
 def test_fuse(gpu_ctx, orb_oracle, kitti_pair, sim3, stereo, th):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     cam = S.camera(1241, 376)
@@ -238,7 +238,7 @@ def test_fuse(gpu_ctx, orb_oracle, kitti_pair, sim3, stereo, th):
 
 @pytest.mark.parametrize("th,orb_dist,check_ori", [(10.0, 100, True), (3.0, 64, False)])
 def test_search_by_projection_kf(gpu_ctx, orb_oracle, kitti_pair, th, orb_dist, check_ori):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import KeyFrameSlots, ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     cam = S.camera(1241, 376)
@@ -257,7 +257,7 @@ def test_search_by_projection_kf(gpu_ctx, orb_oracle, kitti_pair, th, orb_dist, 
 # ---- BoW searches (ORBmatcher.cc:246, :731, :887) ----
 @pytest.mark.parametrize("check_ori", [True, False])
 def test_search_by_bow(gpu_ctx, orb_oracle, kitti_pair, check_ori):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import BowFrame, ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     n1, n2 = S.bow_nodes(d1, 1), S.bow_nodes(d2, 2)
@@ -278,7 +278,7 @@ def test_search_by_bow(gpu_ctx, orb_oracle, kitti_pair, check_ori):
 @pytest.mark.parametrize("stereo,only_stereo,check_ori", [(False, False, False), (True, False, True),
                                                           (True, True, False)])
 def test_search_for_triangulation(gpu_ctx, orb_oracle, kitti_pair, stereo, only_stereo, check_ori):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import BowFrame, ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     cam = S.camera(1241, 376)
@@ -314,7 +314,7 @@ def test_bow_edge_cases(gpu_ctx, kitti_pair):
 
 @pytest.mark.parametrize("s12,th", [(1.0, 7.5), (1.03, 10.0)])
 def test_search_by_sim3(gpu_ctx, orb_oracle, kitti_pair, s12, th):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     from sqrtlm.orb import Frame, ORBmatcher
     k1, d1, k2, d2, bounds = kitti_pair
     cam = S.camera(1241, 376)

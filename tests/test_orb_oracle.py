@@ -485,7 +485,7 @@ def _py_sbp_last(kps, desc, bounds, scale, cam, uright, slot_mp, slot_obs, Tcw, 
 
 @pytest.fixture(scope="module")
 def proj_scene(OB):
-    import orb_scene as S
+    from sqrtlm import orb_scene as S
     a, b = synth.make_image_pair(640, 300, seed=21, shift=(6.0, -2.0))
     p = OB.params(800)
     k1, d1 = OB.extract(p, a)
