@@ -508,13 +508,25 @@ def main():
     # SQLM_BENCH_ONE_GPU=1 puts every rank on GPU 0 (1-GPU rehearsal of the RCCL transport)
     one_gpu = args.comm == "host" or os.environ.get("SQLM_BENCH_ONE_GPU") == "1"
     ctx = Context(0 if one_gpu else local_rank)
+    comm_used = "none" if world == 1 else args.comm
     if world > 1 and args.comm == "rccl":
         import torch
-        from sqrtlm._lib import lib
+        from sqrtlm._lib import lib, SqlmError
         uid = comm_unique_id() if rank == 0 else bytes(lib().sqlm_comm_id_size())
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
-        ctx.set_comm(bytes(t.tolist()), rank, world)
+        ok = torch.tensor([1], dtype=torch.int32)
+        try:
+            ctx.set_comm(bytes(t.tolist()), rank, world)
+        except SqlmError as err:  # every rank switches together: the exchange is collective
+            print(f"rank {rank}: RCCL communicator failed ({err}); using the host transport", file=sys.stderr)
+            ok[0] = 0
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok[0]) == 0:
+            ctx.close()
+            ctx = Context(0 if one_gpu else local_rank)
+            ctx.set_host_comm(rank, world, _gloo_allreduce, _gloo_p2p)
+            comm_used = "host (RCCL communicator init failed)"
     elif world > 1:
         ctx.set_host_comm(rank, world, _gloo_allreduce, _gloo_p2p)
     ctx.set_problem(local)
@@ -579,7 +591,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (repo generator, SplitMix64 seed; inputs rounded through float32 like the reference)",
-            "config": dict(desc, parallelism=f"landmark-shard x{world}"),
+            "config": dict(desc, parallelism=f"landmark-shard x{world}", comm=comm_used),
             "trials_per_step": st["trials"] / max(1, st["iterations"]),
             "final_rmse_px": None,
             "chi2_first": st["trace_chi2"][0] if st["trace_chi2"] else None,
