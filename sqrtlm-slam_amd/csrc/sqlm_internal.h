@@ -240,7 +240,7 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
 // band, the rest a dense border — and only the blocks the factor fills are
 // touched (band = 0: fully dense).
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
-                           hipStream_t st, int band = 0);
+                           hipStream_t st, int band = 0, int n_last = 0);
 // Block-tridiagonal SPD solve with R right-hand sides by cyclic reduction:
 // D / E [p][n][n] (D_I lower, E_I = S(I, I+1)), G [p][n][R] right-hand sides
 // (overwritten), X [p][n][R] solution; A, C, Z scratch of the same shapes, gs /

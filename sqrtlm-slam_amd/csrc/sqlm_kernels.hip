@@ -1337,8 +1337,11 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st) {
 // tile, and the per-observation gathers read LDS instead of L2. Tiles whose
 // window is wider (loop-closure landmarks) read the global arrays.
 constexpr int kUpdWin = 64;
+#ifndef SQLM_UPD_OCC
+#define SQLM_UPD_OCC 1
+#endif
 template <int W, bool ST, bool SPEC>
-__global__ __launch_bounds__(256) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
+__global__ __launch_bounds__(256, SQLM_UPD_OCC) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
                                                          double lambda, int part_off, const int2 *rng) {
   __shared__ double red[4];
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];

@@ -809,27 +809,31 @@ struct DenseView {
   int *flags;
 };
 
-__global__ __launch_bounds__(512) void k_dchol_diag(DenseView v, int k) {
+// nk: rows of the block that are not identity padding (a multiple of 16; the
+// ragged last block of a padded system): only those are factored, the rest of
+// Linv is the identity — the same bits as factoring the padded block.
+__global__ __launch_bounds__(512) void k_dchol_diag(DenseView v, int k, int nk) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int fail;
   constexpr int nb = kCRMaxN;
   const int ld = nb + 1, nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double *L = lds, *tmp = lds + nb * ld, *Dinv = tmp + 2 * nb, *W = Dinv + 17 * nb, *invd = W + 17 * nb;
   const double *Ak = v.A + (size_t)k * nb * v.n + (size_t)k * nb;
-  for (int r = wave; r < nb; r += nw)
-    for (int c = lane; c < nb; c += 64)
+  for (int r = wave; r < nk; r += nw)
+    for (int c = lane; c < nk; c += 64)
       if (c <= (r | 15)) L[r * ld + c] = Ak[(size_t)r * v.n + c];
   __syncthreads();
-  if (!wg_potrf_trtri(L, ld, nb, Dinv, W, invd, &fail) && threadIdx.x == 0) v.flags[0] = 0;
+  if (!wg_potrf_trtri(L, ld, nk, Dinv, W, invd, &fail) && threadIdx.x == 0) v.flags[0] = 0;
   double *Lo = v.Linv + (size_t)k * nb * nb;
   for (int r = wave; r < nb; r += nw)
-    for (int c = lane; c < nb; c += 64) Lo[r * nb + c] = linv_at(L, ld, Dinv, r, c);
+    for (int c = lane; c < nb; c += 64)
+      Lo[r * nb + c] = (r < nk && c < nk) ? linv_at(L, ld, Dinv, r, c) : (r == c ? 1.0 : 0.0);
   // fused forward step: y_k = Linv_kk r_k (r_k already holds every earlier
   // block's update) into x_k; thread (row, quarter), quarters summed in order
   constexpr int q = nb / 4;
   const int t = threadIdx.x, row = t % nb, h = t / nb;
   const double *rk = v.r + (size_t)k * nb;
-  if (h < 4) {
+  if (h < 4 && row < nk) {
     double s = 0.0;
 #pragma unroll 4
     for (int i = 0; i < q; ++i) {
@@ -837,6 +841,8 @@ __global__ __launch_bounds__(512) void k_dchol_diag(DenseView v, int k) {
       if (m <= row) s += linv_at(L, ld, Dinv, row, m) * rk[m];
     }
     W[h * nb + row] = s;
+  } else if (h < 4) {
+    W[h * nb + row] = h == 0 ? rk[row] : 0.0;  // identity row
   }
   __syncthreads();
   if (t < nb) v.x[(size_t)k * nb + t] = ((W[t] + W[nb + t]) + W[2 * nb + t]) + W[3 * nb + t];
@@ -1058,9 +1064,10 @@ __global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k, in
 }
 
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
-                           hipStream_t st, int band) {
+                           hipStream_t st, int band, int n_last) {
   constexpr int nb = kCRMaxN, nt = nb / 16;
   if (n <= 0 || n % nb) return -1;
+  if (n_last <= 0 || n_last > nb || n_last % 16) n_last = nb;
   const int nblk = n / nb;
   band = std::max(0, std::min(band, nblk));
   DenseView v{n, nblk, A, L, Linv, r, x, flags};
@@ -1069,7 +1076,7 @@ int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double
   // forms y_k = Linv_kk r_k, then the panel, the trailing update and
   // r_i -= L_ik y_k for the rows below
   for (int k = 0; k < nblk; ++k) {
-    hipLaunchKernelGGL(k_dchol_diag, dim3(1), dim3(512), lds, st, v, k);
+    hipLaunchKernelGGL(k_dchol_diag, dim3(1), dim3(512), lds, st, v, k, k == nblk - 1 ? n_last : nb);
     const RowSet rs = rows_below(k, nblk, band);
     const int m = rs.count();
     if (m == 0) continue;
@@ -1431,7 +1438,8 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
     hipLaunchKernelGGL(k_arw_gram, dim3(xcd_grid(lt)), dim3(64), 0, st, a, elim, pl.elim_cnt, d.bd_A, pl.Rp, lt);
     hipLaunchKernelGGL(k_arw_gvec, dim3(R / 16), dim3(64), 0, st, a, elim, pl.elim_cnt, d.bd_r);
   }
-  launch_dense_spd_solve(d.bd_A, d.bd_L, d.bd_Linv, d.bd_r, d.bd_x, d.flags, pl.Rp, st);
+  // the border's last block holds R - (Rp - kCRMaxN) real rows (identity padding after them)
+  launch_dense_spd_solve(d.bd_A, d.bd_L, d.bd_Linv, d.bd_r, d.bd_x, d.flags, pl.Rp, st, 0, R - (pl.Rp - kCRMaxN));
   // x_b = P L^-T (w - W x_c)
   if (pl.elim_cnt)
     hipLaunchKernelGGL(k_arw_correct, dim3((pl.elim_cnt * n + 3) / 4), dim3(256), 0, st, a, elim, pl.elim_cnt, d.bd_x);
