@@ -105,6 +105,7 @@ struct sqlm_ctx {
   bool lin_valid = false;          // the current buffers hold the linearization at the current state
   bool spec_outstanding = false;   // a speculative camera pass may still run on the side stream
   hipEvent_t ev_spec_fork = nullptr, ev_spec_join = nullptr;
+  TileStreams tiles;  // RCS tile classes run on stream + these two
   hipEvent_t ev_cam[2][2] = {};    // timing of the speculative camera passes (ping-pong)
   bool cam_pending[2] = {false, false};
   int cam_par = 0;
@@ -191,7 +192,7 @@ enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
   B_OBSLM, B_OBSCAM, B_OBSCAMH, B_OBSUV, B_OBSINFO, B_OBSDELTA, B_OBSS, B_OBSP, B_OBSJP, B_OBSERR, B_CAMPTR, B_CAMOBS, B_CAMSLOT, B_CAMUV, B_SROWIDX,
   B_HPP, B_BP, B_LIDPTR, B_LIDDATA, B_LIDPOSE, B_LIDERR, B_SROW, B_SCOL, B_S, B_G, B_DX, B_DENSE, B_PART,
-  B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS,
+  B_SCAL, B_MAXD, B_FLAGS, B_CRD, B_CRE, B_CRA, B_CRC, B_CRG, B_CRX, B_LMRP, B_TLM, B_TCAMP, B_TCAMS, B_TORDER,
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
@@ -210,6 +211,8 @@ struct TilePlan {
   std::vector<int64_t> part_ptr{0}, gpart_ptr{0};
   int max_cp = 0;
   bool dups = false;
+  std::vector<int> order;  // tile ids grouped by nt class (ascending id within a class)
+  int cls_off[kTileNtMax + 2] = {}, cls_cnt[kTileNtMax + 1] = {};
 };
 
 // fn(t) for t = 0 .. nth-1 on nth host threads (t = 0 on the caller's)
@@ -349,6 +352,27 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
     tp.cam_ptr.push_back(tp.cam_ptr.back() + cp);
     tp.lm_ptr.push_back(tstart[t + 1]);
     tp.max_cp = std::max(tp.max_cp, cp);
+  }
+  {  // launch classes by accumulator width
+    std::vector<int> cls(nt);
+    for (int t = 0; t < nt; ++t) {
+      const int w = (6 * (int)out[t].cams.size() + 15) / 16;
+      cls[t] = std::min(std::max(w, 3), kTileNtMax);  // narrowest compiled class: 3
+      tp.cls_cnt[cls[t]]++;
+    }
+    tp.cls_off[0] = 0;
+    for (int k = 0; k <= kTileNtMax; ++k) tp.cls_off[k + 1] = tp.cls_off[k] + tp.cls_cnt[k];
+    tp.order.assign(std::max(nt, 1), 0);
+    std::vector<int> f(tp.cls_off, tp.cls_off + kTileNtMax + 1);
+    for (int t = 0; t < nt; ++t) tp.order[f[cls[t]]++] = t;
+  }
+  if (std::getenv("SQLM_PREP_TIMING")) {  // window widths of the tiles (cameras), for the NT classes
+    int hist[kTileHardCams + 2] = {0};
+    for (int t = 0; t < nt; ++t) hist[std::min((int)out[t].cams.size(), kTileHardCams + 1)]++;
+    std::fprintf(stderr, "sqlm tiles: %d, cameras per window:", nt);
+    for (int c = 0; c <= kTileHardCams + 1; ++c)
+      if (hist[c]) std::fprintf(stderr, " %d:%d", c, hist[c]);
+    std::fprintf(stderr, "\n");
   }
   auto csr = [](const std::vector<Red> &v, int nkeys, std::vector<int> &ptr, std::vector<int2> &idx) {
     ptr.assign(nkeys + 1, 0);
@@ -868,6 +892,8 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_LMM, 8 * (size_t)nL, d.lm_M);
   AL(B_LMV, 4 * (size_t)nL, d.lm_v);
   d.n_tiles = c->use_tiles ? (int)tp.lm_ptr.size() - 1 : 0;
+  std::copy(tp.cls_off, tp.cls_off + kTileNtMax + 2, d.tile_cls_off);
+  std::copy(tp.cls_cnt, tp.cls_cnt + kTileNtMax + 1, d.tile_cls_cnt);
   d.tile_dups = tp.dups ? 1 : 0;
   {
     int mk = 0;
@@ -878,6 +904,7 @@ int prepare(sqlm_ctx *c, int level) {
   if (c->use_tiles) {
     UP(B_TLM, tp.lm_ptr, d.tile_lm_ptr);
     UP(B_TCAMP, tp.cam_ptr, d.tile_cam_ptr);
+    UP(B_TORDER, tp.order, d.tile_order);
     UP(B_TCAMS, tp.cams, d.tile_cams);
     UP(B_TPART, tp.part_ptr, d.tile_part_ptr);
     UP(B_TGPART, tp.gpart_ptr, d.tile_gpart_ptr);
@@ -1153,7 +1180,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   launch_damp(d, lambda, c->stream);
   tmark(c, 2, true);
   tmark(c, 3, false);
-  if (c->use_tiles) launch_rcs_tiles(d, lambda, c->tile_max_cp, c->tile_max_k, c->stream);
+  if (c->use_tiles) launch_rcs_tiles(d, lambda, c->tile_max_cp, c->tile_max_k, c->stream, &c->tiles);
   else launch_rcs(d, lambda, c->max_row_blocks, c->stream);
   tmark(c, 3, true);
   tmark(c, 8, false);
@@ -1452,7 +1479,12 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_spec_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_spec_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_spec_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->tiles.s[0], hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->tiles.s[1], hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->tiles.fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&c->tiles.join[0], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&c->tiles.join[1], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
     sqlm_ctx_destroy(c);
     return SQLM_ERR_HIP;
   }
@@ -1478,6 +1510,10 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_spec_fork) (void)hipEventDestroy(c->ev_spec_fork);
   if (c->ev_spec_join) (void)hipEventDestroy(c->ev_spec_join);
+  for (hipStream_t &x : c->tiles.s)
+    if (x) (void)hipStreamDestroy(x);
+  for (hipEvent_t x : {c->tiles.fork, c->tiles.join[0], c->tiles.join[1]})
+    if (x) (void)hipEventDestroy(x);
   for (auto &pr : c->ev_cam)
     for (auto &e : pr)
       if (e) (void)hipEventDestroy(e);

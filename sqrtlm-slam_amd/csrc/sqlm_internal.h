@@ -8,6 +8,9 @@
 
 namespace sqlm {
 
+constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
+constexpr int kTileNtMax = (6 * kTileHardCams + 15) / 16;  // widest tile class (9)
+
 constexpr int kBlock = 256;
 
 // HBM layout of one optimize() call. Everything is FP64 except indices.
@@ -84,6 +87,10 @@ struct DevProblem {
   double *dense_r = nullptr, *dense_x = nullptr;  // [n_pad]
   // tiled RCS assembly (landmark tiles with a small camera window)
   int n_tiles = 0;
+  // tiles grouped by accumulator width nt = ceil(6 cp / 16) (one launch per
+  // class, compiled for that width); tile_order[cls_off[nt] ..] = their ids
+  int *tile_order = nullptr;
+  int tile_cls_off[kTileNtMax + 2] = {}, tile_cls_cnt[kTileNtMax + 1] = {};
   int *tile_lm_ptr = nullptr;               // [T+1] landmark slot ranges
   int *tile_cam_ptr = nullptr;              // [T+1] into tile_cams / g partials
   int *tile_cams = nullptr;                 // free hidx, sorted within a tile
@@ -219,13 +226,18 @@ void launch_gather_add(const DevProblem &d, const GatherTab &t, hipStream_t st);
 void launch_flag_pack(const DevProblem &d, bool unpack, hipStream_t st);
 void launch_damp(const DevProblem &d, double lambda, hipStream_t st);
 void launch_rcs(const DevProblem &d, double lambda, int max_row_blocks, hipStream_t st);
-void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st);
+// extra streams for the RCS tile classes (null: everything on st)
+struct TileStreams {
+  hipStream_t s[2] = {nullptr, nullptr};
+  hipEvent_t fork = nullptr, join[2] = {nullptr, nullptr};
+};
+void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st,
+                      const TileStreams *ts = nullptr);
 void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st);
 #ifdef SQLM_TILE_PROF
 int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase counters
 #endif
 constexpr int kRedLong = 24;
-constexpr int kTileMaxCams = 24, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);  // zeroes + scatters unless cr_direct
 // band + border layout: clear F^T / the border system before S is assembled into it

@@ -900,8 +900,20 @@ __device__ __forceinline__ void tile_mfma_wave(int wave, d4v *acc, const double 
   tile_mfma<NT, P>(acc, Y, tmin, tmax, nks, r16, k4);
 }
 
+// occupancy the mono kernel of width NT is compiled for (its accumulators and
+// LDS shrink with NT, so the narrower classes fit more workgroups per CU)
+#ifndef SQLM_TILE_OCC_NARROW
+#define SQLM_TILE_OCC_NARROW 5
+#endif
+#ifndef SQLM_TILE_OCC_MID
+#define SQLM_TILE_OCC_MID 4
+#endif
+template <int NT>
+constexpr int tile_occ() { return NT <= 4 ? SQLM_TILE_OCC_NARROW : NT <= 6 ? SQLM_TILE_OCC_MID : kTileOcc; }
+
 template <int NT, bool ST>
-__global__ __launch_bounds__(kTileThreads, ST ? 2 : kTileOcc) void k_rcs_tile(DevProblem d, double lambda) {
+__global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_tile(DevProblem d, double lambda,
+                                                                                   int cls_off) {
   // wave w owns the accumulator tiles q with q % kTileWaves == w; 3 waves per SIMD
   // for mono problems (167 VGPRs), 2 with the stereo row (spill-free)
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
@@ -916,7 +928,7 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : kTileOcc) void k_rcs_tile(De
   __shared__ double Lx[kTileMaxLm][3];            // landmarks at the linearization point
   __shared__ double Lc[kTileMaxCams][16];         // window cameras: R t fx fy cx cy
   __shared__ double Lbf[ST ? kTileMaxCams : 1];   // window cameras: bf (stereo edges)
-  const int t = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int t = d.tile_order[cls_off + blockIdx.x], tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
   const int ncol = 6 * cp, nt = (ncol + 15) >> 4;
   const int r16 = lane & 15, k4 = lane >> 4;
@@ -1219,21 +1231,42 @@ __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double
   }
 }
 
-void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st) {
+void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st,
+                      const TileStreams *ts) {
   if (d.nP == 0) return;
   (void)max_k;
-  const int nt = (6 * max_cp + 15) / 16;
+  (void)max_cp;
   if (d.n_tiles > 0) {
-#define SQLM_TILE(NTT)                                                                            \
-  do {                                                                                            \
-    if (d.has_stereo) hipLaunchKernelGGL((k_rcs_tile<NTT, true>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d, lambda); \
-    else hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(d.n_tiles), dim3(kTileThreads), 0, st, d, lambda);    \
+    // one launch per accumulator-width class; the classes go to three streams
+    // (wide on st, middle and narrow on the two tile streams) so that no
+    // launch's tail leaves the chip idle
+    const bool par = ts && ts->s[0] && ts->s[1];
+    if (par) {
+      (void)hipEventRecord(ts->fork, st);
+      (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
+      (void)hipStreamWaitEvent(ts->s[1], ts->fork, 0);
+    }
+#define SQLM_TILE(NTT, S)                                                                                     \
+  do {                                                                                                        \
+    const int cnt = d.tile_cls_cnt[NTT], off = d.tile_cls_off[NTT];                                            \
+    if (cnt > 0) {                                                                                            \
+      if (d.has_stereo)                                                                                       \
+        hipLaunchKernelGGL((k_rcs_tile<NTT, true>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);      \
+      else                                                                                                    \
+        hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);     \
+    }                                                                                                         \
   } while (0)
-    if (nt <= 3) SQLM_TILE(3);
-    else if (nt <= 5) SQLM_TILE(5);
-    else if (nt <= 7) SQLM_TILE(7);
-    else SQLM_TILE(9);
+    const hipStream_t sm = par ? ts->s[0] : st, sn = par ? ts->s[1] : st;
+    SQLM_TILE(9, st); SQLM_TILE(8, st);
+    SQLM_TILE(7, sm); SQLM_TILE(6, sm); SQLM_TILE(5, sm);
+    SQLM_TILE(4, sn); SQLM_TILE(3, sn);
 #undef SQLM_TILE
+    if (par) {
+      (void)hipEventRecord(ts->join[0], ts->s[0]);
+      (void)hipEventRecord(ts->join[1], ts->s[1]);
+      (void)hipStreamWaitEvent(st, ts->join[0], 0);
+      (void)hipStreamWaitEvent(st, ts->join[1], 0);
+    }
   }
 }
 
