@@ -926,8 +926,8 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_t
   __shared__ double Lw[kTileMaxLm][3];
   __shared__ double Lr[kTileMaxLm][6];
   __shared__ double Lx[kTileMaxLm][3];            // landmarks at the linearization point
-  __shared__ double Lc[kTileMaxCams][16];         // window cameras: R t fx fy cx cy
-  __shared__ double Lbf[ST ? kTileMaxCams : 1];   // window cameras: bf (stereo edges)
+  __shared__ double Lc[kTileHardCams][16];        // window cameras: R t fx fy cx cy
+  __shared__ double Lbf[ST ? kTileHardCams : 1];  // window cameras: bf (stereo edges)
   const int t = d.tile_order[cls_off + blockIdx.x], tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
   const int ncol = 6 * cp, nt = (ncol + 15) >> 4;
@@ -1237,9 +1237,10 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
   (void)max_k;
   (void)max_cp;
   if (d.n_tiles > 0) {
-    // one launch per accumulator-width class; the classes go to three streams
-    // (wide on st, middle and narrow on the two tile streams) so that no
-    // launch's tail leaves the chip idle
+    // one launch per accumulator-width class (4, 6, 8, 9); the classes go to
+    // three streams so that no launch's tail leaves the chip idle: 8 (the
+    // most work) on st, 6 on the first tile stream, the few widest tiles (9,
+    // one round of long-running workgroups) then 4 on the second
     const bool par = ts && ts->s[0] && ts->s[1];
     if (par) {
       (void)hipEventRecord(ts->fork, st);
@@ -1257,9 +1258,9 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     }                                                                                                         \
   } while (0)
     const hipStream_t sm = par ? ts->s[0] : st, sn = par ? ts->s[1] : st;
-    SQLM_TILE(9, st); SQLM_TILE(8, st);
-    SQLM_TILE(7, sm); SQLM_TILE(6, sm); SQLM_TILE(5, sm);
-    SQLM_TILE(4, sn); SQLM_TILE(3, sn);
+    SQLM_TILE(8, st);
+    SQLM_TILE(6, sm);
+    SQLM_TILE(9, sn); SQLM_TILE(4, sn);
 #undef SQLM_TILE
     if (par) {
       (void)hipEventRecord(ts->join[0], ts->s[0]);
