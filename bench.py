@@ -600,7 +600,11 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "k_rcs_tile", "achieved": ach_tf,
                          "peak": MFMA_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach_tf / MFMA_F64_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": tsrc, "algorithmic_flops": flops,
-                         "launch_ms": t_rcs},
+                         "launch_ms": t_rcs,
+                         "note": "one RCS tile phase per trial = the width-class launches k_rcs_tile<8>, <6>, <9>, "
+                                 "<4> on three streams; launch_ms is the phase's wall time (HIP events on the "
+                                 "context stream around the fork and join), rocprof lists the class kernels "
+                                 "separately with overlapping durations"},
             "roofline_secondary": {"bound": "hbm", "kernel": f"{lin_kernel} (all buckets)", "achieved": achieved,
                                    "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                                    "traffic": lin_traffic, "algorithmic_bytes": alg, "launch_ms": t_lin,
