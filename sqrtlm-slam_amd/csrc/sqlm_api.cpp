@@ -355,11 +355,14 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
   }
   {  // launch classes by accumulator width
     std::vector<int> cls(nt);
+    bool any4 = false;
+    for (int t = 0; t < nt; ++t) any4 |= (6 * (int)out[t].cams.size() + 15) / 16 == 4;
     for (int t = 0; t < nt; ++t) {
-      // classes 4, 6, 8, 9 (a tile goes to the narrowest one that holds it): the
-      // odd widths hold a few dozen tiles each, too few for a launch of their own
+      // classes 3 (only when no tile needs 4: small windows, e.g. local BA), 4,
+      // 6, 8, 9 — a tile goes to the narrowest one that holds it; the odd widths
+      // hold a few dozen tiles each, too few for a launch of their own
       const int w = (6 * (int)out[t].cams.size() + 15) / 16;
-      cls[t] = w <= 4 ? 4 : w <= 6 ? 6 : w <= 8 ? 8 : kTileNtMax;
+      cls[t] = w <= 3 && !any4 ? 3 : w <= 4 ? 4 : w <= 6 ? 6 : w <= 8 ? 8 : kTileNtMax;
       tp.cls_cnt[cls[t]]++;
     }
     tp.cls_off[0] = 0;

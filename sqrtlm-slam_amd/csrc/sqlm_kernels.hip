@@ -1241,7 +1241,9 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     // three streams so that no launch's tail leaves the chip idle: 8 (the
     // most work) on st, 6 on the first tile stream, the few widest tiles (9,
     // one round of long-running workgroups) then 4 on the second
-    const bool par = ts && ts->s[0] && ts->s[1];
+    int ncls = 0;
+    for (int k = 0; k <= kTileNtMax; ++k) ncls += d.tile_cls_cnt[k] > 0;
+    const bool par = ts && ts->s[0] && ts->s[1] && ncls > 1;  // one class (small windows): no fork / join
     if (par) {
       (void)hipEventRecord(ts->fork, st);
       (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
@@ -1260,7 +1262,7 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     const hipStream_t sm = par ? ts->s[0] : st, sn = par ? ts->s[1] : st;
     SQLM_TILE(8, st);
     SQLM_TILE(6, sm);
-    SQLM_TILE(9, sn); SQLM_TILE(4, sn);
+    SQLM_TILE(9, sn); SQLM_TILE(4, sn); SQLM_TILE(3, sn);
 #undef SQLM_TILE
     if (par) {
       (void)hipEventRecord(ts->join[0], ts->s[0]);
