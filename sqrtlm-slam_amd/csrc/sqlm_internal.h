@@ -11,8 +11,11 @@ namespace sqlm {
 #ifndef SQLM_TILE_MAXCAMS
 #define SQLM_TILE_MAXCAMS 24
 #endif
+#ifndef SQLM_TILE_MAXLM
+#define SQLM_TILE_MAXLM 128
+#endif
 // tile window cap of the greedy cut (a single landmark may exceed it up to kTileHardCams)
-constexpr int kTileMaxCams = SQLM_TILE_MAXCAMS, kTileHardCams = 24, kTileMaxLm = 128, kTileMaxK = 1 << 20;
+constexpr int kTileMaxCams = SQLM_TILE_MAXCAMS, kTileHardCams = 24, kTileMaxLm = SQLM_TILE_MAXLM, kTileMaxK = 1 << 20;
 constexpr int kTileNtMax = (6 * kTileHardCams + 15) / 16;  // widest tile class (9)
 
 constexpr int kBlock = 256;

@@ -908,8 +908,13 @@ __device__ __forceinline__ void tile_mfma_wave(int wave, d4v *acc, const double 
 #ifndef SQLM_TILE_OCC_MID
 #define SQLM_TILE_OCC_MID 4
 #endif
+#ifndef SQLM_TILE_OCC_WIDE8
+#define SQLM_TILE_OCC_WIDE8 3
+#endif
 template <int NT>
-constexpr int tile_occ() { return NT <= 4 ? SQLM_TILE_OCC_NARROW : NT <= 6 ? SQLM_TILE_OCC_MID : kTileOcc; }
+constexpr int tile_occ() {
+  return NT <= 4 ? SQLM_TILE_OCC_NARROW : NT <= 6 ? SQLM_TILE_OCC_MID : NT <= 8 ? SQLM_TILE_OCC_WIDE8 : kTileOcc;
+}
 
 template <int NT, bool ST>
 __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_tile(DevProblem d, double lambda,
