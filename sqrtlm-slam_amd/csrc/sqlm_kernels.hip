@@ -1327,7 +1327,10 @@ int launch_dense_solve(const DevProblem &d, hipStream_t st) {
   if (hipMemsetAsync(d.dense, 0, sizeof(double) * nn, st) != hipSuccess) return -2;
   const int64_t items = d.nnzb * 36 + d.dense_n;
   hipLaunchKernelGGL(k_dense_scatter, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, st, d);
-  if (launch_dense_spd_solve(d.dense, d.dense_L, d.dense_Linv, d.dense_r, d.dense_x, d.flags, d.dense_n, st))
+  // the last block's real rows (16-rounded; identity padding after them is not factored)
+  const int n_last = ((n - (d.dense_n - kCRMaxN)) + 15) / 16 * 16;
+  if (launch_dense_spd_solve(d.dense, d.dense_L, d.dense_Linv, d.dense_r, d.dense_x, d.flags, d.dense_n, st, 0,
+                             n_last))
     return -2;
   hipLaunchKernelGGL(k_dense_copy_dx, dim3((n + 255) / 256), dim3(256), 0, st, d);
   return 0;
