@@ -654,7 +654,10 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
         if (c.nb > 0) {
           if (launch_batched_atb(c.Go, c.X, c.P, c.p, c.n, c.R, st)) return SQLM_ERR_HIP;
           hipLaunchKernelGGL(k_egcr_schur, dim3((c.nb * (c.nb + 1) + 255) / 256), dim3(256), 0, st, c);
-          if (launch_dense_spd_solve(c.Sc, c.ScL, c.ScLinv, c.rc, c.xc, flags, c.nc, st, 0)) return SQLM_ERR_HIP;
+          // the border complement's last block holds nb - (nc - kCRMaxN) real rows (identity after them)
+          const int n_last = ((c.nb - (c.nc - kCRMaxN)) + 15) / 16 * 16;
+          if (launch_dense_spd_solve(c.Sc, c.ScL, c.ScLinv, c.rc, c.xc, flags, c.nc, st, 0, n_last))
+            return SQLM_ERR_HIP;
         }
         hipLaunchKernelGGL(k_egcr_final, dim3((n_pad + 255) / 256), dim3(256), 0, st, d, c, x);
       } else {
