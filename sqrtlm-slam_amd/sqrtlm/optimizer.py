@@ -104,12 +104,16 @@ class Context:
         return dict(kind=kind, B=out[1], p=out[2], n=out[3], border_cams=out[4], R=out[5], n_free=out[6],
                     coupled_superblocks=out[7])
 
-    def bench(self, warmup: int, n: int):
+    def bench(self, warmup: int, n: int, timers: bool = True):
+        """(ms per LM iteration, per-phase ms from HIP events or {} without
+        timers, stats). timers=False runs without the phase events."""
         ms = C.c_double(0)
         kms = np.zeros(_lib.NKERNEL_TIMERS)
         st = _lib.Stats()
-        check(lib().sqlm_bench_iterations(self._h, int(warmup), int(n), C.byref(ms), ptr(kms), C.byref(st)),
-              "sqlm_bench_iterations")
+        check(lib().sqlm_bench_iterations(self._h, int(warmup), int(n), C.byref(ms), ptr(kms) if timers else None,
+                                          C.byref(st)), "sqlm_bench_iterations")
+        if not timers:
+            return ms.value, {}, st.as_dict()
         names = [lib().sqlm_kernel_timer_name(i).decode() for i in range(_lib.NKERNEL_TIMERS)]
         return ms.value, dict(zip(names, kms.tolist())), st.as_dict()
 
