@@ -49,6 +49,24 @@ def test_optimize_local_window(gpu_ctx, oracle, seed):
     np.testing.assert_allclose(gpu_ctx.edge_chi2(), ref.edge_chi2(), rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("n_pose", [9, 16, 28, 43, 48])
+def test_small_rcs_superblock_counts(gpu_ctx, oracle, n_pose):
+    """Local-BA-sized reduced camera systems of 2, 3, 5, 8 and 9 superblocks
+    (cyclic reduction with 1..4 levels, odd and even counts) against the
+    oracle's Cholesky (linear_solver_eigen.h:94-124)."""
+    prob = synth.make_problem(n_pose, 50 * n_pose, pair_window=4, n_fixed=3, seed=100 + n_pose, robust=True)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(0, 10)
+    gpu_ctx.set_problem(prob)
+    ng, sg = gpu_ctx.optimize(0, 10)
+    lay = gpu_ctx.rcs_layout()
+    assert lay["kind"] == "band" and lay["p"] >= 2
+    print(f"n_pose {n_pose}: {lay['p']} superblocks of {lay['B']} cameras")
+    assert ng == nr
+    _compare_stats(sg, sr)
+    _compare_state(gpu_ctx, ref)
+
+
 def test_global_ba_variable_track(gpu_ctx, oracle):
     prob = synth.config4(scale=0.01, seed=4)
     ref = oracle.OracleGraph(prob)
