@@ -722,22 +722,32 @@ int prepare(sqlm_ctx *c, int level) {
   }
   // pose id window of every per-landmark block tile (k_landmark_update)
   std::vector<int2> upd_rng;
-  for (Bucket &b : c->buckets) {
-    b.rng_off = (int)upd_rng.size();
-    const int spb = kBlock / b.W;
-    for (int s0 = b.slot_begin; s0 < b.slot_end; s0 += spb) {
-      const int s1 = std::min(s0 + spb, b.slot_end);
-      int lo = std::numeric_limits<int>::max(), hi = -1;
-      for (int o = lm_begin[s0]; o < lm_begin[s1]; ++o) { lo = std::min(lo, obs_cam[o]); hi = std::max(hi, obs_cam[o]); }
-      upd_rng.push_back(hi < 0 ? int2{1, 0} : int2{lo, hi});
+  {  // block slot ranges in bucket order, then their pose windows on host threads
+    std::vector<int2> blk_slots;
+    for (Bucket &b : c->buckets) {
+      b.rng_off = (int)blk_slots.size();
+      const int spb = kBlock / b.W;
+      for (int s0 = b.slot_begin; s0 < b.slot_end; s0 += spb) blk_slots.push_back(int2{s0, std::min(s0 + spb, b.slot_end)});
     }
+    const size_t nb = blk_slots.size();
+    upd_rng.resize(nb);
+    par([&](int t) {
+      for (size_t k = nb * t / nth; k < nb * (t + 1) / nth; ++k) {
+        int lo = std::numeric_limits<int>::max(), hi = -1;
+        for (int o = lm_begin[blk_slots[k].x]; o < lm_begin[blk_slots[k].y]; ++o) {
+          lo = std::min(lo, obs_cam[o]);
+          hi = std::max(hi, obs_cam[o]);
+        }
+        upd_rng[k] = hi < 0 ? int2{1, 0} : int2{lo, hi};
+      }
+    });
   }
   // reduced-camera-system pattern (upper, diagonal first)
   std::vector<int> s_row(nP + 1, 0), s_col;
   {
     std::vector<std::vector<int>> rows(nP);
     {  // rows are independent: a few host threads, each with its own marks
-      const int nth = std::min(8, host_threads(nE));
+      const int nth = host_threads(nE);
       auto work = [&](int t0) {
         std::vector<int> mark(nP, -1), row;
         for (int i = t0; i < nP; i += nth) {
