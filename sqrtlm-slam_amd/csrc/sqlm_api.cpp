@@ -248,6 +248,14 @@ void par_assign(std::vector<T> &v, const T *src, size_t n) {
 void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *obs_camh,
                  const std::vector<int> &s_row, const std::vector<int> &s_col, int lm_cap, TilePlan &tp) {
   const int64_t nE = lm_begin[nL];
+  const bool ptime = std::getenv("SQLM_PREP_TIMING") != nullptr;
+  auto pt0 = std::chrono::steady_clock::now();
+  auto sub = [&](const char *what) {  // sub-phases of "tiles" (SQLM_PREP_TIMING=1)
+    if (!ptime) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "  tiles %-14s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - pt0).count());
+    pt0 = now;
+  };
   tp.obs_local.assign(nE, -1);
   tp.urange.assign(nL, int2{-1, -1});
   // pass 1 (greedy): tile boundaries -- a tile closes before the landmark that
@@ -293,6 +301,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
     if (nL > 0) tstart.push_back(nL);
     else tstart.assign(1, 0);
   }
+  sub("pass 1");
   const int nt = (int)tstart.size() - 1;
   // pass 2 (tiles on host threads): window cameras, local camera of every
   // observation, landmark spans, and the S blocks each tile contributes to
@@ -337,6 +346,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
       for (int u = 0; u < cp; ++u) lidx[cur[u]] = -1;
     }
   });
+  sub("pass 2");
   // pass 3 (tile order): offsets, camera lists, the reduction lists
   std::vector<Red> red, gred;
   for (int t = 0; t < nt; ++t) {
@@ -379,6 +389,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
       if (hist[c]) std::fprintf(stderr, " %d:%d", c, hist[c]);
     std::fprintf(stderr, "\n");
   }
+  sub("pass 3");
   auto csr = [](const std::vector<Red> &v, int nkeys, std::vector<int> &ptr, std::vector<int2> &idx) {
     ptr.assign(nkeys + 1, 0);
     for (auto &r : v) ptr[r.key + 1]++;
@@ -399,6 +410,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
     if (tp.red_ptr[s + 1] - tp.red_ptr[s] > kRedLong) tp.long_s.push_back(s);
   for (int i = 0; i < nP; ++i)
     if (tp.gred_ptr[i + 1] - tp.gred_ptr[i] > kRedLong) tp.long_g.push_back(i);
+  sub("reduction csr");
 }
 
 // Reduced-camera-system solver plan from the upper block pattern of S (hidx
