@@ -175,6 +175,16 @@ void sqlm_pose_to_Tcw_f32(const double q[4], const double t[3], float T[16]);
 int sqlm_comm_id_size(void);
 int sqlm_comm_get_unique_id(char *id_out);
 int sqlm_ctx_set_comm(sqlm_ctx *ctx, const char *unique_id, int rank, int nranks);
+/* RCCL transport checks on ONE GPU (no reference counterpart; test hooks).
+ * sqlm_ctx_set_comm_selfloop: a one-rank RCCL communicator on which the
+ * context takes the sharded code path (every all-reduce, the rank-0 gather and
+ * the dx broadcast run through RCCL with one rank).
+ * sqlm_comm_selftest: on `device`, a one-rank communicator drives the three
+ * exchange primitives — a grouped send/recv to self of `count` doubles, an
+ * in-place broadcast and sum / max all-reduces (f64, i32, u8) — and writes
+ * the largest deviation from the expected buffers to *max_err. */
+int sqlm_ctx_set_comm_selfloop(sqlm_ctx *ctx, const char *unique_id);
+int sqlm_comm_selftest(int device, const char *unique_id, int64_t count, double *max_err);
 
 /* Same sharded algorithm over a caller-provided host collective (for example
  * torch.distributed gloo): the library stages each exchange through host

@@ -50,6 +50,7 @@ struct sqlm_ctx {
   hipStream_t stream = nullptr;
   // ---- host copy of the graph (caller order) ----
   bool has_problem = false;
+  bool prepared = false;  // the last prepare() completed (CR plan, buffers valid)
   int n_pose = 0, n_pt = 0;
   int64_t n_obs = 0, n_lid = 0;
   std::vector<double> pose_q, pose_t, intr, pt;
@@ -196,7 +197,7 @@ enum BufId {
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
-  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG
+  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL
 };
 
 // Landmark tiles for the RCS assembly: runs of consecutive slots whose free
@@ -259,43 +260,50 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
   tp.obs_local.assign(nE, -1);
   tp.urange.assign(nL, int2{-1, -1});
   // pass 1 (greedy): tile boundaries -- a tile closes before the landmark that
-  // would push its window past kTileMaxCams cameras or lm_cap; the slots are
-  // cut into one chunk per host thread (a tile never crosses a chunk start)
+  // would push its window past kTileMaxCams cameras or lm_cap. The slots are
+  // cut into a number of chunks that depends on the problem only (one per
+  // 128k observations, at most 16; a tile never crosses a chunk start), so the
+  // tile plan -- and with it the fixed summation order of S -- is the same on
+  // every host; the chunks are then dealt to however many threads there are.
   std::vector<int> tstart;
   {
-    const int nth = host_threads(nE);
-    std::vector<std::vector<int>> cuts(nth);
-    std::vector<uint8_t> dup(nth, 0);
+    const int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>(16, nE / 131072));
+    const int nth = std::min(nchunk, host_threads(nE));
+    std::vector<std::vector<int>> cuts(nchunk);
+    std::vector<uint8_t> dup(nchunk, 0);
     run_threads(nth, [&](int th) {
-      const int s0 = (int)((int64_t)nL * th / nth), s1 = (int)((int64_t)nL * (th + 1) / nth);
       std::vector<int> stamp(nP, -1), lmst(nP, -1);
-      std::vector<int> &cv = cuts[th];
-      int t = 0, ncur = 0, cur_lm = 0;
-      for (int sl = s0; sl < s1; ++sl) {
-        int nnew = 0;
-        for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
-          const int h = obs_camh[o];
-          if (h < 0) continue;
-          if (lmst[h] == sl) { dup[th] = 1; continue; }
-          lmst[h] = sl;
-          if (stamp[h] != t) ++nnew;
+      for (int ch = th; ch < nchunk; ch += nth) {
+        const int s0 = (int)((int64_t)nL * ch / nchunk), s1 = (int)((int64_t)nL * (ch + 1) / nchunk);
+        std::vector<int> &cv = cuts[ch];
+        int t = 0, ncur = 0, cur_lm = 0;
+        std::fill(stamp.begin(), stamp.end(), -1);
+        for (int sl = s0; sl < s1; ++sl) {
+          int nnew = 0;
+          for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+            const int h = obs_camh[o];
+            if (h < 0) continue;
+            if (lmst[h] == sl) { dup[ch] = 1; continue; }
+            lmst[h] = sl;
+            if (stamp[h] != t) ++nnew;
+          }
+          if (cur_lm == 0 || ncur + nnew > kTileMaxCams || cur_lm >= lm_cap) {
+            cv.push_back(sl);
+            ++t;
+            ncur = 0;
+            cur_lm = 0;
+          }
+          for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
+            const int h = obs_camh[o];
+            if (h >= 0 && stamp[h] != t) { stamp[h] = t; ++ncur; }
+          }
+          ++cur_lm;
         }
-        if (cur_lm == 0 || ncur + nnew > kTileMaxCams || cur_lm >= lm_cap) {
-          cv.push_back(sl);
-          ++t;
-          ncur = 0;
-          cur_lm = 0;
-        }
-        for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
-          const int h = obs_camh[o];
-          if (h >= 0 && stamp[h] != t) { stamp[h] = t; ++ncur; }
-        }
-        ++cur_lm;
       }
     });
-    for (int th = 0; th < nth; ++th) {
-      tstart.insert(tstart.end(), cuts[th].begin(), cuts[th].end());
-      if (dup[th]) tp.dups = true;
+    for (int ch = 0; ch < nchunk; ++ch) {
+      tstart.insert(tstart.end(), cuts[ch].begin(), cuts[ch].end());
+      if (dup[ch]) tp.dups = true;
     }
     if (tstart.empty() || tstart[0] != 0) tstart.insert(tstart.begin(), 0);
     if (nL > 0) tstart.push_back(nL);
@@ -530,6 +538,10 @@ inline bool stopped(const volatile uint8_t *s) { return s && *s; }
 // camera CSR and the upper block pattern of the reduced camera system.
 int prepare(sqlm_ctx *c, int level) {
   DevProblem &d = c->d;
+  c->prepared = false;
+  // the page-locked staging arrays are rewritten (or regrown) below: no DMA of
+  // an earlier call, finished or abandoned on an error path, may still read them
+  HIP_OK(hipStreamSynchronize(c->stream));
   // SQLM_PREP_TIMING=1: host phase times of this setup on stderr
   const bool ptime = std::getenv("SQLM_PREP_TIMING") != nullptr;
   auto pt0 = std::chrono::steady_clock::now();
@@ -1012,6 +1024,7 @@ int prepare(sqlm_ctx *c, int level) {
   if (c->cr.enabled) {
     const size_t nb = (size_t)c->cr.p * c->cr.n * c->cr.n;
     AL(B_CRD, nb, d.cr_D);
+    AL(B_CRL, nb, d.cr_L);
     AL(B_CRE, nb, d.cr_E);
     AL(B_CRA, nb, d.cr_A);
     AL(B_CRC, nb, d.cr_C);
@@ -1100,25 +1113,36 @@ int prepare(sqlm_ctx *c, int level) {
     (void)hipStreamSynchronize(c->stream);
     phase("gpu drain");
   }
+  c->prepared = true;
   return SQLM_OK;
 }
 
-void finish(sqlm_ctx *c) {
+int finish(sqlm_ctx *c) {
   DevProblem &d = c->d;
-  // device -> page-locked staging (one DMA each), then the scatter back to
-  // caller order on host threads
+  // device -> page-locked staging (one DMA each; pageable vectors if the
+  // page-locked arena cannot grow), then the scatter back to caller order on
+  // host threads
   PinVec<double> qt, X, err, err3, lerr;
-  if (pinned(c, P_RQT, 8 * (size_t)c->n_pose, qt) || pinned(c, P_RX, 4 * (size_t)d.nL, X) ||
-      pinned(c, P_RERR, 2 * (size_t)d.nE, err) || pinned(c, P_RERR3, d.obs_err3 ? (size_t)d.nE : 0, err3) ||
-      pinned(c, P_RLERR, (size_t)d.nLid, lerr))
-    return;
+  std::vector<double> fallback[5];
+  auto stage = [&](int id, size_t n, PinVec<double> &v, int k) {
+    if (pinned(c, id, n, v) == SQLM_OK) return;
+    fallback[k].resize(std::max<size_t>(n, 1));
+    v.p = fallback[k].data();
+    v.n = n;
+  };
+  stage(P_RQT, 8 * (size_t)c->n_pose, qt, 0);
+  stage(P_RX, 4 * (size_t)d.nL, X, 1);
+  stage(P_RERR, 2 * (size_t)d.nE, err, 2);
+  stage(P_RERR3, d.obs_err3 ? (size_t)d.nE : 0, err3, 3);
+  stage(P_RLERR, (size_t)d.nLid, lerr, 4);
   if (err3.size())
-    (void)hipMemcpyAsync(err3.data(), d.obs_err3, err3.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  (void)hipMemcpyAsync(qt.data(), d.pose_qt[0], qt.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  if (d.nL) (void)hipMemcpyAsync(X.data(), d.X[0], X.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  if (d.nE) (void)hipMemcpyAsync(err.data(), d.obs_err, err.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  if (d.nLid) (void)hipMemcpyAsync(lerr.data(), d.lid_err, lerr.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
-  (void)hipStreamSynchronize(c->stream);
+    HIP_OK(hipMemcpyAsync(err3.data(), d.obs_err3, err3.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipMemcpyAsync(qt.data(), d.pose_qt[0], qt.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (d.nL) HIP_OK(hipMemcpyAsync(X.data(), d.X[0], X.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (d.nE) HIP_OK(hipMemcpyAsync(err.data(), d.obs_err, err.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (d.nLid)
+    HIP_OK(hipMemcpyAsync(lerr.data(), d.lid_err, lerr.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
   for (int p = 0; p < c->n_pose; ++p) {
     for (int k = 0; k < 4; ++k) c->pose_q[4 * p + k] = qt[8 * p + k];
     for (int k = 0; k < 3; ++k) c->pose_t[3 * p + k] = qt[8 * p + 4 + k];
@@ -1134,6 +1158,7 @@ void finish(sqlm_ctx *c) {
     }
   });
   for (int64_t t = 0; t < d.nLid; ++t) c->lid_err[c->dev_lid_edge[t]] = lerr[t];
+  return SQLM_OK;
 }
 
 inline void tmark(sqlm_ctx *c, int i, bool end) {
@@ -1424,7 +1449,8 @@ int optimize_impl(sqlm_ctx *c, int level, int iterations, double user_lambda, co
   const double setup = ts.ms();
   s = run_lm(c, iterations, user_lambda, stop, st, n_iter, false);
   if (s) return s;
-  finish(c);
+  s = finish(c);
+  if (s) return s;
   if (st) st->ms_setup = setup;
   return SQLM_OK;
 }
@@ -1747,6 +1773,7 @@ int sqlm_get_edge_depth_positive(sqlm_ctx *c, uint8_t *pos) {
 
 int sqlm_get_rcs_layout(sqlm_ctx *c, int out[8]) {
   if (!c || !out) return SQLM_ERR_INVALID_ARG;
+  if (!c->has_problem || !c->prepared) return SQLM_ERR_STATE;
   const CRPlan &pl = c->cr;
   const int nP = c->d.nP;
   out[0] = nP == 0 ? 0 : !pl.enabled ? 3 : pl.R ? 2 : 1;
@@ -1806,6 +1833,80 @@ int sqlm_ctx_set_comm(sqlm_ctx *c, const char *id, int rank, int nranks) {
   return comm_init(c->comm, id, rank, nranks);
 }
 
+int sqlm_ctx_set_comm_selfloop(sqlm_ctx *c, const char *id) {
+  if (!c || !id) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  return comm_init_selfloop(c->comm, id) ? SQLM_ERR_COMM : SQLM_OK;
+}
+
+int sqlm_comm_selftest(int device, const char *id, int64_t n, double *max_err) {
+  if (!id || n <= 0 || !max_err) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(device) != hipSuccess) return SQLM_ERR_HIP;
+  Comm cm;
+  if (comm_init_selfloop(cm, id)) return SQLM_ERR_COMM;
+  hipStream_t st = nullptr;
+  double *a = nullptr, *b = nullptr;
+  int32_t *ia = nullptr;
+  uint8_t *ua = nullptr;
+  int r = SQLM_OK;
+  std::vector<double> ha(n), hb(n);
+  std::vector<int32_t> hi(n);
+  std::vector<uint8_t> hu(n);
+  for (int64_t i = 0; i < n; ++i) {
+    ha[i] = 0.5 * (double)i - 3.25;
+    hi[i] = (int32_t)(7 * i - 11);
+    hu[i] = (uint8_t)(i * 13);
+  }
+  double err = 0.0;
+  auto upd = [&](double v) { err = std::max(err, std::fabs(v)); };
+  if (hipStreamCreate(&st) != hipSuccess || hipMalloc(&a, n * 8) != hipSuccess || hipMalloc(&b, n * 8) != hipSuccess ||
+      hipMalloc(&ia, n * 4) != hipSuccess || hipMalloc(&ua, n) != hipSuccess) {
+    r = SQLM_ERR_HIP;
+  } else if (hipMemcpyAsync(a, ha.data(), n * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+             hipMemsetAsync(b, 0, n * 8, st) != hipSuccess ||
+             hipMemcpyAsync(ia, hi.data(), n * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+             hipMemcpyAsync(ua, hu.data(), n, hipMemcpyHostToDevice, st) != hipSuccess) {
+    r = SQLM_ERR_HIP;
+  } else {
+    // grouped send to self + receive from self (the rank-0 gather's RCCL group)
+    std::vector<P2POp> ops{P2POp{0, true, a, n, SQLM_DT_F64}, P2POp{0, false, b, n, SQLM_DT_F64}};
+    if (comm_group_p2p(cm, ops, st)) r = SQLM_ERR_COMM;
+    if (!r && comm_bcast_dev(cm, b, n, SQLM_DT_F64, 0, st)) r = SQLM_ERR_COMM;
+    if (!r && comm_allreduce_dev(cm, a, n, SQLM_DT_F64, SQLM_OP_SUM, st)) r = SQLM_ERR_COMM;
+    if (!r && comm_allreduce_dev(cm, a, n, SQLM_DT_F64, SQLM_OP_MAX, st)) r = SQLM_ERR_COMM;
+    if (!r && comm_allreduce_dev(cm, ia, n, SQLM_DT_I32, SQLM_OP_SUM, st)) r = SQLM_ERR_COMM;
+    if (!r && comm_allreduce_dev(cm, ua, n, SQLM_DT_U8, SQLM_OP_MAX, st)) r = SQLM_ERR_COMM;
+    double hs = 2.5;  // host-buffer all-reduce (setup-time exchanges)
+    if (!r && comm_allreduce_host(cm, &hs, 1, SQLM_DT_F64, SQLM_OP_SUM, st)) r = SQLM_ERR_COMM;
+    if (!r) upd(hs - 2.5);
+    std::vector<double> ra(n), rb(n);
+    std::vector<int32_t> ri(n);
+    std::vector<uint8_t> ru(n);
+    if (!r && (hipMemcpyAsync(ra.data(), a, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipMemcpyAsync(rb.data(), b, n * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipMemcpyAsync(ri.data(), ia, n * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipMemcpyAsync(ru.data(), ua, n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+               hipStreamSynchronize(st) != hipSuccess))
+      r = SQLM_ERR_HIP;
+    if (!r)
+      for (int64_t i = 0; i < n; ++i) {
+        upd(ra[i] - ha[i]);
+        upd(rb[i] - ha[i]);
+        upd((double)(ri[i] - hi[i]));
+        upd((double)ru[i] - (double)hu[i]);
+      }
+  }
+  if (st) (void)hipStreamSynchronize(st);
+  (void)hipFree(a);
+  (void)hipFree(b);
+  (void)hipFree(ia);
+  (void)hipFree(ua);
+  if (st) (void)hipStreamDestroy(st);
+  comm_destroy(cm);
+  *max_err = err;
+  return r;
+}
+
 int sqlm_bench_iterations(sqlm_ctx *c, int warmup, int n, double *ms_per_iter, double *kernel_ms, sqlm_stats *st) {
   if (!c || !c->has_problem || n <= 0 || warmup < 0) return SQLM_ERR_INVALID_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
@@ -1837,8 +1938,7 @@ int sqlm_bench_iterations(sqlm_ctx *c, int warmup, int n, double *ms_per_iter, d
     for (int i = 0; i < SQLM_NKERNEL_TIMERS; ++i)
       kernel_ms[i] = c->kernel_ms_n ? c->kernel_ms_acc[i] / c->kernel_ms_n : 0.0;
   }
-  finish(c);
-  return SQLM_OK;
+  return finish(c);
 }
 
 #ifdef SQLM_TILE_PROF

@@ -36,8 +36,9 @@ struct Comm {
   sqlm_p2p_fn host_p2p = nullptr;  // send / recv / broadcast for the host transport
   void *host_p2p_user = nullptr;
   int rank = 0, nranks = 1;
+  bool selfloop = false;    // a one-rank RCCL communicator that still takes the sharded path (tests)
   std::vector<char> stage;  // host staging for the callback transport
-  bool enabled() const { return nranks > 1 && (comm != nullptr || host_fn != nullptr); }
+  bool enabled() const { return (nranks > 1 || selfloop) && (comm != nullptr || host_fn != nullptr); }
 };
 
 inline int comm_id_size() { return (int)sizeof(ncclUniqueId); }
@@ -58,6 +59,7 @@ inline void comm_destroy(Comm &c) {
   c.host_p2p_user = nullptr;
   c.rank = 0;
   c.nranks = 1;
+  c.selfloop = false;
 }
 
 inline int comm_init(Comm &c, const char *idbytes, int rank, int nranks) {
@@ -71,6 +73,21 @@ inline int comm_init(Comm &c, const char *idbytes, int rank, int nranks) {
     c.comm = nullptr;
     return -9;
   }
+  return 0;
+}
+
+// A one-rank RCCL communicator on which every exchange of the sharded path
+// runs for real (all-reduces and broadcasts of one rank, the rank-0 gather
+// with no peers): the RCCL transport exercised on a one-GPU box.
+inline int comm_init_selfloop(Comm &c, const char *idbytes) {
+  comm_destroy(c);
+  ncclUniqueId id;
+  std::memcpy(&id, idbytes, sizeof(id));
+  if (ncclCommInitRank(&c.comm, 1, id, 0) != ncclSuccess) {
+    c.comm = nullptr;
+    return -9;
+  }
+  c.selfloop = true;
   return 0;
 }
 

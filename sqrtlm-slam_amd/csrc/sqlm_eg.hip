@@ -313,6 +313,7 @@ __global__ __launch_bounds__(256) void k_eg_reduce(EGDev d, int n_err_parts, int
 struct EGCR {
   int p = 0, n = 0, R = 0, nb = 0, nc = 0;
   double *D = nullptr, *E = nullptr, *A = nullptr, *Cm = nullptr, *gs = nullptr, *xs = nullptr;
+  double *L = nullptr;  // Linv_I of the factored blocks
   double *G = nullptr, *Go = nullptr, *Z = nullptr, *X = nullptr, *P = nullptr;
   double *Sc = nullptr, *ScL = nullptr, *ScLinv = nullptr, *rc = nullptr, *xc = nullptr;
 };
@@ -585,14 +586,14 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
     c.R = (nbr + 1 + 15) / 16 * 16;
     c.nc = nbr > 0 ? (nbr + kCRMaxN - 1) / kCRMaxN * kCRMaxN : kCRMaxN;
     const size_t pnn = (size_t)c.p * c.n * c.n, pnr = (size_t)c.p * c.n * c.R, ncc = (size_t)c.nc * c.nc;
-    c.D = alloc<double>(pnn); c.E = alloc<double>(pnn); c.A = alloc<double>(pnn); c.Cm = alloc<double>(pnn);
+    c.D = alloc<double>(pnn); c.L = alloc<double>(pnn); c.E = alloc<double>(pnn); c.A = alloc<double>(pnn); c.Cm = alloc<double>(pnn);
     c.gs = alloc<double>((size_t)c.p * c.n); c.xs = alloc<double>((size_t)c.p * c.n);
     c.G = alloc<double>(pnr); c.Go = alloc<double>(pnr); c.Z = alloc<double>(pnr); c.X = alloc<double>(pnr);
     c.P = alloc<double>((size_t)c.p * c.R * c.R);
     c.Sc = alloc<double>(ncc); c.ScL = alloc<double>(ncc);
     c.ScLinv = alloc<double>((size_t)(c.nc / kCRMaxN) * kCRMaxN * kCRMaxN);
     c.rc = alloc<double>(c.nc); c.xc = alloc<double>(c.nc);
-    if (!c.D || !c.E || !c.A || !c.Cm || !c.gs || !c.xs || !c.G || !c.Go || !c.Z || !c.X || !c.P || !c.Sc || !c.ScL ||
+    if (!c.D || !c.L || !c.E || !c.A || !c.Cm || !c.gs || !c.xs || !c.G || !c.Go || !c.Z || !c.X || !c.P || !c.Sc || !c.ScL ||
         !c.ScLinv || !c.rc || !c.xc)
       return SQLM_ERR_OOM;
     // the scratch right-hand side of the reused single-RHS kernels: finite values
@@ -649,7 +650,7 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
       if (use_cr) {
         const int64_t tot = (int64_t)c.p * c.n * c.n + (int64_t)c.p * c.n * c.R + (int64_t)c.nc * c.nc;
         hipLaunchKernelGGL(k_egcr_gather, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, d, c, lambda);
-        if (launch_cr_multi(c.D, c.E, c.A, c.Cm, c.gs, c.xs, c.G, c.Z, c.X, flags, c.p, c.n, c.R, st))
+        if (launch_cr_multi(c.D, c.L, c.E, c.A, c.Cm, c.gs, c.xs, c.G, c.Z, c.X, flags, c.p, c.n, c.R, st))
           return SQLM_ERR_HIP;
         if (c.nb > 0) {
           if (launch_batched_atb(c.Go, c.X, c.P, c.p, c.n, c.R, st)) return SQLM_ERR_HIP;

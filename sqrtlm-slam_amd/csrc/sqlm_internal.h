@@ -123,6 +123,7 @@ struct DevProblem {
   int tile_maxk = 0;                        // longest track (staging fast path needs <= kTileFastK = 64)
   // block-tridiagonal cyclic reduction workspace (sqlm_rcs_solve.hip)
   double *cr_D = nullptr, *cr_E = nullptr;  // [p][n][n]
+  double *cr_L = nullptr;                   // [p][n][n] Linv_I of the factored superblocks
   double *cr_A = nullptr, *cr_C = nullptr;  // [p][n][n]
   double *cr_g = nullptr, *cr_x = nullptr;  // [p][n]
   int cr_direct = 0;                        // k_rcs_reduce writes D/E/g in CR layout (no BSR S)
@@ -250,7 +251,7 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);  // 
 // band + border layout: clear F^T / the border system before S is assembled into it
 void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st);
 // CR levels + top + back substitution on blocks already in CR layout (microbench / tests)
-void launch_cr_core(double *D, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
+void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
                     hipStream_t st);
 // Dense SPD solve (sqlm_rcs_solve.hip): A (n x n, lower, n % kCRMaxN == 0) is
 // factored in place into L (+ diagonal block inverses Linv), r is consumed,
@@ -265,7 +266,7 @@ int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double
 // (overwritten), X [p][n][R] solution; A, C, Z scratch of the same shapes, gs /
 // xs [p][n] scratch. n <= kCRMaxN, n and R multiples of 16. flags[0] = 0 if a
 // pivot is not positive.
-int launch_cr_multi(double *D, double *E, double *A, double *C, double *gs, double *xs, double *G, double *Z,
+int launch_cr_multi(double *D, double *L, double *E, double *A, double *C, double *gs, double *xs, double *G, double *Z,
                     double *X, int *flags, int p, int n, int R, hipStream_t st);
 // P_I = A_I^T B_I for I < p, A_I / B_I [n][R] row-major, P_I [R][R] (R % 16 == 0).
 int launch_batched_atb(const double *A, const double *B, double *P, int p, int n, int R, hipStream_t st);

@@ -347,6 +347,7 @@ struct CRView {
   int p, n, B, nP;
   double *D, *E, *A, *C, *g, *x;  // [p][n][n] x4, [p][n] x2
   int *flags;
+  double *L;  // [p][n][n]: Linv_I of every factored superblock
 };
 
 __device__ __forceinline__ double *blk(double *base, int I, int n) { return base + (size_t)I * n * n; }
@@ -429,6 +430,10 @@ __device__ __forceinline__ void cr_factor_block(const CRView &v, int I, double *
   if (!wg_potrf_trtri(L, ld, n, Dinv, W, invd, fail) && threadIdx.x == 0) v.flags[0] = 0;
 }
 
+}  // namespace sqlm
+#include "sqlm_cr_aug.h"
+namespace sqlm {
+
 // Level h, step 1: every odd superblock I (I = h, 3h, 5h, ...) is factored:
 // D_I <- Linv_I = chol(D_I)^-1 (lower block triangle, zero above), g_I <- z_I = Linv_I g_I.
 __device__ __forceinline__ void cr_factor_store(const CRView &v, int I, double *lds, int *fail_p) {
@@ -437,7 +442,7 @@ __device__ __forceinline__ void cr_factor_store(const CRView &v, int I, double *
   const int nw = blockDim.x >> 6, wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
   cr_factor_block(v, I, lds, &fail);
   const double *L = lds, *tmp = lds + n * ld, *Dinv = tmp + 2 * n;
-  double *Dg = blk(v.D, I, n);
+  double *Dg = blk(v.L, I, n);
   {  // dense Linv, one 16x16 tile per wave step; lane: row lane/4, 4 columns
     const int r = lane >> 2, c = 4 * (lane & 3);
     for (int q = wave; q < nt * nt; q += nw) {
@@ -521,10 +526,10 @@ __device__ __forceinline__ void cr_elim_item(const CRView &v, int h, int lb) {
   const int which = rem / per, t = rem - which * per, ti = t / nt, tj = t - ti * nt;
   const int I = h + 2 * h * odd;
   if (which == 0) {
-    const d4 acc = tile_gemm<false, true, true>(blk(v.D, I, n), blk(v.E, I - h, n), n, ti, tj);
+    const d4 acc = tile_gemm<false, true, true>(blk(v.L, I, n), blk(v.E, I - h, n), n, ti, tj);
     tile_store(blk(v.A, I, n), n, ti, tj, acc, 1.0, false);
   } else if (I + h < v.p) {
-    const d4 acc = tile_gemm<false, false, true>(blk(v.D, I, n), blk(v.E, I, n), n, ti, tj);
+    const d4 acc = tile_gemm<false, false, true>(blk(v.L, I, n), blk(v.E, I, n), n, ti, tj);
     tile_store(blk(v.C, I, n), n, ti, tj, acc, 1.0, false);
   }
 }
@@ -709,6 +714,8 @@ __global__ __launch_bounds__(512) void k_cr_top(CRView v) {
 // Back substitution at level h: x_I = Linv_I^T (z_I - A_I x_{I-h} - C_I x_{I+h}).
 // One wave per 16-row slice (blockDim = 64 nt).
 // Waves nt .. of a larger workgroup only join the barrier.
+// LINV = false: only y = z_I - A_I x_{I-h} - C_I x_{I+h} into t (k_cr_back_u).
+template <bool LINV>
 __device__ __forceinline__ void cr_back_body(const CRView &v, int h, int I, double *t) {
   const int n = v.n;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, lo = lane & 7, hi = lane >> 3;
@@ -725,7 +732,7 @@ __device__ __forceinline__ void cr_back_body(const CRView &v, int h, int I, doub
   const d2 *A = reinterpret_cast<const d2 *>(blk(v.A, I, n)), *C = reinterpret_cast<const d2 *>(blk(v.C, I, n));
   const d2 *xl = reinterpret_cast<const d2 *>(v.x + (size_t)(I - h) * n);
   const d2 *xr = reinterpret_cast<const d2 *>(v.x + (size_t)(I + (right ? h : 0)) * n);
-  const d2 *Li = reinterpret_cast<const d2 *>(blk(v.D, I, n));
+  const d2 *Li = reinterpret_cast<const d2 *>(blk(v.L, I, n));
   const int r0 = 16 * wave + hi, hn = n >> 1;
   d2 a0[kCRMaxN / 16], a1[kCRMaxN / 16], c0[kCRMaxN / 16], c1[kCRMaxN / 16], vl[kCRMaxN / 16], vr[kCRMaxN / 16];
   d2 li[kCRMaxN / 8];
@@ -737,8 +744,10 @@ __device__ __forceinline__ void cr_back_body(const CRView &v, int h, int I, doub
     a1[u] = A[(r0 + 8) * hn + c];
     vl[u] = xl[c];
   }
+  if (LINV) {
 #pragma unroll
-  for (int u = 0; u < kCRMaxN / 8; ++u) li[u] = Li[kclamp(16 * wave + 8 * u + hi, n) * hn + 8 * wave + lo];
+    for (int u = 0; u < kCRMaxN / 8; ++u) li[u] = Li[kclamp(16 * wave + 8 * u + hi, n) * hn + 8 * wave + lo];
+  }
   if (right) {
 #pragma unroll
     for (int u = 0; u < kCRMaxN / 16; ++u) {
@@ -770,7 +779,7 @@ __device__ __forceinline__ void cr_back_body(const CRView &v, int h, int I, doub
   }
   }
   __syncthreads();
-  if (!act) return;
+  if (!LINV || !act) return;
   double x0 = 0.0, x1 = 0.0;
 #pragma unroll
   for (int u = 0; u < kCRMaxN / 8; ++u) {
@@ -792,7 +801,66 @@ __device__ __forceinline__ void cr_back_body(const CRView &v, int h, int I, doub
 
 __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
   extern __shared__ __attribute__((aligned(16))) double t[];
-  cr_back_body(v, h, h + 2 * h * blockIdx.x, t);
+  cr_back_body<true>(v, h, h + 2 * h * blockIdx.x, t);
+}
+
+// Back substitution with the factor kept as U (upper tiles) and T_i = L_ii^-1
+// on the diagonal (k_cr_aug<.., false>): x_I = U^-1 y with y = z_I - A_I x_{I-h}
+// - C_I x_{I+h} (TOP: y = z_0), blocked from the bottom:
+//   x_i = T_i^T (y_i - sum_{j>i} U_ij x_j),  i = nt-1 .. 0.
+// Wave i owns block row i: its U tiles and T_i are loaded up front, each U_ij x_j
+// term is added as soon as x_j is flagged in LDS, so after x_{i+1} only one
+// 16x16 product, two 16-lane sums and T_i^T remain on the chain.
+template <bool TOP>
+__global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN;
+  int *fx = reinterpret_cast<int *>(sm + 3 * kCRMaxN);
+  const int I = TOP ? 0 : h + 2 * h * blockIdx.x, n = v.n, nt = n >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
+  if (threadIdx.x < aug::kMaxNt) fx[threadIdx.x] = 0;
+  if (TOP) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) y[k] = v.g[(size_t)I * n + k];
+    __syncthreads();
+  } else {
+    cr_back_body<false>(v, h, I, y);  // ends with a barrier (also covers fx)
+  }
+  if (wave >= nt) return;
+  const int i = wave;
+  const double *Lb = blk(v.L, I, n);
+  double u[aug::kMaxNt][4], tv[4];
+#pragma unroll
+  for (int j = 0; j < aug::kMaxNt; ++j)
+    if (j > i && j < nt) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) u[j][m] = Lb[(size_t)(16 * i + r) * n + 16 * j + 4 * q + m];  // U_ij[r][4q+m]
+    }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) tv[m] = Lb[(size_t)(16 * i + 4 * q + m) * n + 16 * i + r];  // T_i[4q+m][r]
+  double acc = 0.0;
+#pragma unroll
+  for (int j = aug::kMaxNt - 1; j > 0; --j)
+    if (j > i && j < nt) {
+      aug::spin(&fx[j]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = fma(u[j][m], xs[16 * j + 4 * q + m], acc);
+    }
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  if (q == 0) rr[16 * i + r] = y[16 * i + r] - acc;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double x = 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) x = fma(tv[m], rr[16 * i + 4 * q + m], x);  // lane (q, c = r)
+  x += __shfl_xor(x, 16, 64);
+  x += __shfl_xor(x, 32, 64);
+  if (q == 0) {
+    xs[16 * i + r] = x;
+    v.x[(size_t)I * n + 16 * i + r] = x;
+  }
+  aug::raise_flag(&fx[i], lane);
 }
 
 
@@ -1220,24 +1288,65 @@ __global__ __launch_bounds__(512) void k_cr_factor_at(CRView v, int I) {
   cr_factor_store(v, I, lds, &fail);
 }
 
-int launch_cr_multi(double *D, double *E, double *A, double *C, double *gs, double *xs, double *G, double *Z,
-                    double *X, int *flags, int p, int n, int R, hipStream_t st) {
+// SQLM_CR_LEGACY=1: the round-2 factor (panel Cholesky + explicit Linv in LDS,
+// k_cr_factor / k_cr_factor_elim / k_cr_top) instead of k_cr_aug (A/B only).
+inline bool cr_legacy() {
+  static const bool on = std::getenv("SQLM_CR_LEGACY") != nullptr;
+  return on;
+}
+
+// Factor `count` superblocks I = I0 + stride q: z_I -> g_I, and Linv_I (linv)
+// or U_I with T on the diagonal (k_cr_back_u) -> L_I. Legacy: always Linv.
+static void launch_cr_factor(const CRView &v, int h, int I0, int stride, int count, bool linv, hipStream_t st) {
+  if (cr_legacy()) {
+    const size_t lds = cr_factor_lds(v.n);
+    if (stride == 0) hipLaunchKernelGGL(k_cr_factor_at, dim3(1), dim3(512), lds, st, v, I0);
+    else hipLaunchKernelGGL(k_cr_factor, dim3(count), dim3(512), lds, st, v, h);
+    return;
+  }
+  if (linv) hipLaunchKernelGGL((k_cr_aug<1, true>), dim3(count), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, I0, stride, 1);
+  else hipLaunchKernelGGL((k_cr_aug<1, false>), dim3(count), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, I0, stride, 1);
+}
+
+// Level h, steps 1 + 2: every odd superblock factored, A_I / C_I / z_I formed.
+static void launch_cr_level(const CRView &v, int h, int n_odd, int fuse_min, bool fuse_ok, bool linv, hipStream_t st) {
+  const int nt = v.n / 16;
+  if (!cr_legacy()) {
+    const int sp = aug_split(n_odd, nt, linv, aug::extra_columns(nt, true, true));
+    if (linv)
+      hipLaunchKernelGGL((k_cr_aug<0, true>), dim3(n_odd * sp), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, h, 2 * h, sp);
+    else
+      hipLaunchKernelGGL((k_cr_aug<0, false>), dim3(n_odd * sp), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, h, 2 * h, sp);
+    return;
+  }
+  const size_t lds = cr_factor_lds(v.n);
+  if (fuse_ok) {
+    const int sp = n_odd >= fuse_min ? 1 : cr_split(n_odd, nt);
+    hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd * sp), dim3(512), lds, st, v, h, sp);
+  } else {
+    const int per = nt * nt;
+    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
+    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
+  }
+}
+
+int launch_cr_multi(double *D, double *L, double *E, double *A, double *C, double *gs, double *xs, double *G,
+                    double *Z, double *X, int *flags, int p, int n, int R, hipStream_t st) {
   if (p <= 0 || n % 16 || n > kCRMaxN || R <= 0 || R % 16) return -1;
-  CRView v{p, n, 0, 0, D, E, A, C, gs, xs, flags};
-  CRMView m{p, n, R, D, A, C, G, Z, X};
-  const size_t lds = cr_factor_lds(n);
+  CRView v{p, n, 0, 0, D, E, A, C, gs, xs, flags, L};
+  CRMView m{p, n, R, L, A, C, G, Z, X};
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt, rhs = nt * (R / 16);
   int h = 1;
   for (; h < p; h *= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
-    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
+    launch_cr_factor(v, h, h, 2 * h, n_odd, true, st);
     hipLaunchKernelGGL(k_crm_fwd, dim3(xcd_grid(n_odd * rhs)), dim3(64), 0, st, m, h, 2 * h, n_odd * rhs);
     hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
     hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
     hipLaunchKernelGGL(k_crm_upd, dim3(xcd_grid(n_even * rhs)), dim3(64), 0, st, m, h, n_even * rhs);
   }
-  hipLaunchKernelGGL(k_cr_factor_at, dim3(1), dim3(512), lds, st, v, 0);
+  launch_cr_factor(v, 0, 0, 0, 1, true, st);
   hipLaunchKernelGGL(k_crm_fwd, dim3(xcd_grid(rhs)), dim3(64), 0, st, m, 0, 1, rhs);
   hipLaunchKernelGGL(k_crm_bwd, dim3(xcd_grid(rhs)), dim3(64), 0, st, m, 0, 1, rhs);
   for (h /= 2; h >= 1; h /= 2) {
@@ -1404,9 +1513,8 @@ void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
 // along, the border system, and the back substitution.
 static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
   const int p = pl.p, n = pl.n, R = pl.R;
-  CRView v{p, n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags};
-  ArwView a{p, n, R, d.cr_D, d.cr_A, d.cr_C, d.arw_G, d.arw_Z, d.cr_g};
-  const size_t lds = cr_factor_lds(n);
+  CRView v{p, n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
+  ArwView a{p, n, R, d.cr_L, d.cr_A, d.cr_C, d.arw_G, d.arw_Z, d.cr_g};
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt, rhs = nt * (R / 16);
   static const int fuse_min = std::getenv("SQLM_CR_FUSE_MIN") ? std::atoi(std::getenv("SQLM_CR_FUSE_MIN")) : 128;
   static const bool fuse_ok = std::getenv("SQLM_CR_UNFUSED") == nullptr;
@@ -1416,19 +1524,13 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
     const int fo = pl.lvl[4 * lv], fc = pl.lvl[4 * lv + 1], uo = pl.lvl[4 * lv + 2], uc = pl.lvl[4 * lv + 3];
-    if (fuse_ok) {
-      const int sp = n_odd >= fuse_min ? 1 : cr_split(n_odd, nt);
-      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd * sp), dim3(512), lds, st, v, h, sp);
-    } else {
-      hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
-      hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
-    }
+    launch_cr_level(v, h, n_odd, fuse_min, fuse_ok, true, st);
     if (fc) hipLaunchKernelGGL(k_arw_fwd, dim3(xcd_grid(fc * rhs)), dim3(64), 0, st, a, S + fo, fc * rhs);
     hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
     if (uc) hipLaunchKernelGGL(k_arw_upd, dim3(xcd_grid(uc * rhs)), dim3(64), 0, st, a, h, S + uo, uc * rhs);
   }
-  // top superblock: factor (Linv_0 into D_0, z_0 into g_0) and its Z_0
-  hipLaunchKernelGGL(k_cr_factor_at, dim3(1), dim3(512), lds, st, v, 0);
+  // top superblock: factor (Linv_0 into L_0, z_0 into g_0) and its Z_0
+  launch_cr_factor(v, 0, 0, 0, 1, true, st);
   const int *elim = S + pl.elim_off;
   if (pl.top_active)
     hipLaunchKernelGGL(k_arw_fwd, dim3(xcd_grid(rhs)), dim3(64), 0, st, a, elim + pl.elim_cnt - 1, rhs);
@@ -1451,9 +1553,9 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
 }
 
 // Levels, top solve and back substitution on D/E/g already in CR layout.
-void launch_cr_core(double *D, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
-                    hipStream_t st) {
-  CRView v{p, n, 0, 0, D, E, A, C, g, x, flags};
+void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p,
+                    int n, hipStream_t st) {
+  CRView v{p, n, 0, 0, D, E, A, C, g, x, flags, L};
   const size_t lds = cr_factor_lds(n);
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt;
   // SQLM_CR_UNFUSED=1: separate factor and elimination launches (A/B only)
@@ -1464,24 +1566,27 @@ void launch_cr_core(double *D, double *E, double *A, double *C, double *g, doubl
   for (; h < p; h *= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
-    if (fuse_ok) {
-      const int sp = n_odd >= fuse_min ? 1 : cr_split(n_odd, nt);
-      hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd * sp), dim3(512), lds, st, v, h, sp);
-    } else {
-      hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
-      hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
-    }
+    launch_cr_level(v, h, n_odd, fuse_min, fuse_ok, false, st);
     hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
   }
-  hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
+  const size_t back_lds = 3 * kCRMaxN * sizeof(double) + aug::kMaxNt * sizeof(int);
+  if (cr_legacy()) {
+    hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
+  } else {  // x_0 = U_0^-1 z_0
+    launch_cr_factor(v, 0, 0, 0, 1, false, st);
+    hipLaunchKernelGGL(k_cr_back_u<true>, dim3(1), dim3(64 * nt), back_lds, st, v, 0);
+  }
   for (h /= 2; h >= 1; h /= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
-    hipLaunchKernelGGL(k_cr_back, dim3(n_odd), dim3(64 * nt), (size_t)n * sizeof(double), st, v, h);
+    if (cr_legacy())
+      hipLaunchKernelGGL(k_cr_back, dim3(n_odd), dim3(64 * nt), (size_t)n * sizeof(double), st, v, h);
+    else
+      hipLaunchKernelGGL(k_cr_back_u<false>, dim3(n_odd), dim3(64 * nt), back_lds, st, v, h);
   }
 }
 
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
-  CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags};
+  CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
   if (!d.cr_direct) {  // BSR S (sharded runs / row-kernel RCS): zero the superblocks and scatter
     const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
     if (hipMemsetAsync(d.cr_D, 0, blkbytes, st) != hipSuccess) return -2;
@@ -1490,7 +1595,7 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
     hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
   }
   if (pl.R) launch_arrow_solve(d, pl, st);
-  else launch_cr_core(d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
+  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
   hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }

@@ -121,6 +121,12 @@ class Context:
         buf = C.create_string_buffer(unique_id, len(unique_id))
         check(lib().sqlm_ctx_set_comm(self._h, buf, int(rank), int(nranks)), "sqlm_ctx_set_comm")
 
+    def set_comm_selfloop(self, unique_id: bytes) -> None:
+        """A one-rank RCCL communicator: the sharded code path with every
+        exchange through real RCCL on one GPU (sqlm_ctx_set_comm_selfloop)."""
+        buf = C.create_string_buffer(unique_id, len(unique_id))
+        check(lib().sqlm_ctx_set_comm_selfloop(self._h, buf), "sqlm_ctx_set_comm_selfloop")
+
     def set_host_comm(self, rank: int, nranks: int, allreduce, p2p) -> None:
         """Shard over host collectives: ``allreduce(arr, op)`` must reduce the
         numpy array ``arr`` in place across ranks (op "sum" or "max");
@@ -216,6 +222,15 @@ def comm_unique_id() -> bytes:
     buf = C.create_string_buffer(n)
     check(lib().sqlm_comm_get_unique_id(buf), "sqlm_comm_get_unique_id")
     return buf.raw
+
+
+def comm_selftest(device: int = 0, count: int = 1 << 16) -> float:
+    """sqlm_comm_selftest: the RCCL exchange primitives on a one-rank
+    communicator; returns the largest deviation from the expected buffers."""
+    err = C.c_double(-1.0)
+    buf = C.create_string_buffer(comm_unique_id(), lib().sqlm_comm_id_size())
+    check(lib().sqlm_comm_selftest(int(device), buf, C.c_int64(count), C.byref(err)), "sqlm_comm_selftest")
+    return err.value
 
 
 def pose_from_Tcw_f32(T):

@@ -32,9 +32,9 @@ int main(int argc, char **argv) {
       for (size_t k = 0; k < (size_t)n * n; ++k) E[(size_t)I * n * n + k] = U(rng);
   }
   for (auto &v : g) v = U(rng);
-  double *dD, *dE, *dA, *dC, *dg, *dx;
+  double *dD, *dE, *dA, *dC, *dg, *dx, *dL;
   int *dflags;
-  CK(hipMalloc(&dD, nb * 8)); CK(hipMalloc(&dE, nb * 8)); CK(hipMalloc(&dA, nb * 8)); CK(hipMalloc(&dC, nb * 8));
+  CK(hipMalloc(&dD, nb * 8)); CK(hipMalloc(&dL, nb * 8)); CK(hipMalloc(&dE, nb * 8)); CK(hipMalloc(&dA, nb * 8)); CK(hipMalloc(&dC, nb * 8));
   CK(hipMalloc(&dg, g.size() * 8)); CK(hipMalloc(&dx, g.size() * 8)); CK(hipMalloc(&dflags, 16));
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -47,7 +47,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(sqlm::g_cr_prof), &dprof, sizeof(dprof)));
     CK(hipMemcpy(dD, D.data(), (size_t)n * n * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dg, g.data(), (size_t)n * 8, hipMemcpyHostToDevice));
-    sqlm::CRView v{1, n, 0, 0, dD, dE, dA, dC, dg, dx, dflags};
+    sqlm::CRView v{1, n, 0, 0, dD, dE, dA, dC, dg, dx, dflags, dL};
     hipLaunchKernelGGL(sqlm::k_cr_top, dim3(1), dim3(512), sqlm::cr_factor_lds(n), st, v);
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(prof, dprof, 64 * 8, hipMemcpyDeviceToHost));
@@ -58,16 +58,59 @@ int main(int argc, char **argv) {
       if (prof[i]) std::printf("\"%d\": %lld, ", i, prof[i] - prof[0]);
     std::printf("\"end\": 0}}\n");
   }
-  {  // k_cr_factor alone (h = 1): Linv D Linv^T == I and z == Linv g on every odd block
+  // phase profile of k_cr_aug: factor only (one block) and a level step of I = 1 (h = 1)
+  for (int mode = 0; mode < 3 && p >= 3; ++mode) {
+    static long long zero[1024 * 16], prof[1024 * 16];
+    long long *dprof;
+    CK(hipMalloc(&dprof, sizeof(zero)));
+    CK(hipMemcpy(dprof, zero, sizeof(zero), hipMemcpyHostToDevice));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(sqlm::g_cr_prof), &dprof, sizeof(dprof)));
+    CK(hipMemcpy(dD, D.data(), nb * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dE, E.data(), nb * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice));
+    sqlm::CRView v{p, n, 0, 0, dD, dE, dA, dC, dg, dx, dflags, dL};
+    const int nt = n / 16, sp = mode == 1 ? 1 : sqlm::aug_split(1, nt, false, sqlm::aug::extra_columns(nt, true, true));
+    for (int rep = 0; rep < 2; ++rep) {  // the second launch is timed (warm caches and TLB)
+    CK(hipMemcpy(dprof, zero, sizeof(zero), hipMemcpyHostToDevice));
+    if (mode == 0) hipLaunchKernelGGL((sqlm::k_cr_aug<1, false>), dim3(1), dim3(sqlm::aug::kThreads), sizeof(sqlm::aug::Shared), st, v, 1, 1, 0, 1);
+    else hipLaunchKernelGGL((sqlm::k_cr_aug<0, false>), dim3(mode == 1 ? 1 : sp), dim3(sqlm::aug::kThreads), sizeof(sqlm::aug::Shared), st, v, 1, 1, 0,
+                            mode == 1 ? sqlm::aug::min_split(nt, false, sqlm::aug::extra_columns(nt, true, true)) : sp);
+    CK(hipStreamSynchronize(st));
+    }
+    CK(hipMemcpy(prof, dprof, sizeof(prof), hipMemcpyDeviceToHost));
+    long long *nul = nullptr;
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(sqlm::g_cr_prof), &nul, sizeof(nul)));
+    std::printf("{\"aug_phase_cycles_%s\": {", mode == 0 ? "factor" : mode == 1 ? "level_wg0_minsplit" : "level_wg0");
+    for (int i = 1; i < 64; ++i)
+      if (prof[i]) std::printf("\"%d\": %lld, ", i, prof[i] - prof[0]);
+    std::printf("\"end\": 0}}\n");
+    std::printf("{\"aug_wave_steps_%d\": {", mode);  // wave: [step k: event 0, 1]
+    for (int w = 0; w < 16; ++w) {
+      std::printf("\"w%d simd%lld\": [", w, (prof[900 + w] >> 4) & 3);
+      for (int k = 0; k < 7; ++k)
+        for (int e = 0; e < 2; ++e) {
+          const long long v = prof[64 + 32 * w + 4 * k + e];
+          std::printf("%lld%s", v ? v - prof[0] : -1, (k == 6 && e == 1) ? "" : ",");
+        }
+      std::printf("]%s", w == 15 ? "" : ", ");
+    }
+    std::printf("}}\n");
+    CK(hipFree(dprof));
+  }
+  {  // factor alone (h = 1): Linv D Linv^T == I and z == Linv g on every odd block
     CK(hipMemcpy(dD, D.data(), nb * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice));
-    sqlm::CRView v{p, n, 0, 0, dD, dE, dA, dC, dg, dx, dflags};
+    CK(hipMemset(dL, 0, nb * 8));
+    sqlm::CRView v{p, n, 0, 0, dD, dE, dA, dC, dg, dx, dflags, dL};
     const int n_odd = p / 2;
     if (n_odd > 0) {
-      hipLaunchKernelGGL(sqlm::k_cr_factor, dim3(n_odd), dim3(512), sqlm::cr_factor_lds(n), st, v, 1);
+      sqlm::launch_cr_factor(v, 1, 1, 2, n_odd, true, st);
       CK(hipStreamSynchronize(st));
       std::vector<double> Li(nb), z(g.size());
-      CK(hipMemcpy(Li.data(), dD, nb * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(Li.data(), dL, nb * 8, hipMemcpyDeviceToHost));
+      for (int I = 0; I < p; ++I)  // only the lower block triangle of Linv is defined
+        for (int r = 0; r < n; ++r)
+          for (int c = (r | 15) + 1; c < n; ++c) Li[(size_t)I * n * n + r * n + c] = 0.0;
       CK(hipMemcpy(z.data(), dg, z.size() * 8, hipMemcpyDeviceToHost));
       double emax = 0.0, zmax = 0.0;
       for (int I = 1; I < p; I += 2) {
@@ -102,7 +145,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpyAsync(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(dflags, &one, 4, hipMemcpyHostToDevice, st));
     CK(hipEventRecord(e0, st));
-    sqlm::launch_cr_core(dD, dE, dA, dC, dg, dx, dflags, p, n, st);
+    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st);
     CK(hipEventRecord(e1, st));
     CK(hipStreamSynchronize(st));
     CK(hipGetLastError());
@@ -114,13 +157,17 @@ int main(int argc, char **argv) {
   int flag = 0;
   CK(hipMemcpy(x.data(), dx, x.size() * 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(&flag, dflags, 4, hipMemcpyDeviceToHost));
-  if (p == 2) {  // stage-by-stage host check of the one-level solve
-    std::vector<double> dDh(nb), dAh(nb), dgh(g.size());
+  if (p == 2 && std::getenv("SQLM_CR_LEGACY")) {  // stage-by-stage host check of the one-level solve (Linv layout)
+    std::vector<double> dDh(nb), dLh(nb), dAh(nb), dgh(g.size());
     CK(hipMemcpy(dDh.data(), dD, nb * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(dLh.data(), dL, nb * 8, hipMemcpyDeviceToHost));
+    for (size_t I = 0; I < 2; ++I)  // Linv is defined on its lower block triangle
+      for (int r = 0; r < n; ++r)
+        for (int c = (r | 15) + 1; c < n; ++c) dLh[I * n * n + r * n + c] = 0.0;
     CK(hipMemcpy(dAh.data(), dA, nb * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(dgh.data(), dg, g.size() * 8, hipMemcpyDeviceToHost));
     const size_t nn = (size_t)n * n;
-    const double *L1 = dDh.data() + nn, *E0 = E.data(), *A1 = dAh.data() + nn;
+    const double *L1 = dLh.data() + nn, *E0 = E.data(), *A1 = dAh.data() + nn;
     double ea = 0, ed = 0, eg = 0, ex0 = 0, ex1 = 0;
     std::vector<double> Ae(nn, 0.0), D0((size_t)nn), g0(n), z1(n);
     for (int r = 0; r < n; ++r)
