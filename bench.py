@@ -176,7 +176,7 @@ def host_cpu() -> dict:
     return {"cpu_model": model, "nproc": usable, "machine_cpus": os.cpu_count()}
 
 
-def cpu_baseline(prob, name: str, omp: bool = False):
+def cpu_baseline(prob, name: str, omp: bool = False, gba_iters: int = 8, min_s: float = 10.0):
     """The oracle (g2o-semantics port) on a bounded sample of the same
     workload: a fixed number of LM iterations of the full config-4 problem, or
     repeated 10-iteration solves of config 2 until >= 10 s. Only the optimize()
@@ -191,19 +191,23 @@ def cpu_baseline(prob, name: str, omp: bool = False):
     while True:
         g = O.OracleGraph(prob, omp=omp)
         t0 = time.perf_counter()
-        n, st = g.optimize(0, 8 if name.startswith("gba") else 10)
+        n, st = g.optimize(0, gba_iters if name.startswith("gba") else 10)
         total_dt += time.perf_counter() - t0
         total_n += max(n, 1)
         runs += 1
         del g
-        if name.startswith("gba") or total_dt >= 10.0:
+        if name.startswith("gba") or total_dt >= min_s:
             break
     host = host_cpu()
-    threads = int(os.environ.get("OMP_NUM_THREADS") or host["nproc"] or 1) if omp else 1
-    return dict({"value": total_n / total_dt, "unit": "LM iterations/s", "cores": threads, "kind": "port",
-                 "sample": f"{total_n} LM iterations ({runs} x optimize()) on the full {name} workload, "
-                           f"{threads} thread(s), {total_dt:.1f} s of optimize() time",
-                 "build": "oracle/g2o_ref.c gcc -O2" + (" -fopenmp (ORC_OMP)" if omp else "")}, **host)
+    threads = O.omp_threads() if omp else 1
+    out = dict({"value": total_n / total_dt, "unit": "LM iterations/s", "cores": threads, "kind": "port",
+                "sample": f"{total_n} LM iterations ({runs} x optimize()) on the full {name} workload, "
+                          f"{threads} thread(s), {total_dt:.1f} s of optimize() time",
+                "build": "oracle/g2o_ref.c gcc -O2" + (" -fopenmp (ORC_OMP)" if omp else "")}, **host)
+    if omp:
+        out["threads_note"] = (f"{threads} OpenMP threads = the job's CPU share (OMP_NUM_THREADS); the host shows "
+                               f"{host['nproc']} usable of {host['machine_cpus']} CPUs, most of them other jobs'")
+    return out
 
 
 EG_N_KF = 1500  # KITTI-00 keyframe count of ORB-SLAM2-style mapping (SURVEY.md §8 sizes, config 5: EG 7*#KF)
@@ -477,33 +481,12 @@ def bench_orb(args, world):
         dist.destroy_process_group()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["gba", "gba_loop", "lba", "eg", "orb"], default="gba")
-    ap.add_argument("--scale", type=float, default=1.0, help="shrink config 4 (parity / debugging only)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
-                    help="host = exchange through gloo on the host, all ranks on GPU 0 (1-GPU rehearsal of N>1)")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.config == "eg":
-        return bench_eg(args, world)
-    if args.config == "orb":
-        return bench_orb(args, world)
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # rendezvous + scalar reductions only
-        dist.init_process_group("gloo", init_method="env://")
-
+def run_ba(args, world, rank, local_rank, dist, config, cpu_iters=8, cpu_min_s=10.0):
+    """One BA workload (config 4, the loop-closed config 4, or config 2) on this
+    rank's context; returns the bench dict on rank 0 (None elsewhere)."""
     from sqrtlm.optimizer import Context, comm_unique_id
     from sqrtlm.shard import shard
-    prob, desc = make_workload(args.config, args.scale)
+    prob, desc = make_workload(config, args.scale)
     local = shard(prob, rank, world)
     # SQLM_BENCH_ONE_GPU=1 puts every rank on GPU 0 (1-GPU rehearsal of the RCCL transport)
     one_gpu = args.comm == "host" or os.environ.get("SQLM_BENCH_ONE_GPU") == "1"
@@ -538,7 +521,7 @@ def main():
     _ms_timed, kms, _st = ctx.bench(args.warmup, args.steps)
     sse, nres = reprojection_sse(local, *ctx.poses(), ctx.points())
     e2e = None
-    if world == 1 and args.config == "lba":
+    if world == 1 and config == "lba":
         # the drop-in LocalBundleAdjustment call: host arrays in, the three-pass
         # schedule (5 Huber iterations, outlier tags, 10 more, + LiDAR 20), out
         t0 = time.perf_counter()
@@ -549,7 +532,7 @@ def main():
                "lm_iterations": int(sum(x["iterations"] for x in sts)),
                "setup_ms": float(sum(x["ms_setup"] for x in sts)), "optimize_ms": float(sum(x["ms_total"] for x in sts)),
                "what": "sqlm_set_problem + sqlm_local_ba (3-pass schedule) + sqlm_get_poses/points, host buffers"}
-    if world == 1 and args.config in ("gba", "gba_loop"):
+    if world == 1 and config in ("gba", "gba_loop"):
         # the drop-in call as the reference makes it (GlobalBundleAdjustemnt, 10
         # iterations): host arrays in, setup (sorting, tiles, H2D), the solve,
         # results out (D2H) — reported beside the metric, never as `value`
@@ -568,13 +551,13 @@ def main():
         tt = torch.tensor([sse, nres], dtype=torch.float64)
         dist.all_reduce(tt)
         sse, nres = float(tt[0]), float(tt[1])
-
+    out = None
     if rank == 0:
         launches = max(1.0, st["trials"] / max(1, st["iterations"]))  # k_rcs_tile runs once per trial
         t_rcs = kms["k_rcs_tile"] / launches
         flops = algorithmic_flops_rcs(local)
         ach_tf = flops / (t_rcs * 1e-3) / 1e12 if t_rcs > 0 else 0.0
-        traffic, tsrc = pmc_traffic("k_rcs_tile", args.config, local.n_obs) if world == 1 else (None, None)
+        traffic, tsrc = pmc_traffic("k_rcs_tile", config, local.n_obs) if world == 1 else (None, None)
         # the landmark linearization runs inside k_landmark_update (speculative,
         # DESIGN.md §2 step 7) unless SQLM_NO_SPEC=1 puts it back in k_linearize
         spec = os.environ.get("SQLM_NO_SPEC", "0") in ("", "0")
@@ -582,7 +565,7 @@ def main():
         t_lin = kms[lin_kernel] / (launches if spec else 1.0)
         alg = algorithmic_bytes_update(local) if spec else algorithmic_bytes_linearize(local)
         achieved = alg / (t_lin * 1e-3) / 1e9 if t_lin > 0 else 0.0
-        lin_traffic, _ = pmc_traffic(lin_kernel, args.config, local.n_obs) if world == 1 else (None, None)
+        lin_traffic, _ = pmc_traffic(lin_kernel, config, local.n_obs) if world == 1 else (None, None)
         out = {
             "metric": "LM iterations/sec (synthetic KITTI-00-scale BA)",
             "value": 1000.0 / ms,
@@ -622,10 +605,62 @@ def main():
         if e2e is not None:
             out["end_to_end"] = e2e
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(prob, args.config)
-            out["cpu_baseline_all_cores"] = cpu_baseline(prob, args.config, omp=True)
-        print(json.dumps(out))
+            out["cpu_baseline"] = cpu_baseline(prob, config, gba_iters=cpu_iters, min_s=cpu_min_s)
+            out["cpu_baseline_multithread"] = cpu_baseline(prob, config, omp=True, gba_iters=cpu_iters,
+                                                           min_s=cpu_min_s)
     ctx.close()
+    return out
+
+
+def summary(out) -> dict:
+    """The keys of a workload's line that the default line repeats for it."""
+    keep = ("metric", "value", "unit", "ms_per_step", "trials_per_step", "final_rmse_px", "config", "end_to_end")
+    s = {k: out[k] for k in keep if k in out}
+    s["roofline"] = {k: out["roofline"][k] for k in ("kernel", "achieved", "peak", "unit", "frac")}
+    s["kernel_ms_per_step"] = out["kernel_ms_per_step"]
+    for k in ("cpu_baseline", "cpu_baseline_multithread"):
+        if k in out:
+            s[k] = {kk: out[k][kk] for kk in ("value", "unit", "cores", "kind", "sample")}
+    return s
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", choices=["gba", "gba_loop", "lba", "eg", "orb"], default="gba")
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink config 4 (parity / debugging only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="default line without the loop-closed GBA and config-2 LBA figures")
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                    help="host = exchange through gloo on the host, all ranks on GPU 0 (1-GPU rehearsal of N>1)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.config == "eg":
+        return bench_eg(args, world)
+    if args.config == "orb":
+        return bench_orb(args, world)
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # rendezvous + scalar reductions only
+        dist.init_process_group("gloo", init_method="env://")
+    out = run_ba(args, world, rank, local_rank, dist, args.config)
+    if out is not None and args.config == "gba" and world == 1 and not args.no_extras and args.scale == 1.0:
+        # the workloads the reference's own BA calls have, beside the metric's:
+        # GBA only ever runs after a loop closure (LoopClosing.cc:877, :987-991),
+        # and LocalMapping's local BA (LocalMapping.cc:131) is config 2's shape;
+        # bounded CPU samples (3 LM iterations / 5 s) keep the default run short
+        out["extra_workloads"] = {
+            "gba_loop": summary(run_ba(args, world, rank, local_rank, dist, "gba_loop", cpu_iters=3, cpu_min_s=5.0)),
+            "lba": summary(run_ba(args, world, rank, local_rank, dist, "lba", cpu_iters=3, cpu_min_s=5.0)),
+        }
+    if out is not None:
+        print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -20,6 +20,18 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef ORC_OMP
+#include <omp.h>
+#endif
+
+/* threads the OpenMP loops of this build run on (1 for the serial build) */
+int orc_omp_threads(void) {
+#ifdef ORC_OMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
 
 /* ------------------------------------------------------------------ edges */
 

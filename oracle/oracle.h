@@ -104,6 +104,8 @@ int orc_local_ba(orc_graph *g, const volatile uint8_t *stop, uint8_t *outlier, o
 
 /* g2oOptimizer::BundleAdjustment (g2oOptimizer.cc:110-362): optimize(level 0, n). */
 int orc_global_ba(orc_graph *g, int iterations, const volatile uint8_t *stop, orc_stats *st);
+/* OpenMP threads of the loops of this build (1 for the serial build) */
+int orc_omp_threads(void);
 
 /* Converter::toSE3Quat (Converter.cc:55-68): float 4x4 Tcw -> q (x,y,z,w), t. */
 void orc_se3_from_Tcw_f32(const float T[16], double q[4], double t[3]);

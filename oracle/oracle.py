@@ -71,6 +71,12 @@ def lib(omp: bool = False) -> C.CDLL:
     return _libs[omp]
 
 
+def omp_threads() -> int:
+    """OpenMP threads of the all-cores build's loops (OMP_NUM_THREADS or the
+    runtime's default) -- the `cores` of its labelled baseline."""
+    return int(lib(True).orc_omp_threads())
+
+
 def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None else None
 

@@ -19,28 +19,29 @@
 // v_mfma_f64_16x16x4f64 on the tiles as they stand, with no data movement.
 //
 // Roles (16 waves; a workgroup's waves w, w+4, w+8, w+12 share one SIMD):
-//   wave 0        the diagonal wave: factors diagonal tile k at step k in four
-//                 rank-4 groups (a 4x4 Cholesky on uniform values from
-//                 readlane, W = L44^-1 per lane, the finished rows X = W M4 by
-//                 one MFMA, the rank-4 update by one MFMA) and publishes each
-//                 group's W and finished rows in LDS. Waves 4, 8, 12 stay idle
-//                 so the critical path has its SIMD (matrix pipe and issue) to
-//                 itself: any MFMA-busy partner triples its time (tools/
-//                 group_probe).
+//   wave 0        the diagonal wave. Step k: diagonal tile k in four rank-4
+//                 groups (a 4x4 Cholesky on uniform values from readlane,
+//                 W = L44^-1 per lane, the finished rows X = W M4 by one MFMA,
+//                 the rank-4 update by one MFMA). In the pipe beside that scalar
+//                 chain the same groups turn an identity tile into T_k = L_kk^-1
+//                 (published for the workers), finish P = (k, k+1) -> U_k,k+1 and
+//                 apply its piece to the next diagonal Q = (k+1, k+1). At the end
+//                 of the step it takes column k+2's tiles (k+1, k+2), (k+2, k+2)
+//                 (handed over through step k-1) and U_k,k+2, and forms the next
+//                 step's P and Q. Waves 4, 8, 12 stay idle: any MFMA-busy wave on
+//                 this SIMD triples the chain, whatever the priorities
+//                 (tools/group_probe).
 //   workers       the other 12 waves own one column of tiles each: D column J
-//                 (the U tiles above its diagonal, and its diagonal tile until
-//                 step J, when it hands it to wave 0 through LDS; in LINV mode
-//                 continued below the diagonal by identity column J+1), the T
-//                 column (diagonal inverses; LINV: identity column 0), g, and
-//                 the E^T / E columns dealt over the `split` workgroups that
-//                 share the superblock (each repeats the factorization: it is
-//                 the latency, the E columns are the parallel work).
-// Step k: every row-k tile follows wave 0 one group behind (group_apply: the
-// same two MFMAs per group); D columns publish U_kJ for the trailing updates
-// tile(I, col) -= U_kI^T X_k,col (row k+1 first, the rest deferred into the
-// next step). The owner of column k+1 folds the update of its diagonal tile
-// into its group_apply (one MFMA per group) and hands the tile over.
-// Hand-offs are LDS flags (no barrier after the start).
+//                 (the U tiles above the diagonal; rows J-1 and J go to wave 0
+//                 at step J-2; in LINV mode continued below the diagonal by
+//                 identity column J+1), identity column 0 (LINV), g, and the
+//                 E^T / E columns dealt over the `split` workgroups that share
+//                 the superblock (each repeats the factorization: it is the
+//                 latency, the E columns are the parallel work).
+// Step k on a worker: row-k tile <- T_k tile (four MFMAs), D columns publish
+// U_kJ; trailing tile(I, col) -= U_kI^T X_k,col for I > k, row k+1 at once, the
+// rest deferred into the next step. Hand-offs are LDS flags (no barrier after
+// the start).
 #pragma once
 
 namespace sqlm {
@@ -48,14 +49,15 @@ namespace aug {
 
 constexpr int kWaves = 16, kThreads = 64 * kWaves, kMaxNt = kCRMaxN / 16, kWorkers = 12;
 constexpr int kPairs = kMaxNt * (kMaxNt - 1) / 2;
-enum : int { kNone = 0, kColD = 1, kColT = 2, kColI0 = 3, kColEt = 4, kColE = 5, kColG = 6 };
+enum : int { kNone = 0, kColD = 1, kColI0 = 3, kColEt = 4, kColE = 5, kColG = 6 };
 
+constexpr int kTp = 17;  // padded row stride of the T_k images
 struct Shared {
-  double W[kMaxNt][4][64];  // group a of step k: A operand W[i][b] at lane 16 b + i (W = L44^-1)
-  double O[kMaxNt][4][64];  // the group's finished rows U[4a+b][i] (i > 4a+3) at lane 16 b + i
+  double T[kMaxNt][16 * kTp];  // T_k = L_kk^-1 of step k, row-major (the workers read it as an A operand)
   double U[kPairs][256];    // U_kJ (k < J), accumulator layout: element j of lane l at [64 j + l]
-  double Dg[kMaxNt][256];   // diagonal tile k handed to wave 0, same layout
-  int fG[kMaxNt][4], fU[kPairs], fD[kMaxNt];
+  double Hp[kMaxNt][256];   // column J's tiles (J-1, J) and (J, J) through step J-3, handed to wave 0
+  double Hq[kMaxNt][256];
+  int fT[kMaxNt], fU[kPairs], fH[kMaxNt];
 };
 
 // (k, J), k < J < kMaxNt -> 0 .. kPairs-1
@@ -140,11 +142,15 @@ __device__ __forceinline__ d4 get_tile(const double *src, int lane) {
   return t;
 }
 
-// Step k on the diagonal tile Dg, in four rank-4 groups. Each group publishes
-// its A operand W (L44^-1) and its finished rows for group_apply.
-__device__ __forceinline__ void diag_groups(Shared &sh, int k, d4 Dg, int lane, bool &bad) {
+// Step k on the diagonal tile Dg, in four rank-4 groups; T_k = L_kk^-1 in Tt.
+// With PQ the same groups also finish P = tile (k, k+1) -> U_k,k+1 and take
+// the step-k piece of the next diagonal tile Q = (k+1, k+1) -= U_k,k+1^T
+// U_k,k+1: the critical path of the next step stays on this wave's SIMD.
+template <bool PQ>
+__device__ __forceinline__ void diag_groups(d4 Dg, d4 &P, d4 &Q, d4 &Tt, int lane, bool &bad) {
   const int b = lane >> 4, i = lane & 15, c = lane & 15;
   const d4 zero = {0.0, 0.0, 0.0, 0.0};
+  Tt = identity_tile(lane);
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
     // the group's 4x4 pivot block: rows / columns 4a .. 4a+3 sit in element a
@@ -168,32 +174,39 @@ __device__ __forceinline__ void diag_groups(Shared &sh, int k, d4 Dg, int lane, 
     const double w2 = b == 2 ? d2 : (b < 2 ? -d2 * fma(u12, w1, u02 * w0) : 0.0);
     const double w3 = b == 3 ? d3 : -d3 * fma(u23, w2, fma(u13, w1, u03 * w0));
     const double aop = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : i == 3 ? w3 : 0.0;
-    sh.W[k][a][lane] = aop;
     // finished rows 4a .. 4a+3 = W M4 (rows 0..3 of the product, element 0);
     // the rank-4 update of the rows and columns past the group
     const d4 Xd = mfma(aop, Dg[a], zero);
     const double op = c >= 4 * a + 4 ? Xd[0] : 0.0;
-    sh.O[k][a][lane] = op;
     Dg = mfma(-op, op, Dg);
-    __builtin_amdgcn_sched_barrier(0);  // the update is issued before the flag's LDS wait
-    raise_flag(&sh.fG[k][a], lane);
+    __builtin_amdgcn_sched_barrier(0);  // the chain's update is issued first
+    // off the chain (in the pipe while the next group's scalar work runs):
+    // T_k = the same groups on the identity; with PQ, P = (k, k+1) -> U_k,k+1
+    // and the step-k piece of the next diagonal Q = (k+1, k+1) -= U^T U
+    const d4 Xt = mfma(aop, Tt[a], zero);
+    Tt[a] = Xt[0];
+    Tt = mfma(-op, Xt[0], Tt);
+    if (PQ) {
+      const d4 Xp = mfma(aop, P[a], zero);
+      P[a] = Xp[0];
+      P = mfma(-op, Xp[0], P);
+      Q = mfma(-Xp[0], Xp[0], Q);
+    }
   }
 }
 
-// The same four groups on a tile of block row k: t <- L_kk^-1 t. With `diag`,
-// the rank-4 pieces of the trailing update diag -= t^T t follow each group.
-template <bool DIAG>
-__device__ __forceinline__ void group_apply(Shared &sh, int k, d4 &t, d4 &diag, int lane) {
-  const d4 zero = {0.0, 0.0, 0.0, 0.0};
+// Row-k tile t <- T_k t (T_k = L_kk^-1 from wave 0, read from LDS as the A
+// operand: lane 16 b + i holds T_k[i][4 s + b] for K-step s).
+__device__ __forceinline__ void tile_trsm(Shared &sh, int k, d4 &t, int lane) {
+  const int b = lane >> 4, i = lane & 15;
+  spin(&sh.fT[k]);
+  double ta[4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    spin(&sh.fG[k][a]);
-    const double aop = sh.W[k][a][lane], op = sh.O[k][a][lane];
-    const d4 X = mfma(aop, t[a], zero);
-    t[a] = X[0];
-    t = mfma(-op, X[0], t);
-    if (DIAG) diag = mfma(-X[0], X[0], diag);
-  }
+  for (int s4 = 0; s4 < 4; ++s4) ta[s4] = sh.T[k][i * kTp + 4 * s4 + b];
+  d4 x = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) x = mfma(ta[s4], t[s4], x);
+  t = x;
 }
 
 // tile loads in the accumulator layout: (r0, c0) = first row / column in P
@@ -225,8 +238,10 @@ __host__ __device__ __forceinline__ int d_columns(int nt, bool linv) { return li
 __host__ __device__ __forceinline__ int extra_columns(int nt, bool level, bool right) {
   return (level ? nt : 0) + (level && right ? nt : 0) + 1;
 }
+// workers left for the E / g columns (LINV also carries identity column 0)
+__host__ __device__ __forceinline__ int fixed_columns(int nt, bool linv) { return d_columns(nt, linv) + (linv ? 1 : 0); }
 inline int min_split(int nt, bool linv, int ne) {
-  const int cap = kWorkers - d_columns(nt, linv) - 1;
+  const int cap = kWorkers - fixed_columns(nt, linv);
   return (ne + cap - 1) / cap;
 }
 
@@ -240,11 +255,11 @@ __device__ __forceinline__ void column_of(int q, int nt, bool linv, bool level, 
     J = linv ? q : q + 1;
     return;
   }
-  if (q == nd) {
-    type = linv ? kColI0 : kColT;
+  if (linv && q == nd) {
+    type = kColI0;
     return;
   }
-  const int e = (q - nd - 1) * split + sidx;
+  const int e = (q - fixed_columns(nt, linv)) * split + sidx;
   const int net = level ? nt : 0, nee = (level && right) ? nt : 0;
   if (e < net) {
     type = kColEt;
@@ -258,9 +273,11 @@ __device__ __forceinline__ void column_of(int q, int nt, bool linv, bool level, 
 }
 
 // Does column (type, J) take the trailing update of row I from step k (k < I)?
+// D column J keeps its rows J-1 and J only through step J-3: at step J-2 it
+// hands them to wave 0, which applies the rest.
 template <bool LINV>
 __device__ __forceinline__ bool takes_update(int type, int J, int k, int I) {
-  if (type == kColD) return I <= J || (LINV && k >= J + 1);  // U tile / diagonal, or identity column J+1
+  if (type == kColD) return (I <= J && (I <= J - 2 || k <= J - 3)) || (LINV && I > J && k >= J + 1);
   return type == kColI0 || type == kColEt || type == kColE || type == kColG;
 }
 
@@ -279,10 +296,10 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
   const int ob = blockIdx.x / split, sidx = blockIdx.x - ob * split;
   const int I = I0 + stride * ob, n = v.n, nt = n >> 4;
   const bool level = MODE == 0, right = level && I + h < v.p, first = sidx == 0;
-  for (int t = threadIdx.x; t < 4 * kMaxNt + kPairs + kMaxNt; t += blockDim.x) {
-    if (t < 4 * kMaxNt) sh.fG[t >> 2][t & 3] = 0;
-    else if (t < 4 * kMaxNt + kPairs) sh.fU[t - 4 * kMaxNt] = 0;
-    else sh.fD[t - 4 * kMaxNt - kPairs] = 0;
+  for (int t = threadIdx.x; t < 2 * kMaxNt + kPairs; t += blockDim.x) {
+    if (t < kMaxNt) sh.fT[t] = 0;
+    else if (t < kMaxNt + kPairs) sh.fU[t - kMaxNt] = 0;
+    else if (t < 2 * kMaxNt + kPairs) sh.fH[t - kMaxNt - kPairs] = 0;
   }
   __syncthreads();
   if (threadIdx.x == 0) AUG_PROF(0);
@@ -292,17 +309,45 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
   if (wave == 0) {  // ---- the diagonal wave
     __builtin_amdgcn_s_setprio(3);
     AUG_PROF(1);
+    double *Lb = blk(v.L, I, n);
+    d4 Dg = load_tile(Dblk, n, 0, 0, lane), P = {0.0, 0.0, 0.0, 0.0}, Q = P;
+    if (nt > 1) {
+      P = load_tile_t(Dblk, n, 0, 16, lane);  // U tile (0, 1) from the lower block (1, 0)
+      Q = load_tile(Dblk, n, 16, 16, lane);
+    }
     for (int k = 0; k < nt; ++k) {
-      d4 Dg;
-      if (k == 0) {
-        Dg = load_tile(Dblk, n, 0, 0, lane);
-      } else {
-        spin(&sh.fD[k]);
-        Dg = get_tile(sh.Dg[k], lane);
-      }
       AUG_STAMP(0, k, 0);
-      diag_groups(sh, k, Dg, lane, bad);
+      d4 Tt;
+      if (k + 1 < nt) diag_groups<true>(Dg, P, Q, Tt, lane, bad);
+      else diag_groups<false>(Dg, P, Q, Tt, lane, bad);
+      {  // T_k for the workers (row-major) and, U/T layout, for the back substitution
+        const int k4 = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sh.T[k][(k4 + 4 * j) * kTp + c] = Tt[j];
+        raise_flag(&sh.fT[k], lane);
+        if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * k, Tt, lane);
+      }
       AUG_PROF(2 + k);
+      if (k + 1 < nt) {  // U_k,k+1 feeds the trailing updates of row k+1
+        put_tile(sh.U[pair_id(k, k + 1)], P, lane);
+        raise_flag(&sh.fU[pair_id(k, k + 1)], lane);
+        if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * (k + 1), P, lane);
+      }
+      if (k + 2 < nt) {  // the next step's P = (k+1, k+2) and Q = (k+2, k+2) through step k
+        spin(&sh.fH[k + 2]);
+        d4 P2 = get_tile(sh.Hp[k + 2], lane), Q2 = get_tile(sh.Hq[k + 2], lane);
+        spin(&sh.fU[pair_id(k, k + 2)]);
+        const d4 X = get_tile(sh.U[pair_id(k, k + 2)], lane);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) Q2 = mfma(-X[s4], X[s4], Q2);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) P2 = mfma(-P[s4], X[s4], P2);
+        Dg = Q;
+        P = P2;
+        Q = Q2;
+      } else {
+        Dg = Q;
+      }
     }
     if (bad && lane == 0) v.flags[0] = 0;
     return;
@@ -338,8 +383,7 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
 #pragma unroll
   for (int k = 0; k < kMaxNt; ++k) {
     if (k >= nt) break;
-    // deferred trailing of step k-1: rows k+1 .. (the diagonal of column k+1
-    // took its step-(k-1) piece inside group_apply)
+    // deferred trailing of step k-1: rows k+1 .. (rows handed to wave 0 excluded)
     if (k >= 1) {
 #pragma unroll
       for (int r = k + 1; r < kMaxNt; ++r) {
@@ -351,34 +395,25 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
         for (int s = 0; s < 4; ++s) t[r] = mfma(-U[64 * s + lane], t[k - 1][s], t[r]);
       }
     }
+    if (type == kColD && k == J - 2 && k + 2 < kMaxNt) {  // rows J-1, J through step J-3: to wave 0
+      put_tile(sh.Hp[k + 2], t[k + 1], lane);
+      put_tile(sh.Hq[k + 2], t[k + 2], lane);
+      raise_flag(&sh.fH[k + 2], lane);
+    }
     AUG_STAMP(wave, k, 0);
-    // row k
-    const bool dtile = type == kColD && k < J, next = type == kColD && J == k + 1;
-    const bool rowk = type == kColT || (type == kColD ? (k < J || (LINV && k > J)) : true);
+    // row k: U_kJ (D column, k <= J-2), identity column J+1 (LINV, k > J), T, I0, E, g
+    const bool dtile = type == kColD && k <= J - 2;
+    const bool rowk = type == kColD ? (dtile || (LINV && k > J)) : type != kNone;
     if (rowk) {
-      if (type == kColT) t[k] = identity_tile(lane);
-      if (next) {
-        __builtin_amdgcn_s_setprio(2);
-        d4 dd = t[k + 1];
-        group_apply<true>(sh, k, t[k], dd, lane);
-        t[k + 1] = dd;
+      tile_trsm(sh, k, t[k], lane);
+      if (dtile) {  // U_kJ feeds the trailing updates of row J
         put_tile(sh.U[pair_id(k, J)], t[k], lane);
         raise_flag(&sh.fU[pair_id(k, J)], lane);
-        put_tile(sh.Dg[k + 1], t[k + 1], lane);  // the diagonal tile, complete: to wave 0
-        raise_flag(&sh.fD[k + 1], lane);
-        __builtin_amdgcn_s_setprio(0);
-      } else {
-        d4 none;
-        group_apply<false>(sh, k, t[k], none, lane);
-        if (dtile) {  // U_kJ feeds the trailing updates of row J
-          put_tile(sh.U[pair_id(k, J)], t[k], lane);
-          raise_flag(&sh.fU[pair_id(k, J)], lane);
-        }
       }
     }
     AUG_STAMP(wave, k, 1);
     // trailing of step k, row k+1 (the next step's row)
-    if (k + 1 < nt && rowk && type != kColT && !next && takes_update<LINV>(type, J, k, k + 1)) {
+    if (k + 1 < nt && rowk && takes_update<LINV>(type, J, k, k + 1)) {
       const int pid = pair_id(k, k + 1);
       spin(&sh.fU[pid]);
       const double *U = sh.U[pid];
@@ -395,10 +430,8 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
       if (LINV) {
         if (first && r > J) store_tile(Lb, n, 16 * r, 16 * (J + 1), t[r], lane);  // Linv block column J+1
       } else {
-        if (first && r < J) store_tile(Lb, n, 16 * r, 16 * J, t[r], lane);  // U tile (r, J)
+        if (first && r <= J - 2) store_tile(Lb, n, 16 * r, 16 * J, t[r], lane);  // U tile (r, J); (J-1, J): wave 0
       }
-    } else if (type == kColT) {
-      if (first) store_tile(Lb, n, 16 * r, 16 * r, t[r], lane);  // T_r on the diagonal
     } else if (type == kColI0) {
       if (first) store_tile(Lb, n, 16 * r, 0, t[r], lane);
     } else if (type == kColEt) {

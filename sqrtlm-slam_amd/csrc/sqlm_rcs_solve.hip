@@ -819,14 +819,8 @@ __global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
   const int I = TOP ? 0 : h + 2 * h * blockIdx.x, n = v.n, nt = n >> 4;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
   if (threadIdx.x < aug::kMaxNt) fx[threadIdx.x] = 0;
-  if (TOP) {
-    for (int k = threadIdx.x; k < n; k += blockDim.x) y[k] = v.g[(size_t)I * n + k];
-    __syncthreads();
-  } else {
-    cr_back_body<false>(v, h, I, y);  // ends with a barrier (also covers fx)
-  }
-  if (wave >= nt) return;
-  const int i = wave;
+  // this wave's U row and T_i first: in flight during the right-hand side
+  const int i = wave < nt ? wave : nt - 1;
   const double *Lb = blk(v.L, I, n);
   double u[aug::kMaxNt][4], tv[4];
 #pragma unroll
@@ -837,6 +831,13 @@ __global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
     }
 #pragma unroll
   for (int m = 0; m < 4; ++m) tv[m] = Lb[(size_t)(16 * i + 4 * q + m) * n + 16 * i + r];  // T_i[4q+m][r]
+  if (TOP) {
+    for (int k = threadIdx.x; k < n; k += blockDim.x) y[k] = v.g[(size_t)I * n + k];
+    __syncthreads();
+  } else {
+    cr_back_body<false>(v, h, I, y);  // ends with a barrier (also covers fx)
+  }
+  if (wave >= nt) return;
   double acc = 0.0;
 #pragma unroll
   for (int j = aug::kMaxNt - 1; j > 0; --j)
@@ -1288,8 +1289,58 @@ __global__ __launch_bounds__(512) void k_cr_factor_at(CRView v, int I) {
   cr_factor_store(v, I, lds, &fail);
 }
 
+// A_I = L^-1 E_{I-h}^T and C_I = L^-1 E_I for the odd superblocks of level h
+// by forward substitution with the factor k_cr_aug<1, false> left in L_I (U tiles
+// above the diagonal, T_k = L_kk^-1 on it): for k = 0 .. nt-1, X_k = T_k M_k,
+// then M_r -= U_kr^T X_k (r > k); tiles in the MFMA accumulator layout as in
+// k_cr_aug. One wavefront per 16-column strip: the levels with many odd
+// superblocks (the fused kernel would need more workgroups than CUs) run the
+// factor and this kernel instead.
+__global__ __launch_bounds__(256) void k_cr_trsm(CRView v, int h, int total) {
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= total) return;
+  const int n = v.n, nt = n >> 4, lane = threadIdx.x & 63, b = lane >> 4, i16 = lane & 15;
+  const int ob = gw / (2 * nt), s = gw - ob * 2 * nt, I = h + 2 * h * ob;
+  const bool et = s < nt;
+  const int J = et ? s : s - nt;
+  if (!et && I + h >= v.p) return;
+  const double *Lb = blk(v.L, I, n);
+  d4 t[aug::kMaxNt];
+#pragma unroll
+  for (int r = 0; r < aug::kMaxNt; ++r)
+    if (r < nt)
+      t[r] = et ? aug::load_tile_t(blk(v.E, I - h, n), n, 16 * r, 16 * J, lane)
+                : aug::load_tile(blk(v.E, I, n), n, 16 * r, 16 * J, lane);
+#pragma unroll
+  for (int k = 0; k < aug::kMaxNt; ++k) {
+    if (k >= nt) break;
+    double ta[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) ta[m] = Lb[(size_t)(16 * k + i16) * n + 16 * k + 4 * m + b];  // T_k[i][4m+b]
+    d4 x = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) x = aug::mfma(ta[m], t[k][m], x);
+    t[k] = x;
+#pragma unroll
+    for (int r = k + 1; r < aug::kMaxNt; ++r)
+      if (r < nt) {
+        const d4 u = aug::load_tile(Lb, n, 16 * k, 16 * r, lane);  // U_kr
+#pragma unroll
+        for (int m = 0; m < 4; ++m) t[r] = aug::mfma(-u[m], t[k][m], t[r]);
+      }
+  }
+  double *out = blk(et ? v.A : v.C, I, n);
+#pragma unroll
+  for (int r = 0; r < aug::kMaxNt; ++r)
+    if (r < nt) aug::store_tile(out, n, 16 * r, 16 * J, t[r], lane);
+}
+
 // SQLM_CR_LEGACY=1: the round-2 factor (panel Cholesky + explicit Linv in LDS,
 // k_cr_factor / k_cr_factor_elim / k_cr_top) instead of k_cr_aug (A/B only).
+// odd superblocks x minimum split above which a level runs factor + TRSM
+// instead of the fused k_cr_aug (SQLM_CR_WIDE overrides)
+static const int kCrAugWideWGs = std::getenv("SQLM_CR_WIDE") ? std::atoi(std::getenv("SQLM_CR_WIDE")) : 160;
+
 inline bool cr_legacy() {
   static const bool on = std::getenv("SQLM_CR_LEGACY") != nullptr;
   return on;
@@ -1313,6 +1364,19 @@ static void launch_cr_level(const CRView &v, int h, int n_odd, int fuse_min, boo
   const int nt = v.n / 16;
   if (!cr_legacy()) {
     const int sp = aug_split(n_odd, nt, linv, aug::extra_columns(nt, true, true));
+    if ((int64_t)n_odd * aug::min_split(nt, linv, aug::extra_columns(nt, true, true)) > kCrAugWideWGs) {
+      // too many odd superblocks for the fused kernel's workgroups on one
+      // round of CUs: the factor alone, then the strips as a wide kernel
+      launch_cr_factor(v, h, h, 2 * h, n_odd, linv, st);
+      if (linv) {
+        const int per = nt * nt;
+        hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
+      } else {
+        const int total = n_odd * 2 * nt;
+        hipLaunchKernelGGL(k_cr_trsm, dim3((total + 3) / 4), dim3(256), 0, st, v, h, total);
+      }
+      return;
+    }
     if (linv)
       hipLaunchKernelGGL((k_cr_aug<0, true>), dim3(n_odd * sp), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, h, 2 * h, sp);
     else

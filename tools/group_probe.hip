@@ -13,11 +13,11 @@ using sqlm::d4;
 // 2: 15 more waves running MFMA chains; 3: VALU/readlane part only (no MFMA)
 __global__ __launch_bounds__(1024) void k_probe(double *out, long long *cyc, int mode) {
   __shared__ int done;
-  __shared__ sqlm::aug::Shared sh;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) done = 0;
   __syncthreads();
   if (wave == 0) {
+    if (mode == 4) __builtin_amdgcn_s_setprio(3);
     d4 t;
     const int k4 = lane >> 4, c = lane & 15;
 #pragma unroll
@@ -45,9 +45,10 @@ __global__ __launch_bounds__(1024) void k_probe(double *out, long long *cyc, int
         }
         Tt = t;
       } else {
-        if (lane == 0) for (int a = 0; a < 4; ++a) sh.fG[0][a] = 0;
-        sqlm::aug::diag_groups(sh, 0, t, lane, bad);
-        Tt = t;
+        d4 P = t, Q = t, T2;
+        if (mode == 4) sqlm::aug::diag_groups<true>(t, P, Q, T2, lane, bad);
+        else sqlm::aug::diag_groups<false>(t, P, Q, T2, lane, bad);
+        Tt = T2 + P + Q;
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) t[j] += 1e-30 * Tt[j];
@@ -73,15 +74,16 @@ int main() {
   double *out;
   long long *cyc, h;
   if (hipMalloc(&out, 4096 * 8) != hipSuccess || hipMalloc(&cyc, 8) != hipSuccess) return 1;
-  const char *names[] = {"alone", "with_15_spinning", "with_15_mfma", "valu_readlane_only"};
+  const char *names[] = {"alone", "with_15_spinning", "with_15_mfma", "valu_readlane_only",
+                         "alone_with_PQ"};
   std::printf("{");
-  for (int mode = 0; mode < 4; ++mode) {
-    const int threads = mode == 0 || mode == 3 ? 64 : 1024;
+  for (int mode = 0; mode < 5; ++mode) {
+    const int threads = mode == 0 || mode == 3 || mode == 4 ? 64 : 1024;
     hipLaunchKernelGGL(k_probe, dim3(1), dim3(threads), 0, 0, out, cyc, mode);
     hipLaunchKernelGGL(k_probe, dim3(1), dim3(threads), 0, 0, out, cyc, mode);
     if (hipDeviceSynchronize() != hipSuccess) return 2;
     if (hipMemcpy(&h, cyc, 8, hipMemcpyDeviceToHost) != hipSuccess) return 3;
-    std::printf("\"diag_groups_%s\": %lld%s", names[mode], h, mode < 3 ? ", " : "");
+    std::printf("\"diag_groups_%s\": %lld%s", names[mode], h, mode < 4 ? ", " : "");
   }
   std::printf("}\n");
   return 0;
