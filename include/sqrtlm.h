@@ -142,6 +142,12 @@ int sqlm_eg_optimize(sqlm_ctx *ctx, int iterations, double user_lambda, const vo
 int sqlm_eg_get_poses(sqlm_ctx *ctx, double *Siw);
 /* e->chi2() from the last computed error (g2o semantics). */
 int sqlm_eg_get_edge_chi2(sqlm_ctx *ctx, double *chi2);
+/* The numeric Jacobians EdgeSim3::linearizeOplus computes at the current
+ * estimates (BaseBinaryEdge, base_binary_edge.hpp:131-205: central differences
+ * through oplus, delta 1e-9), on the GPU with the arithmetic of the optimizer's
+ * k_eg_linearize: J [n_edge][2][7][7] row-major, [e][0] = d e / d S_i,
+ * [e][1] = d e / d S_j, zero for a fixed vertex. Diagnostics / parity tests. */
+int sqlm_eg_get_jacobians(sqlm_ctx *ctx, double *J);
 
 /* Results (write-back inputs, g2oOptimizer.cc:1167-1189, :306-360). */
 int sqlm_get_poses(sqlm_ctx *ctx, double *pose_q, double *pose_t);

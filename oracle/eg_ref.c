@@ -15,6 +15,7 @@
 
 #include "oracle.h"
 #include "se3_ref.h"
+#include "sqlm_libm.h" /* exp / log / sin / cos / acos, the same bits as the GPU (include/) */
 #include "skyline_ref.h"
 
 /* ------------------------------------------------------------ Sim3 (sim3.h) */
@@ -43,7 +44,7 @@ void orc_sim3_from_update(const double u[7], double S[8]) {
   const double theta = norm3(omega);
   double O[9], O2[9], R[9];
   skew3(omega, O);
-  const double s = exp(sigma);
+  const double s = sqlm_exp(sigma);
   o3_matmul(O, O, O2);
   const double eps = 0.00001;
   double A, B, C;
@@ -55,9 +56,9 @@ void orc_sim3_from_update(const double u[7], double S[8]) {
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + O[k]) + O2[k];
     } else {
       const double theta2 = theta * theta;
-      A = (1 - cos(theta)) / (theta2);
-      B = (theta - sin(theta)) / (theta2 * theta);
-      const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+      A = (1 - sqlm_cos(theta)) / (theta2);
+      B = (theta - sqlm_sin(theta)) / (theta2 * theta);
+      const double a = sqlm_sin(theta) / theta, b = (1 - sqlm_cos(theta)) / (theta * theta);
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + a * O[k]) + b * O2[k];
     }
   } else {
@@ -68,9 +69,9 @@ void orc_sim3_from_update(const double u[7], double S[8]) {
       B = ((0.5 * sigma2 - sigma + 1) * s) / (sigma2 * sigma);
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + O[k]) + O2[k];
     } else {
-      const double ra = sin(theta) / theta, rb = (1 - cos(theta)) / (theta * theta);
+      const double ra = sqlm_sin(theta) / theta, rb = (1 - sqlm_cos(theta)) / (theta * theta);
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + ra * O[k]) + rb * O2[k];
-      const double a = s * sin(theta), b = s * cos(theta);
+      const double a = s * sqlm_sin(theta), b = s * sqlm_cos(theta);
       const double theta2 = theta * theta, sigma2 = sigma * sigma, c = theta2 + sigma2;
       A = (a * sigma + (1 - b) * theta) / (theta * c);
       B = (C - ((b - 1) * sigma + a * theta) / (c)) * 1. / (theta2);
@@ -117,9 +118,15 @@ static void lu_solve3(const double Win[9], const double b[3], double x[3]) {
 }
 
 /* Sim3::log (sim3.h:147-237). */
+void orc_libm(int fn, const double *x, double *y, int n) {
+  for (int i = 0; i < n; ++i)
+    y[i] = fn == 0 ? sqlm_exp(x[i]) : fn == 1 ? sqlm_log(x[i]) : fn == 2 ? sqlm_sin(x[i])
+         : fn == 3 ? sqlm_cos(x[i]) : sqlm_acos(x[i]);
+}
+
 void orc_sim3_log(const double S[8], double out[7]) {
   const double s = S[7];
-  const double sigma = log(s);
+  const double sigma = sqlm_log(s);
   double R[9], omega[3], O[9], dr[3];
   oq_to_mat(S, R);
   const double d = 0.5 * (R[0] + R[4] + R[8] - 1);
@@ -133,11 +140,11 @@ void orc_sim3_log(const double S[8], double out[7]) {
       A = 1. / 2.;
       B = 1. / 6.;
     } else {
-      const double theta = acos(d), theta2 = theta * theta;
+      const double theta = sqlm_acos(d), theta2 = theta * theta;
       const double f = theta / (2 * sqrt(1 - d * d));
       for (int k = 0; k < 3; ++k) omega[k] = f * dr[k];
-      A = (1 - cos(theta)) / (theta2);
-      B = (theta - sin(theta)) / (theta2 * theta);
+      A = (1 - sqlm_cos(theta)) / (theta2);
+      B = (theta - sqlm_sin(theta)) / (theta2 * theta);
     }
   } else {
     C = (s - 1) / sigma;
@@ -147,11 +154,11 @@ void orc_sim3_log(const double S[8], double out[7]) {
       A = ((sigma - 1) * s + 1) / (sigma2);
       B = ((0.5 * sigma2 - sigma + 1) * s) / (sigma2 * sigma);
     } else {
-      const double theta = acos(d);
+      const double theta = sqlm_acos(d);
       const double f = theta / (2 * sqrt(1 - d * d));
       for (int k = 0; k < 3; ++k) omega[k] = f * dr[k];
       const double theta2 = theta * theta;
-      const double a = s * sin(theta), b = s * cos(theta);
+      const double a = s * sqlm_sin(theta), b = s * sqlm_cos(theta);
       const double c = theta2 + sigma * sigma;
       A = (a * sigma + (1 - b) * theta) / (theta * c);
       B = (C - ((b - 1) * sigma + a * theta) / (c)) * 1. / (theta2);

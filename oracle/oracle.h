@@ -134,6 +134,8 @@ int orc_eg_optimize(orc_eg_graph *g, int iterations, double user_lambda, const v
                     orc_stats *st);
 void orc_sim3_from_update(const double u[7], double S[8]);
 void orc_sim3_log(const double S[8], double out[7]);
+/* include/sqlm_libm.h on n arguments: fn 0 exp, 1 log, 2 sin, 3 cos, 4 acos */
+void orc_libm(int fn, const double *x, double *y, int n);
 void orc_sim3_mul(const double a[8], const double b[8], double out[8]);
 void orc_sim3_inverse(const double a[8], double out[8]);
 void orc_eg_edge_error(const double Si[8], const double Sj[8], const double C[8], double e[7]);

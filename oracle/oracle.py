@@ -259,6 +259,15 @@ def sim3_from_update(u):
     return S
 
 
+def libm(fn: str, x):
+    """include/sqlm_libm.h (the bits the GPU's Sim3 code computes) on an array."""
+    x = np.ascontiguousarray(x, np.float64).reshape(-1)
+    y = np.zeros_like(x)
+    code = {"exp": 0, "log": 1, "sin": 2, "cos": 3, "acos": 4}[fn]
+    lib().orc_libm(code, _p(x), _p(y), x.size)
+    return y
+
+
 def sim3_log(S):
     o = np.zeros(7)
     lib().orc_sim3_log(_f(S), _p(o))

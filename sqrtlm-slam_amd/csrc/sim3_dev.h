@@ -5,9 +5,12 @@
 //   EdgeSim3::computeError                     types_seven_dof_expmap.h:106-114
 //   numeric Jacobian (delta = 1e-9, central)   core/base_binary_edge.hpp:131-205
 // S = [qx qy qz qw tx ty tz s]. Like se3_dev.h, evaluated without FMA
-// contraction: the numeric Jacobians divide error differences by 2e-9.
+// contraction: the numeric Jacobians divide error differences by 2e-9. The
+// transcendental functions are sqlm_libm.h's, shared with the oracle, so the
+// Jacobians are the oracle's bit for bit.
 #pragma once
 #include "se3_dev.h"
+#include "../../include/sqlm_libm.h"
 
 namespace sqlm {
 
@@ -24,7 +27,7 @@ SQLM_HD void sim3_from_update(const double u[7], double S[8]) {
   const double theta = sqrt((omega[0] * omega[0] + omega[1] * omega[1]) + omega[2] * omega[2]);
   double O[9], O2[9], R[9];
   skew3(omega, O);
-  const double s = exp(sigma);
+  const double s = sqlm_exp(sigma);
   mat3_mul(O, O, O2);
   const double eps = 0.00001;
   double A, B, C;
@@ -37,9 +40,9 @@ SQLM_HD void sim3_from_update(const double u[7], double S[8]) {
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + O[k]) + O2[k];
     } else {
       const double theta2 = theta * theta;
-      A = (1 - cos(theta)) / (theta2);
-      B = (theta - sin(theta)) / (theta2 * theta);
-      const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta);
+      A = (1 - sqlm_cos(theta)) / (theta2);
+      B = (theta - sqlm_sin(theta)) / (theta2 * theta);
+      const double a = sqlm_sin(theta) / theta, b = (1 - sqlm_cos(theta)) / (theta * theta);
 #pragma unroll
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + a * O[k]) + b * O2[k];
     }
@@ -52,10 +55,10 @@ SQLM_HD void sim3_from_update(const double u[7], double S[8]) {
 #pragma unroll
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + O[k]) + O2[k];
     } else {
-      const double ra = sin(theta) / theta, rb = (1 - cos(theta)) / (theta * theta);
+      const double ra = sqlm_sin(theta) / theta, rb = (1 - sqlm_cos(theta)) / (theta * theta);
 #pragma unroll
       for (int k = 0; k < 9; ++k) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + ra * O[k]) + rb * O2[k];
-      const double a = s * sin(theta), b = s * cos(theta);
+      const double a = s * sqlm_sin(theta), b = s * sqlm_cos(theta);
       const double theta2 = theta * theta, sigma2 = sigma * sigma, c = theta2 + sigma2;
       A = (a * sigma + (1 - b) * theta) / (theta * c);
       B = (C - ((b - 1) * sigma + a * theta) / (c)) * 1. / (theta2);
@@ -106,7 +109,7 @@ SQLM_HD void lu_solve3(const double Win[9], const double b[3], double x[3]) {
 
 SQLM_HD void sim3_log(const double S[8], double out[7]) {
   const double s = S[7];
-  const double sigma = log(s);
+  const double sigma = sqlm_log(s);
   double R[9], omega[3], O[9], dr[3];
   q_to_mat(S, R);
   const double d = 0.5 * (R[0] + R[4] + R[8] - 1);
@@ -123,12 +126,12 @@ SQLM_HD void sim3_log(const double S[8], double out[7]) {
       A = 1. / 2.;
       B = 1. / 6.;
     } else {
-      const double theta = acos(d), theta2 = theta * theta;
+      const double theta = sqlm_acos(d), theta2 = theta * theta;
       const double f = theta / (2 * sqrt(1 - d * d));
 #pragma unroll
       for (int k = 0; k < 3; ++k) omega[k] = f * dr[k];
-      A = (1 - cos(theta)) / (theta2);
-      B = (theta - sin(theta)) / (theta2 * theta);
+      A = (1 - sqlm_cos(theta)) / (theta2);
+      B = (theta - sqlm_sin(theta)) / (theta2 * theta);
     }
   } else {
     C = (s - 1) / sigma;
@@ -139,12 +142,12 @@ SQLM_HD void sim3_log(const double S[8], double out[7]) {
       A = ((sigma - 1) * s + 1) / (sigma2);
       B = ((0.5 * sigma2 - sigma + 1) * s) / (sigma2 * sigma);
     } else {
-      const double theta = acos(d);
+      const double theta = sqlm_acos(d);
       const double f = theta / (2 * sqrt(1 - d * d));
 #pragma unroll
       for (int k = 0; k < 3; ++k) omega[k] = f * dr[k];
       const double theta2 = theta * theta;
-      const double a = s * sin(theta), b = s * cos(theta);
+      const double a = s * sqlm_sin(theta), b = s * sqlm_cos(theta);
       const double c = theta2 + sigma * sigma;
       A = (a * sigma + (1 - b) * theta) / (theta * c);
       B = (C - ((b - 1) * sigma + a * theta) / (c)) * 1. / (theta2);
@@ -194,7 +197,7 @@ SQLM_HD void sim3_oplus(double S[8], const double upd[7], bool fix_scale) {
   for (int k = 0; k < 8; ++k) S[k] = o[k];
 }
 
-// EdgeSim3 error: log(C * Si * Sj^-1)
+// EdgeSim3 error: sqlm_log(C * Si * Sj^-1)
 SQLM_HD void eg_edge_error(const double Si[8], const double Sj[8], const double C[8], double e[7]) {
   double a[8], b[8], jinv[8];
   sim3_mul(C, Si, a);

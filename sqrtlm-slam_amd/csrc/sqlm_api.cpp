@@ -1738,6 +1738,12 @@ int sqlm_eg_get_edge_chi2(sqlm_ctx *c, double *chi2) {
   return eg_get_edge_chi2(c->eg, chi2);
 }
 
+int sqlm_eg_get_jacobians(sqlm_ctx *c, double *J) {
+  if (!c || !c->eg) return SQLM_ERR_STATE;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  return eg_get_jacobians(c->eg, J);
+}
+
 int sqlm_global_ba(sqlm_ctx *c, int iterations, const volatile uint8_t *stop, sqlm_stats *st, int *n_iter) {
   return sqlm_optimize(c, 0, iterations, 0.0, stop, st, n_iter);
 }

@@ -225,6 +225,16 @@ __device__ __forceinline__ d4 load_tile_t(const double *P, int n, int r0, int c0
   for (int j = 0; j < 4; ++j) t[j] = P[(size_t)(c0 + c) * n + r0 + k4 + 4 * j];
   return t;
 }
+// diagonal tile (r0, r0) from its lower triangle (the dense solvers keep only
+// that one; a symmetric block gives the same bits as load_tile)
+__device__ __forceinline__ d4 load_tile_sym(const double *P, int n, int r0, int lane) {
+  const int k4 = lane >> 4, c = lane & 15;
+  const d4 lo = load_tile(P, n, r0, r0, lane), up = load_tile_t(P, n, r0, r0, lane);
+  d4 t;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t[j] = k4 + 4 * j >= c ? lo[j] : up[j];
+  return t;
+}
 __device__ __forceinline__ void store_tile(double *P, int n, int r0, int c0, const d4 &t, int lane) {
   const int k4 = lane >> 4, c = lane & 15;
 #pragma unroll
@@ -304,16 +314,21 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
   __syncthreads();
   if (threadIdx.x == 0) AUG_PROF(0);
   AUG_HWID(wave);
-  const double *Dblk = blk(v.D, I, n);
+  // MODE 1 with v.ld: one diagonal block of a larger dense matrix (row stride ld)
+  // (its diagonal tiles are read from their lower triangles: the dense solver
+  // keeps only that one; the CR superblocks are stored whole)
+  const bool dense = MODE == 1 && v.ld;
+  const int ldd = dense ? v.ld : n;
+  const double *Dblk = dense ? v.D : blk(v.D, I, n);
   bool bad = false;
   if (wave == 0) {  // ---- the diagonal wave
     __builtin_amdgcn_s_setprio(3);
     AUG_PROF(1);
     double *Lb = blk(v.L, I, n);
-    d4 Dg = load_tile(Dblk, n, 0, 0, lane), P = {0.0, 0.0, 0.0, 0.0}, Q = P;
+    d4 Dg = dense ? load_tile_sym(Dblk, ldd, 0, lane) : load_tile(Dblk, n, 0, 0, lane), P = {0.0, 0.0, 0.0, 0.0}, Q = P;
     if (nt > 1) {
-      P = load_tile_t(Dblk, n, 0, 16, lane);  // U tile (0, 1) from the lower block (1, 0)
-      Q = load_tile(Dblk, n, 16, 16, lane);
+      P = load_tile_t(Dblk, ldd, 0, 16, lane);  // U tile (0, 1) from the lower block (1, 0)
+      Q = dense ? load_tile_sym(Dblk, ldd, 16, lane) : load_tile(Dblk, n, 16, 16, lane);
     }
     for (int k = 0; k < nt; ++k) {
       AUG_STAMP(0, k, 0);
@@ -364,8 +379,8 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
     t[r] = d4{0.0, 0.0, 0.0, 0.0};
     if (r >= nt) continue;
     if (type == kColD) {
-      if (r < J) t[r] = load_tile_t(Dblk, n, 16 * r, 16 * J, lane);  // U tile (r, J) from the lower block (J, r)
-      else if (r == J) t[r] = load_tile(Dblk, n, 16 * r, 16 * J, lane);
+      if (r < J) t[r] = load_tile_t(Dblk, ldd, 16 * r, 16 * J, lane);  // U tile (r, J) from the lower block (J, r)
+      else if (r == J) t[r] = dense ? load_tile_sym(Dblk, ldd, 16 * r, lane) : load_tile(Dblk, n, 16 * r, 16 * J, lane);
       else if (LINV && r == J + 1) t[r] = identity_tile(lane);
     } else if (type == kColI0) {
       if (r == 0) t[r] = identity_tile(lane);

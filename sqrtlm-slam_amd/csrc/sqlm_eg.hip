@@ -208,6 +208,38 @@ __global__ __launch_bounds__(256) void k_eg_linearize(EGDev d, const double *__r
   }
 }
 
+// sqlm_eg_get_jacobians: one thread per (edge, side, dimension), the same
+// perturbation, error and difference arithmetic as k_eg_linearize's lanes.
+__global__ __launch_bounds__(256) void k_eg_jacobians(const double *__restrict__ S, const int32_t *__restrict__ ei,
+                                                      const int32_t *__restrict__ ej, const double *__restrict__ C,
+                                                      const uint8_t *__restrict__ fixed, int fix_scale, int64_t nE,
+                                                      double *__restrict__ J) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 14 * nE) return;
+  const int64_t k = t / 14;
+  const int side = (int)(t % 14) / 7, dim = (int)(t % 7);
+  const int vi = ei[k], vj = ej[k];
+  double *o = J + 98 * k + 49 * side;
+  if (fixed[side == 0 ? vi : vj]) {
+    for (int r = 0; r < 7; ++r) o[7 * r + dim] = 0.0;
+    return;
+  }
+  double e2[2][7];
+  for (int m = 0; m < 2; ++m) {
+    double Si[8], Sj[8], add[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < 8; ++c) { Si[c] = S[8 * vi + c]; Sj[c] = S[8 * vj + c]; }
+    add[dim] = m ? -1e-9 : 1e-9;
+    sim3_oplus(side == 0 ? Si : Sj, add, fix_scale != 0);
+    eg_edge_error(Si, Sj, C + 8 * k, e2[m]);
+  }
+  const double scalar = 1.0 / (2 * 1e-9);
+  for (int r = 0; r < 7; ++r) {
+    double bak = e2[0][r];
+    bak -= e2[1][r];
+    o[7 * r + dim] = scalar * bak;
+  }
+}
+
 // One wavefront per destination: a 7x7 block of H0 (lower) or a b vector;
 // contributions summed in edge order.
 __global__ __launch_bounds__(64) void k_eg_assemble(EGDev d, int nD) {
@@ -763,6 +795,32 @@ int eg_get_poses(const EGSolver *s, double *Siw) {
   if (!Siw && s->nK) return SQLM_ERR_INVALID_ARG;
   std::memcpy(Siw, s->S.data(), s->S.size() * sizeof(double));
   return SQLM_OK;
+}
+
+int eg_get_jacobians(EGSolver *s, double *J) {
+  if (!J && s->nE) return SQLM_ERR_INVALID_ARG;
+  if (s->nE == 0) return SQLM_OK;
+  std::vector<void *> keep;
+  keep.swap(s->mem);  // the optimizer's buffers stay as they are
+  int rc = SQLM_OK;
+  double *dS = s->upload(s->S), *dC = s->upload(s->C);
+  int32_t *dei = s->upload(s->ei), *dej = s->upload(s->ej);
+  uint8_t *dfx = s->upload(s->fixed);
+  double *dJ = s->alloc<double>(98 * (size_t)s->nE);
+  if (!dS || !dC || !dei || !dej || !dfx || !dJ) {
+    rc = SQLM_ERR_HIP;
+  } else {
+    const int64_t n = 14 * s->nE;
+    hipLaunchKernelGGL(k_eg_jacobians, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s->st, dS, dei, dej, dC, dfx,
+                       s->fix_scale, s->nE, dJ);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpyAsync(J, dJ, 98 * sizeof(double) * (size_t)s->nE, hipMemcpyDeviceToHost, s->st) != hipSuccess ||
+        hipStreamSynchronize(s->st) != hipSuccess)
+      rc = SQLM_ERR_HIP;
+  }
+  s->release();
+  s->mem.swap(keep);
+  return rc;
 }
 
 int eg_get_edge_chi2(const EGSolver *s, double *chi2) {

@@ -290,6 +290,7 @@ int eg_optimize(EGSolver *s, int iterations, double user_lambda, const volatile 
                 int *n_iter);
 int eg_get_poses(const EGSolver *s, double *Siw);
 int eg_get_edge_chi2(const EGSolver *s, double *chi2);
+int eg_get_jacobians(EGSolver *s, double *J);
 
 // ORB front end (sqlm_orb.hip): one engine per context, on the context's stream.
 struct OrbEngine;

@@ -348,6 +348,7 @@ struct CRView {
   double *D, *E, *A, *C, *g, *x;  // [p][n][n] x4, [p][n] x2
   int *flags;
   double *L;  // [p][n][n]: Linv_I of every factored superblock
+  int ld;     // k_cr_aug<1, *> only: nonzero = D is one block with this row stride (dense solve)
 };
 
 __device__ __forceinline__ double *blk(double *base, int I, int n) { return base + (size_t)I * n * n; }
@@ -898,7 +899,7 @@ __global__ __launch_bounds__(512) void k_dchol_diag(DenseView v, int k, int nk) 
     for (int c = lane; c < nb; c += 64)
       Lo[r * nb + c] = (r < nk && c < nk) ? linv_at(L, ld, Dinv, r, c) : (r == c ? 1.0 : 0.0);
   // fused forward step: y_k = Linv_kk r_k (r_k already holds every earlier
-  // block's update) into x_k; thread (row, quarter), quarters summed in order
+  // block's update) in place; thread (row, quarter), quarters summed in order
   constexpr int q = nb / 4;
   const int t = threadIdx.x, row = t % nb, h = t / nb;
   const double *rk = v.r + (size_t)k * nb;
@@ -914,7 +915,7 @@ __global__ __launch_bounds__(512) void k_dchol_diag(DenseView v, int k, int nk) 
     W[h * nb + row] = h == 0 ? rk[row] : 0.0;  // identity row
   }
   __syncthreads();
-  if (t < nb) v.x[(size_t)k * nb + t] = ((W[t] + W[nb + t]) + W[2 * nb + t]) + W[3 * nb + t];
+  if (t < nb) v.r[(size_t)k * nb + t] = ((W[t] + W[nb + t]) + W[2 * nb + t]) + W[3 * nb + t];
 }
 
 // 16x16 tile of X Y^T over K = kend (X, Y row-major with their own leading dims).
@@ -1065,34 +1066,14 @@ __global__ __launch_bounds__(512) void k_dchol_update_blk(DenseView v, int k, Ro
   }
 }
 
-// forward: y_k = Linv_kk r_k (into x): thread (r, quarter) sums its 28
-// columns m <= r (fixed trip count, every load in flight at once), the four
-// quarters are added in LDS in a fixed order.
-__global__ __launch_bounds__(512) void k_dtrsv_fwd_diag(DenseView v, int k) {
-  constexpr int nb = kCRMaxN, q = nb / 4;
-  __shared__ double part[4][nb];
-  const int t = threadIdx.x, r = t % nb, h = t / nb;
-  const double *Lk = v.Linv + (size_t)k * nb * nb, *rk = v.r + (size_t)k * nb;
-  if (h < 4) {
-    double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < q; ++i) {
-      const int m = h * q + i;
-      s += m <= r ? Lk[(size_t)r * nb + m] * rk[m] : 0.0;
-    }
-    part[h][r] = s;
-  }
-  __syncthreads();
-  if (t < nb) v.x[(size_t)k * nb + t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
-}
-
 // one wavefront per row of the block rows rs below block k: r_i -= L_i,k-block . y_k
+// (y_k in r_k: the diagonal step forms it in place)
 __global__ __launch_bounds__(256) void k_dtrsv_fwd_update(DenseView v, int k, RowSet rs) {
   constexpr int nb = kCRMaxN;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (q >= rs.count() * nb) return;
   const int row = rs.at(q / nb) * nb + q % nb;
-  const double *Lr = v.L + (size_t)row * v.n + (size_t)k * nb, *y = v.x + (size_t)k * nb;
+  const double *Lr = v.L + (size_t)row * v.n + (size_t)k * nb, *y = v.r + (size_t)k * nb;
   double s = 0.0;
   for (int m = lane; m < nb; m += 64) s += Lr[m] * y[m];
   s = wave_sum_d(s);
@@ -1132,6 +1113,9 @@ __global__ __launch_bounds__(256) void k_dtrsv_bwd_update(DenseView v, int k, in
   v.r[c] -= (s[0] + s[1]) + (s[2] + s[3]);
 }
 
+inline bool cr_legacy();
+static void launch_cr_factor(const CRView &v, int h, int I0, int stride, int count, bool linv, hipStream_t st);
+
 int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double *x, int *flags, int n,
                            hipStream_t st, int band, int n_last) {
   constexpr int nb = kCRMaxN, nt = nb / 16;
@@ -1142,10 +1126,18 @@ int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double
   DenseView v{n, nblk, A, L, Linv, r, x, flags};
   const size_t lds = cr_factor_lds(nb);
   // factor + forward substitution in one sweep: block k's diagonal kernel also
-  // forms y_k = Linv_kk r_k, then the panel, the trailing update and
-  // r_i -= L_ik y_k for the rows below
+  // forms y_k = Linv_kk r_k (in place), then the panel, the trailing update and
+  // r_i -= L_ik y_k for the rows below. The diagonal factor is the augmented
+  // MFMA Cholesky of sqlm_cr_aug.h on the block in place (row stride n; the
+  // identity padding of a ragged last block factors to itself exactly).
   for (int k = 0; k < nblk; ++k) {
-    hipLaunchKernelGGL(k_dchol_diag, dim3(1), dim3(512), lds, st, v, k, k == nblk - 1 ? n_last : nb);
+    if (cr_legacy()) {
+      hipLaunchKernelGGL(k_dchol_diag, dim3(1), dim3(512), lds, st, v, k, k == nblk - 1 ? n_last : nb);
+    } else {
+      const CRView dv{1, nb, 0, 0, A + (size_t)k * nb * n + (size_t)k * nb, nullptr, nullptr, nullptr,
+                      r + (size_t)k * nb, nullptr, flags, Linv + (size_t)k * nb * nb, n};
+      launch_cr_factor(dv, 0, 0, 0, 1, true, st);
+    }
     const RowSet rs = rows_below(k, nblk, band);
     const int m = rs.count();
     if (m == 0) continue;
@@ -1158,8 +1150,7 @@ int launch_dense_spd_solve(double *A, double *L, double *Linv, double *r, double
       hipLaunchKernelGGL(k_dchol_update_blk, dim3(xcd_grid(npairs)), dim3(512), 0, st, v, k, rs, npairs);
     hipLaunchKernelGGL(k_dtrsv_fwd_update, dim3((m * nb + 3) / 4), dim3(256), 0, st, v, k, rs);
   }
-  // y (in x) becomes the right-hand side of the backward pass
-  if (hipMemcpyAsync(r, x, sizeof(double) * n, hipMemcpyDeviceToDevice, st) != hipSuccess) return -2;
+  // y (in r) is the right-hand side of the backward pass
   for (int k = nblk - 1; k >= 0; --k) {
     hipLaunchKernelGGL(k_dtrsv_bwd_diag, dim3(1), dim3(512), 0, st, v, k);
     // L_kj != 0: j = k - 1 for a band block, every j < k for a border block
@@ -1218,9 +1209,7 @@ __device__ __forceinline__ void mm_store(double *C, int ldc, int ti, int tj, con
 }
 
 // Z_I = Linv_I G_I for I = I0 + stride q (Linv lower: K up to the tile row)
-__global__ __launch_bounds__(64) void k_crm_fwd(CRMView v, int I0, int stride, int total) {
-  const int lb = xcd_block(total);
-  if (lb >= total) return;
+__device__ __forceinline__ void crm_fwd_item(const CRMView &v, int I0, int stride, int lb) {
   const int nt = v.n >> 4, rt = v.R >> 4, per = nt * rt;
   const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, I = I0 + stride * q;
   const size_t nn = (size_t)v.n * v.n, nr = (size_t)v.n * v.R;
@@ -1228,10 +1217,13 @@ __global__ __launch_bounds__(64) void k_crm_fwd(CRMView v, int I0, int stride, i
   mm_store(v.Z + I * nr, v.R, ti, tj, acc, 1.0, false);
 }
 
-// even J = 2 h q: G_J -= A_{J+h}^T Z_{J+h} + C_{J-h}^T Z_{J-h}
-__global__ __launch_bounds__(64) void k_crm_upd(CRMView v, int h, int total) {
+__global__ __launch_bounds__(64) void k_crm_fwd(CRMView v, int I0, int stride, int total) {
   const int lb = xcd_block(total);
-  if (lb >= total) return;
+  if (lb < total) crm_fwd_item(v, I0, stride, lb);
+}
+
+// even J = 2 h q: G_J -= A_{J+h}^T Z_{J+h} + C_{J-h}^T Z_{J-h}
+__device__ __forceinline__ void crm_upd_item(const CRMView &v, int h, int lb) {
   const int n = v.n, nt = n >> 4, rt = v.R >> 4, per = nt * rt;
   const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, J = 2 * h * q;
   const size_t nn = (size_t)n * n, nr = (size_t)n * v.R;
@@ -1240,6 +1232,22 @@ __global__ __launch_bounds__(64) void k_crm_upd(CRMView v, int h, int total) {
   if (right) acc = mm_tile<true>(v.A + (J + h) * nn, n, v.Z + (J + h) * nr, v.R, ti, tj, 0, n);
   if (left) acc += mm_tile<true>(v.C + (J - h) * nn, n, v.Z + (J - h) * nr, v.R, ti, tj, 0, n);
   if (right || left) mm_store(v.G + J * nr, v.R, ti, tj, acc, -1.0, true);
+}
+
+// Level h of the many-right-hand-side CR in two launches after the factor:
+// (1) the eliminations A_I / C_I and Z_I = Linv_I G_I (both read only Linv_I),
+// (2) the even superblocks' update of D / E / g and of G (both read A / C / Z).
+__global__ __launch_bounds__(64) void k_crm_elim(CRView v, CRMView m, int h, int nel, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  if (lb < nel) cr_elim_item(v, h, lb);
+  else crm_fwd_item(m, h, 2 * h, lb - nel);
+}
+__global__ __launch_bounds__(64) void k_crm_update(CRView v, CRMView m, int h, int nup, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  if (lb < nup) cr_update_item(v, h, lb);
+  else crm_upd_item(m, h, lb - nup);
 }
 
 // odd I = h + 2 h q: Z_I -= A_I X_{I-h} + C_I X_{I+h} (in place, tile by tile)
@@ -1359,12 +1367,19 @@ static void launch_cr_factor(const CRView &v, int h, int I0, int stride, int cou
   else hipLaunchKernelGGL((k_cr_aug<1, false>), dim3(count), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, I0, stride, 1);
 }
 
+// A level with too many odd superblocks for the fused kernel's workgroups on
+// one round of CUs: the factor alone, then the strips as a wide kernel.
+static bool cr_level_wide(int n_odd, int nt, bool linv) {
+  return !cr_legacy() &&
+         (int64_t)n_odd * aug::min_split(nt, linv, aug::extra_columns(nt, true, true)) > kCrAugWideWGs;
+}
+
 // Level h, steps 1 + 2: every odd superblock factored, A_I / C_I / z_I formed.
 static void launch_cr_level(const CRView &v, int h, int n_odd, int fuse_min, bool fuse_ok, bool linv, hipStream_t st) {
   const int nt = v.n / 16;
   if (!cr_legacy()) {
     const int sp = aug_split(n_odd, nt, linv, aug::extra_columns(nt, true, true));
-    if ((int64_t)n_odd * aug::min_split(nt, linv, aug::extra_columns(nt, true, true)) > kCrAugWideWGs) {
+    if (cr_level_wide(n_odd, nt, linv)) {
       // too many odd superblocks for the fused kernel's workgroups on one
       // round of CUs: the factor alone, then the strips as a wide kernel
       launch_cr_factor(v, h, h, 2 * h, n_odd, linv, st);
@@ -1405,10 +1420,9 @@ int launch_cr_multi(double *D, double *L, double *E, double *A, double *C, doubl
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
     launch_cr_factor(v, h, h, 2 * h, n_odd, true, st);
-    hipLaunchKernelGGL(k_crm_fwd, dim3(xcd_grid(n_odd * rhs)), dim3(64), 0, st, m, h, 2 * h, n_odd * rhs);
-    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
-    hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
-    hipLaunchKernelGGL(k_crm_upd, dim3(xcd_grid(n_even * rhs)), dim3(64), 0, st, m, h, n_even * rhs);
+    const int nel = n_odd * 2 * per, t1 = nel + n_odd * rhs, nup = n_even * upd, t2 = nup + n_even * rhs;
+    hipLaunchKernelGGL(k_crm_elim, dim3(xcd_grid(t1)), dim3(64), 0, st, v, m, h, nel, t1);
+    hipLaunchKernelGGL(k_crm_update, dim3(xcd_grid(t2)), dim3(64), 0, st, v, m, h, nup, t2);
   }
   launch_cr_factor(v, 0, 0, 0, 1, true, st);
   hipLaunchKernelGGL(k_crm_fwd, dim3(xcd_grid(rhs)), dim3(64), 0, st, m, 0, 1, rhs);
@@ -1462,9 +1476,7 @@ struct ArwView {
 };
 
 // Z_I = Linv_I G_I for the superblocks I of `list`
-__global__ __launch_bounds__(64) void k_arw_fwd(ArwView a, const int *list, int total) {
-  const int lb = xcd_block(total);
-  if (lb >= total) return;
+__device__ __forceinline__ void arw_fwd_item(const ArwView &a, const int *list, int lb) {
   const int nt = a.n >> 4, rt = a.R >> 4, per = nt * rt;
   const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt, I = list[q];
   const size_t nn = (size_t)a.n * a.n, nr = (size_t)a.n * a.R;
@@ -1472,12 +1484,24 @@ __global__ __launch_bounds__(64) void k_arw_fwd(ArwView a, const int *list, int 
   mm_store(a.Z + I * nr, a.R, ti, tj, acc, 1.0, false);
 }
 
+__global__ __launch_bounds__(64) void k_arw_fwd(ArwView a, const int *list, int total) {
+  const int lb = xcd_block(total);
+  if (lb < total) arw_fwd_item(a, list, lb);
+}
+
+// a wide level's eliminations A_I / C_I (cr_elim_item, items [0, nel)) and the
+// border right-hand sides' Z_I (the rest) in one launch: both read only Linv_I
+__global__ __launch_bounds__(64) void k_arw_elim(CRView v, ArwView a, int h, int nel, const int *list, int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  if (lb < nel) cr_elim_item(v, h, lb);
+  else arw_fwd_item(a, list, lb - nel);
+}
+
 // even J of level h: G_J = [G_J] - A_{J+h}^T Z_{J+h} - C_{J-h}^T Z_{J-h}, the
 // terms present per the entry's flags (a superblock without a right-hand side
 // yet starts from zero)
-__global__ __launch_bounds__(64) void k_arw_upd(ArwView a, int h, const int *list, int total) {
-  const int lb = xcd_block(total);
-  if (lb >= total) return;
+__device__ __forceinline__ void arw_upd_item(const ArwView &a, int h, const int *list, int lb) {
   const int n = a.n, nt = n >> 4, rt = a.R >> 4, per = nt * rt;
   const int q = lb / per, t = lb - q * per, ti = t / rt, tj = t - ti * rt;
   const int e = list[q], J = e & kUpdMask;
@@ -1486,6 +1510,17 @@ __global__ __launch_bounds__(64) void k_arw_upd(ArwView a, int h, const int *lis
   if (e & kUpdRight) acc = mm_tile<true>(a.A + (J + h) * nn, n, a.Z + (J + h) * nr, a.R, ti, tj, 0, n);
   if (e & kUpdLeft) acc += mm_tile<true>(a.C + (J - h) * nn, n, a.Z + (J - h) * nr, a.R, ti, tj, 0, n);
   mm_store(a.G + J * nr, a.R, ti, tj, acc, -1.0, (e & kUpdHad) != 0);
+}
+
+// Level h, step 3 of the band (cr_update_item, items [0, ncr)) and the border
+// right-hand sides' update (arw_upd_item, the rest) in one launch: both read
+// only the level's eliminations A / C / Z.
+__global__ __launch_bounds__(64) void k_arw_update_gemm(CRView v, ArwView a, int h, int ncr, const int *list,
+                                                        int total) {
+  const int lb = xcd_block(total);
+  if (lb >= total) return;
+  if (lb < ncr) cr_update_item(v, h, lb);
+  else arw_upd_item(a, h, list, lb - ncr);
 }
 
 // Border Schur complement, lower 16x16 tiles: Ab -= sum_{I in elim} Z_I^T Z_I
@@ -1540,13 +1575,21 @@ __global__ __launch_bounds__(256) void k_arw_correct(ArwView a, const int *elim,
   if (lane == 0) a.g[(size_t)I * a.n + k] -= s;
 }
 
-// x_0 = Linv_0^T z_0 (the top superblock, factored by k_cr_factor_at)
-__global__ __launch_bounds__(128) void k_arw_top_back(ArwView a, double *x) {
-  const int c = threadIdx.x;
-  if (c >= a.n) return;
-  double s = 0.0;
-  for (int r = c; r < a.n; ++r) s += a.D[(size_t)r * a.n + c] * a.g[r];
-  x[c] = s;
+// x_0 = Linv_0^T z_0 (the top superblock, factored with LINV): thread (c, h)
+// sums its quarter of rows m >= c of column c, the quarters added in order
+__global__ __launch_bounds__(512) void k_arw_top_back(ArwView a, double *x) {
+  __shared__ double part[4][kCRMaxN];
+  const int n = a.n, t = threadIdx.x, c = t % kCRMaxN, h = t / kCRMaxN, q = (n + 3) / 4;
+  if (h < 4 && c < n) {
+    double s = 0.0;
+    for (int i = 0; i < q; ++i) {
+      const int m = h * q + i;
+      if (m >= c && m < n) s += a.D[(size_t)m * n + c] * a.g[m];
+    }
+    part[h][c] = s;
+  }
+  __syncthreads();
+  if (t < n) x[t] = ((part[0][t] + part[1][t]) + part[2][t]) + part[3][t];
 }
 
 // Border system init per trial: clear F^T in the superblocks that carry it,
@@ -1588,10 +1631,16 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
     const int fo = pl.lvl[4 * lv], fc = pl.lvl[4 * lv + 1], uo = pl.lvl[4 * lv + 2], uc = pl.lvl[4 * lv + 3];
-    launch_cr_level(v, h, n_odd, fuse_min, fuse_ok, true, st);
-    if (fc) hipLaunchKernelGGL(k_arw_fwd, dim3(xcd_grid(fc * rhs)), dim3(64), 0, st, a, S + fo, fc * rhs);
-    hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
-    if (uc) hipLaunchKernelGGL(k_arw_upd, dim3(xcd_grid(uc * rhs)), dim3(64), 0, st, a, h, S + uo, uc * rhs);
+    if (cr_level_wide(n_odd, nt, true)) {  // factor, then the eliminations with Z_I in one launch
+      launch_cr_factor(v, h, h, 2 * h, n_odd, true, st);
+      const int nel = n_odd * 2 * per, tot = nel + fc * rhs;
+      hipLaunchKernelGGL(k_arw_elim, dim3(xcd_grid(tot)), dim3(64), 0, st, v, a, h, nel, S + fo, tot);
+    } else {
+      launch_cr_level(v, h, n_odd, fuse_min, fuse_ok, true, st);
+      if (fc) hipLaunchKernelGGL(k_arw_fwd, dim3(xcd_grid(fc * rhs)), dim3(64), 0, st, a, S + fo, fc * rhs);
+    }
+    const int ncr = n_even * upd, tot = ncr + uc * rhs;
+    hipLaunchKernelGGL(k_arw_update_gemm, dim3(xcd_grid(tot)), dim3(64), 0, st, v, a, h, ncr, S + uo, tot);
   }
   // top superblock: factor (Linv_0 into L_0, z_0 into g_0) and its Z_0
   launch_cr_factor(v, 0, 0, 0, 1, true, st);
@@ -1609,7 +1658,7 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
   // x_b = P L^-T (w - W x_c)
   if (pl.elim_cnt)
     hipLaunchKernelGGL(k_arw_correct, dim3((pl.elim_cnt * n + 3) / 4), dim3(256), 0, st, a, elim, pl.elim_cnt, d.bd_x);
-  hipLaunchKernelGGL(k_arw_top_back, dim3(1), dim3(128), 0, st, a, d.cr_x);
+  hipLaunchKernelGGL(k_arw_top_back, dim3(1), dim3(512), 0, st, a, d.cr_x);
   for (h /= 2; h >= 1; h /= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     hipLaunchKernelGGL(k_cr_back, dim3(n_odd), dim3(64 * nt), (size_t)n * sizeof(double), st, v, h);

@@ -32,6 +32,7 @@ EXPORTS = [
     "sqlm_bench_iterations",
     "sqlm_kernel_timer_name", "sqlm_set_stereo",
     "sqlm_eg_set_problem", "sqlm_eg_optimize", "sqlm_eg_get_poses", "sqlm_eg_get_edge_chi2",
+    "sqlm_eg_get_jacobians",
     "sqlm_get_rcs_layout",
 ]
 # every symbol include/sqrtlm_capture.h declares

@@ -216,6 +216,13 @@ class Context:
         check(lib().sqlm_eg_get_edge_chi2(self._h, ptr(out)), "sqlm_eg_get_edge_chi2")
         return out
 
+    def eg_jacobians(self):
+        """(n_edge, 2, 7, 7): d e / d S_i and d e / d S_j at the current estimates
+        (sqlm_eg_get_jacobians, the optimizer's numeric Jacobians)."""
+        out = np.zeros((self.pose_graph.n_edge, 2, 7, 7))
+        check(lib().sqlm_eg_get_jacobians(self._h, ptr(out)), "sqlm_eg_get_jacobians")
+        return out
+
 
 def comm_unique_id() -> bytes:
     n = lib().sqlm_comm_id_size()

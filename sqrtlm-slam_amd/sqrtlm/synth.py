@@ -145,7 +145,8 @@ def pose_through_f32(R: np.ndarray, t: np.ndarray):
 def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_window: int = 0,
                  n_fixed: int = 1, seed: int = 0, outlier_frac: float = 0.02, robust: bool = True,
                  huber_delta: float | None = None, noise: bool = True, perturb: bool = True,
-                 loop: int = 0, loop_cams: int = 24, perturb_center: bool = False) -> BAProblem:
+                 loop: int = 0, loop_cams: int = 24, perturb_center: bool = False,
+                 revisits: tuple = (), drift: tuple | None = None) -> BAProblem:
     """Generate a synthetic BA problem.
 
     pair_window > 0 selects the local-BA layout of config 2: every landmark has
@@ -161,6 +162,19 @@ def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_
     points (src/backend/LoopClosing.cc:863-877): the reduced camera system then
     couples keyframes 0.. with n_kf - loop.. far off its band.
 
+    revisits = ((start_kf, length, place0), ...) generalises ``loop`` to several
+    loop closures: keyframes start_kf .. start_kf+length-1 re-drive the places
+    place0 .. of keyframes driven earlier (0.5 m to alternating sides), the
+    other keyframes drive new places around the circle; twins as for ``loop``.
+    A revisit must go to places already driven before it starts.
+
+    drift = (deg, m) replaces the independent initial errors by the error of a
+    visual-odometry map: a world-frame rigid motion G_i per keyframe, a random
+    walk of N(0, deg^2) rotation and N(0, m^2) translation steps from KF 0 (exact),
+    applied to the keyframe (T_wc' = G_i T_wc) and to each point with its first
+    observer, plus small independent noise (deg / 2, m, points 0.02 m):
+    neighbouring keyframes stay consistent, the far end of a loop has drifted.
+
     perturb_center: the initial pose error is a rotation about the camera
     centre plus a displacement of the centre (a drifted keyframe), instead of a
     perturbation of T_cw = [R | t] itself, whose rotation part swings the
@@ -169,7 +183,31 @@ def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_
     fx, fy, cx, cy = KITTI_INTR
     W, H = KITTI_WH
     idx = np.arange(n_kf)
-    if loop > 0:
+    rv_place = None
+    if revisits:
+        place = np.full(n_kf, -1, np.int64)
+        side = np.zeros(n_kf)
+        for r, (s0, ln, p0) in enumerate(revisits):
+            place[s0:s0 + ln] = p0 + np.arange(ln)
+            side[s0:s0 + ln] = 0.5 if r % 2 == 0 else -0.5
+        first = place < 0
+        place[first] = np.arange(int(first.sum()))
+        Lc = int(first.sum())
+        for s0, ln, p0 in revisits:
+            if p0 + ln > int(first[:s0].sum()):
+                raise ValueError("a revisit must go to places driven before it")
+        th = 2.0 * np.pi * place / Lc
+        rad = Lc / (2.0 * np.pi)
+        yaw = th + 0.02 * np.sin(idx / 10.0)
+        c = np.stack([rad * (1.0 - np.cos(th)) + side * np.cos(th), np.zeros(n_kf),
+                      rad * np.sin(th) - side * np.sin(th)], axis=1)
+        fp_of_place = np.empty(Lc, np.int64)
+        fp_of_place[place[first]] = idx[first]
+        rv_place = -np.ones(Lc, np.int64)  # the (first) revisiting keyframe of each place
+        for k in idx[~first][::-1]:
+            rv_place[place[k]] = k
+        twin_of = np.where(first, rv_place[place], fp_of_place[place])
+    elif loop > 0:
         Lc = n_kf - loop
         place = np.where(idx < Lc, idx, idx - Lc)
         th = 2.0 * np.pi * place / Lc
@@ -217,11 +255,14 @@ def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_
         starts = np.repeat(a, k)
         first = np.repeat(np.cumsum(k) - k, k)
         kf = starts + (np.arange(lm.size) - first)
-    if loop > 0:
+    if loop > 0 or rv_place is not None:
         # twins: the other pass's keyframe at the place of each track keyframe,
         # in track order, while the landmark has fewer than loop_cams observers
-        Lc = n_kf - loop
-        tw = np.where(kf < loop, kf + Lc, np.where(kf >= Lc, kf - Lc, -1))
+        if rv_place is not None:
+            tw = twin_of[kf]
+        else:
+            Lc = n_kf - loop
+            tw = np.where(kf < loop, kf + Lc, np.where(kf >= Lc, kf - Lc, -1))
         cand = tw >= 0
         cnt = np.bincount(lm[cand], minlength=n_lm)
         rank_in_lm = np.cumsum(cand) - 1 - (np.cumsum(cnt) - cnt)[lm]  # lm is grouped, ascending
@@ -278,7 +319,26 @@ def make_problem(n_kf: int, n_lm: int, *, k_min: int = 2, k_max: int = 18, pair_
     gt_X = X.astype(np.float32).astype(np.float64)
     R0, t0 = R_cw.copy(), t_cw.copy()
     X0 = X.copy()
-    if perturb:
+    if perturb and drift is not None:
+        free = np.nonzero(fixed == 0)[0]
+        sr, st_ = np.deg2rad(drift[0]), drift[1]
+        w = np.cumsum(rng.normal(3 * n_kf).reshape(-1, 3) * sr, axis=0)
+        tau = np.cumsum(rng.normal(3 * n_kf).reshape(-1, 3) * st_, axis=0)
+        w -= w[0]
+        tau -= tau[0]
+        Gr = _so3_exp(w)
+        Gr[fixed != 0] = np.eye(3)
+        tau[fixed != 0] = 0.0
+        c0 = np.einsum("nij,nj->ni", Gr, c) + tau
+        R0 = np.transpose(np.einsum("nij,njk->nik", Gr, R_wc), (0, 2, 1))
+        dth = rng.normal(3 * free.size).reshape(-1, 3) * (0.5 * sr)
+        R0[free] = _so3_exp(dth) @ R0[free]
+        c0[free] += rng.normal(3 * free.size).reshape(-1, 3) * st_
+        t0 = -np.einsum("nij,nj->ni", R0, c0)
+        fo = np.full(X.shape[0], n_kf, np.int64)  # first observer of each point
+        np.minimum.at(fo, lm, kf)
+        X0 = np.einsum("nij,nj->ni", Gr[fo], X) + tau[fo] + rng.normal(3 * X.shape[0]).reshape(-1, 3) * 0.02
+    elif perturb:
         free = np.nonzero(fixed == 0)[0]
         dth = rng.normal(3 * free.size).reshape(-1, 3) * np.deg2rad(0.3)
         dt = rng.normal(3 * free.size).reshape(-1, 3) * 0.05
@@ -336,6 +396,24 @@ def config4_loop(seed: int = 4, scale: float = 1.0, loop: int = 30, **kw) -> BAP
     kw.setdefault("robust", False)
     kw.setdefault("perturb_center", True)
     return make_problem(n_kf, n_lm, k_min=2, k_max=18, n_fixed=1, seed=seed, loop=min(loop, n_kf // 4), **kw)
+
+
+KITTI00_REVISITS = ((700, 40, 200), (1400, 100, 0))
+
+
+def kitti00_map(seed: int = 4, n_kf: int = 1500, n_lm: int = 100000, revisits=KITTI00_REVISITS,
+                stereo_frac: float = 0.5) -> BAProblem:
+    """Stand-in for the KITTI-00 map that configs 3 / 5 run on (the sequence
+    itself is not available): 1.5k keyframes, 1e5 landmarks over k ~ U{2..18}
+    consecutive keyframes (~1e6 observations), two loop closures — a 40-KF
+    re-entry into a stretch driven 500 KFs earlier and the final 100-KF revisit
+    of the start — with the matched points fused into both passes, odometry
+    drift (0.005 deg and 0.005 m per keyframe, random walk), and half of the
+    observations stereo (KITTI is a stereo rig; cfg/KITTI00-02.yaml Camera.bf)."""
+    prob = make_problem(n_kf, n_lm, k_min=2, k_max=18, n_fixed=1, seed=seed, robust=True, revisits=revisits,
+                        drift=(0.005, 0.005))
+    prob.meta["revisits"] = tuple(revisits)
+    return add_stereo(prob, stereo_frac, seed=seed)
 
 
 def add_lidar_flat(prob: BAProblem, pose: int, n: int, *, seed: int = 0, noise: float = 0.01,

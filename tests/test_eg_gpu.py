@@ -188,3 +188,69 @@ def test_eg_bench_size_first_iteration(gpu_ctx, oracle, monkeypatch):
     dense = gpu_ctx.eg_poses().copy()
     assert _rel(arrow, ref.Siw) < 1e-6 and _rel(dense, ref.Siw) < 1e-6
     assert _rel(arrow, dense) < 1e-9
+
+
+def _oracle_jacobians(oracle, pg):
+    out = np.zeros((pg.n_edge, 2, 7, 7))
+    for e in range(pg.n_edge):
+        i, j = pg.ei[e], pg.ej[e]
+        Ji, Jj = oracle.eg_edge_jacobians(pg.Siw[i], pg.Siw[j], pg.Sji[e], pg.fix_scale,
+                                          int(pg.fixed[i] == 0), int(pg.fixed[j] == 0))
+        out[e, 0], out[e, 1] = Ji, Jj
+    return out
+
+
+@pytest.mark.parametrize("fix_scale", [True, False])
+def test_eg_numeric_jacobians_bitwise(gpu_ctx, oracle, fix_scale):
+    """The GPU's 7x7 numeric Jacobians (the arithmetic of k_eg_linearize:
+    central differences over delta = 1e-9 through oplus, base_binary_edge.hpp:
+    131-205) equal the oracle's BIT FOR BIT on the 1500-keyframe bench graph:
+    both sides evaluate Sim3 exp / log with include/sqlm_libm.h's sin / cos /
+    exp / log / acos and IEEE + - * / sqrt without contraction."""
+    pg = synth.make_pose_graph(1500, window=8, n_loops=20, seed=5, fix_scale=fix_scale)
+    gpu_ctx.eg_set_problem(pg)
+    Jg = gpu_ctx.eg_jacobians()
+    Jo = _oracle_jacobians(oracle, pg)
+    assert np.abs(Jo).max() > 0.1
+    np.testing.assert_array_equal(Jg, Jo)
+
+
+def test_eg_bench_size_full_schedule(gpu_ctx, oracle):
+    """The bench graph through the whole optimize(20) (lambda 1e-16, the
+    reference's schedule, LoopClosing.cc:863 -> g2oOptimizer.cc:1212-1534).
+
+    1e-6 after 20 iterations is NOT a property the reference itself has on
+    this graph, so it is not what is asserted: the oracle run twice, with ONE
+    measurement moved by one ulp, ends up to 3e-3 apart (translations of far
+    keyframes moving metres) after 2-20 iterations (measured
+    below). The normal equations of this graph have a condition number of
+    5.5e13 (Lanczos on the oracle's H: eigenvalues 4e-8 .. 2.2e6; rotations
+    couple to world-frame translations of up to 1.5 km), so a Gauss-Newton
+    step (lambda 1e-16) resolves its near-null directions only to ~kappa * eps
+    = 5e-3, whichever the summation order: the second iteration's chi2 already
+    moves by percents between two correct implementations. With the Jacobians bitwise
+    equal (test above), what still differs is the order of the sums in H and
+    in the factorization; the GPU must stay within 10x of the reference's own
+    one-ulp spread (and under a 1e-2 cap), reach the same chi2 within 10x of
+    the reference's own spread, and take the same first step to 1e-6."""
+    pg = synth.make_pose_graph(1500, window=8, n_loops=20, seed=5, fix_scale=True)
+    ref = oracle.OracleEG(pg)
+    nr, sr = ref.optimize(20, 1e-16)
+    gpu_ctx.eg_set_problem(pg)
+    ng, sg = gpu_ctx.eg_optimize(20, 1e-16)
+    assert sg["trace_trials"][0] == sr["trace_trials"][0] and min(ng, nr) >= 10
+    np.testing.assert_allclose(sg["trace_chi2"][0], sr["trace_chi2"][0], rtol=1e-6)
+    spread, chi_spread = 0.0, 0.0
+    for r, c in ((0, 4), (5, 0)):
+        p2 = pg.copy()
+        p2.Sji[r, c] = np.nextafter(p2.Sji[r, c], 1e9)
+        g = oracle.OracleEG(p2)
+        _, s2 = g.optimize(20, 1e-16)
+        spread = max(spread, _rel(g.Siw, ref.Siw))
+        chi_spread = max(chi_spread, abs(s2["chi2_end"] - sr["chi2_end"]) / sr["chi2_end"])
+    assert spread > 1e-5  # the reference's own rounding sensitivity on this graph
+    d = _rel(gpu_ctx.eg_poses(), ref.Siw)
+    print(f"eg 20 iterations: gpu {ng} it, oracle {nr} it | gpu-oracle {d:.2e}, oracle 1-ulp spread {spread:.2e} | "
+          f"chi2 gpu {sg['chi2_end']:.9g} oracle {sr['chi2_end']:.9g} (1-ulp spread {chi_spread:.2e})")
+    assert d < min(1e-2, 10.0 * spread)
+    assert abs(sg["chi2_end"] - sr["chi2_end"]) / sr["chi2_end"] < max(1e-6, 10.0 * chi_spread)

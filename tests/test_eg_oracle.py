@@ -94,3 +94,27 @@ def test_eg_noise_free_converges(oracle, fix_scale):
     # poses relative to the fixed KF 0 recover the ground truth
     for p in range(pg.n_kf):
         np.testing.assert_allclose(g.Siw[p, 4:], gt[p, 4:], rtol=1e-6, atol=1e-6)
+
+
+def test_shared_libm_within_one_ulp_of_glibc(oracle):
+    """include/sqlm_libm.h (the sin / cos / exp / log / acos both the oracle's
+    and the GPU's Sim3 code use, so their numeric Jacobians agree bit for bit)
+    stays within 1 ulp of the platform libm on the arguments Sim3 exp / log
+    meet and well beyond them."""
+    rng = np.random.default_rng(3)
+    cases = {
+        "exp": np.concatenate([rng.uniform(-5, 5, 20000), rng.uniform(-1e-6, 1e-6, 500), rng.uniform(-700, 700, 2000),
+                               [0.0, -0.0, 1e-300, 0.5 * np.log(2), 1.5 * np.log(2)]]),
+        "log": np.concatenate([rng.uniform(0.5, 2, 20000), np.exp(rng.uniform(-700, 700, 2000)),
+                               [1.0, 2.0, 1e-310, 1 - 1e-16, 1 + 2e-16]]),
+        "sin": np.concatenate([rng.uniform(-4, 4, 20000), rng.uniform(-1e-9, 1e-9, 500), rng.uniform(-1e4, 1e4, 2000),
+                               [0.0, np.pi, np.pi / 4, 3 * np.pi / 4]]),
+        "cos": np.concatenate([rng.uniform(-4, 4, 20000), rng.uniform(-1e-9, 1e-9, 500), rng.uniform(-1e4, 1e4, 2000),
+                               [0.0, np.pi, np.pi / 4, 3 * np.pi / 4]]),
+        "acos": np.concatenate([rng.uniform(-1, 1, 20000), [1.0, -1.0, 0.0, 0.5, -0.5, 1 - 1e-16, 1e-17]]),
+    }
+    ref = {"exp": np.exp, "log": np.log, "sin": np.sin, "cos": np.cos, "acos": np.arccos}
+    for fn, x in cases.items():
+        y, r = oracle.libm(fn, x), ref[fn](x)
+        ulp = np.abs(y.view(np.int64) - r.view(np.int64))
+        assert ulp.max() <= 1, (fn, x[ulp.argmax()], y[ulp.argmax()], r[ulp.argmax()])

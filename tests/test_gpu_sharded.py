@@ -34,13 +34,15 @@ def _gpu_rank(rank, world, gen, scale, iters):
 
 
 @pytest.mark.parametrize("world,gen,scale", [(2, "band", 0.01), (3, "band", 0.05), (2, "loop", 0.02),
-                                             (3, "loop", 0.05)])
+                                             (3, "loop", 0.05), (2, "band", 1.0), (2, "loop", 1.0)])
 def test_sharded_global_ba_matches_oracle(oracle, world, gen, scale):
     """Loop-closed maps ("loop"): the ranks holding the revisited keyframes'
     landmarks see S blocks far off the band; the shared S pattern is the union
-    of the shards' patterns, so every rank plans the same band + border solve."""
+    of the shards' patterns, so every rank plans the same band + border solve.
+    scale 1.0: BASELINE config 4 itself (5k poses, 500k landmarks) on two
+    ranks; the oracle runs with its OpenMP loops (bit-identical results)."""
     prob = _problem(gen, scale)
-    ref = oracle.OracleGraph(prob)
+    ref = oracle.OracleGraph(prob, omp=scale >= 0.5)
     nr, sr = ref.global_ba(10)
     res = run_ranks(_gpu_rank, world, gen, scale, 10)
     ranges = landmark_ranges(prob, world)
