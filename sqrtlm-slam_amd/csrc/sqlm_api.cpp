@@ -8,10 +8,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
+#include <mutex>
 #include <new>
 #include <queue>
 #include <thread>
@@ -45,6 +48,41 @@ const char *kTimerNames[SQLM_NKERNEL_TIMERS] = {"k_linearize", "k_camera_pass", 
 
 }  // namespace
 
+// Landmark tiles for the RCS assembly: runs of consecutive slots whose free
+// cameras fit a window of <= kTileMaxCams cameras (sorted), plus the reduction
+// lists that sum each S block / g row from its tiles in tile order.
+struct TilePlan {
+  std::vector<int> lm_ptr{0}, cam_ptr{0}, cams, obs_local, ld, red_ptr, gred_ptr;
+  std::vector<int2> urange, gred_idx;
+  std::vector<int64_t> red_off;   // absolute offset (doubles) of each contribution's 6x6 block in part
+  std::vector<int64_t> gred_off;  // ... and of each g contribution's 6 doubles in gpart
+  std::vector<int> long_s, long_g;  // S blocks / cameras with more than kRedLong contributions
+  std::vector<int64_t> part_ptr{0}, gpart_ptr{0};
+  int max_cp = 0;
+  bool dups = false;
+  std::vector<int> order;  // tile ids grouped by nt class (ascending id within a class)
+  int cls_off[kTileNtMax + 2] = {}, cls_cnt[kTileNtMax + 1] = {};
+  // back to the empty plan, keeping every vector's memory (a context reuses
+  // its plan across calls: no reallocation, no first-touch page faults)
+  void reset() {
+    lm_ptr.assign(1, 0);
+    cam_ptr.assign(1, 0);
+    part_ptr.assign(1, 0);
+    gpart_ptr.assign(1, 0);
+    for (auto *v : {&cams, &obs_local, &ld, &red_ptr, &gred_ptr, &long_s, &long_g, &order}) v->clear();
+    urange.clear();
+    gred_idx.clear();
+    red_off.clear();
+    gred_off.clear();
+    max_cp = 0;
+    dups = false;
+    std::fill(cls_off, cls_off + kTileNtMax + 2, 0);
+    std::fill(cls_cnt, cls_cnt + kTileNtMax + 1, 0);
+  }
+};
+
+
+
 struct sqlm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -77,6 +115,12 @@ struct sqlm_ctx {
   std::vector<int> cam_pos;          // hidx -> band position or -(1 + border index)
   bool use_tiles = false;
   int tile_max_cp = 0, tile_max_k = 0;
+  // host plan scratch kept across calls (capacity reused: prepare() allocates
+  // and first-touches none of its large arrays after the first call)
+  TilePlan tp;
+  std::vector<std::vector<int>> scat_base;  // per-thread counting-sort bases (slots)
+  std::vector<int> h_kcount, h_span_lo, h_span_hi, h_pt_slot, h_key;
+  std::vector<uint8_t> h_pose_act, h_pt_act;
   // ---- device memory ----
   std::vector<DevBuf> bufs;
   std::vector<DevBuf> pins;  // page-locked host staging of the large uploads (async DMA)
@@ -200,25 +244,81 @@ enum BufId {
   B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL
 };
 
-// Landmark tiles for the RCS assembly: runs of consecutive slots whose free
-// cameras fit a window of <= kTileMaxCams cameras (sorted), plus the reduction
-// lists that sum each S block / g row from its tiles in tile order.
-struct TilePlan {
-  std::vector<int> lm_ptr{0}, cam_ptr{0}, cams, obs_local, ld, red_ptr, gred_ptr;
-  std::vector<int2> urange, gred_idx;
-  std::vector<int64_t> red_off;   // absolute offset (doubles) of each contribution's 6x6 block in part
-  std::vector<int64_t> gred_off;  // ... and of each g contribution's 6 doubles in gpart
-  std::vector<int> long_s, long_g;  // S blocks / cameras with more than kRedLong contributions
-  std::vector<int64_t> part_ptr{0}, gpart_ptr{0};
-  int max_cp = 0;
-  bool dups = false;
-  std::vector<int> order;  // tile ids grouped by nt class (ascending id within a class)
-  int cls_off[kTileNtMax + 2] = {}, cls_cnt[kTileNtMax + 1] = {};
+// Persistent host worker pool for the setup passes (a prepare() runs ~20
+// parallel passes; starting and joining 15 threads each time cost ~0.4 ms per
+// pass). One caller at a time: a context that finds it busy (another context
+// preparing on another thread) falls back to threads of its own.
+class HostPool {
+ public:
+  static HostPool &get() {
+    static HostPool p;
+    return p;
+  }
+  // fn(t) for t = 1 .. nth-1 on the workers while the caller runs fn(0)
+  bool try_run(int nth, const std::function<void(int)> &fn) {
+    std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      while ((int)th_.size() < nth - 1) {
+        const int id = (int)th_.size() + 1;
+        th_.emplace_back([this, id] { worker(id); });
+      }
+      job_ = &fn;
+      active_ = nth;
+      pending_ = nth - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return pending_ == 0; });
+    job_ = nullptr;
+    return true;
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto &t : th_) t.join();
+  }
+
+ private:
+  void worker(int id) {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      if (id >= active_) continue;
+      const std::function<void(int)> *f = job_;
+      lk.unlock();
+      (*f)(id);
+      lk.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::mutex use_, m_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  const std::function<void(int)> *job_ = nullptr;
+  uint64_t gen_ = 0;
+  int active_ = 0, pending_ = 0;
+  bool stop_ = false;
 };
 
 // fn(t) for t = 0 .. nth-1 on nth host threads (t = 0 on the caller's)
 template <class F>
 void run_threads(int nth, F &&fn) {
+  if (nth <= 1) {
+    fn(0);
+    return;
+  }
+  const std::function<void(int)> f = [&fn](int t) { fn(t); };
+  if (HostPool::get().try_run(nth, f)) return;
   std::vector<std::thread> th;
   for (int t = 1; t < nth; ++t) th.emplace_back(fn, t);
   fn(0);
@@ -257,6 +357,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
     std::fprintf(stderr, "  tiles %-14s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - pt0).count());
     pt0 = now;
   };
+  tp.reset();
   tp.obs_local.assign(nE, -1);
   tp.urange.assign(nL, int2{-1, -1});
   // pass 1 (greedy): tile boundaries -- a tile closes before the landmark that
@@ -321,27 +422,33 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
     std::vector<int> lidx(nP, -1), lcams;
     std::vector<uint8_t> pst;
     for (int t = th; t < nt; t += nth) {
+      // the window's cameras: first sight marks (lidx = -2), then sorted (<= 24 of them)
       std::vector<int> &cur = out[t].cams;
-      for (int o = lm_begin[tstart[t]]; o < lm_begin[tstart[t + 1]]; ++o)
-        if (obs_camh[o] >= 0) cur.push_back(obs_camh[o]);
+      for (int o = lm_begin[tstart[t]]; o < lm_begin[tstart[t + 1]]; ++o) {
+        const int h = obs_camh[o];
+        if (h >= 0 && lidx[h] == -1) { lidx[h] = -2; cur.push_back(h); }
+      }
       std::sort(cur.begin(), cur.end());
-      cur.erase(std::unique(cur.begin(), cur.end()), cur.end());
       const int cp = (int)cur.size();
       for (int u = 0; u < cp; ++u) lidx[cur[u]] = u;
       pst.assign((size_t)cp * cp, 0);
       for (int sl = tstart[t]; sl < tstart[t + 1]; ++sl) {
         lcams.clear();
+        int lo = cp, hi = -1;
         for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
           const int h = obs_camh[o];
-          tp.obs_local[o] = h >= 0 ? lidx[h] : -1;
-          if (h >= 0) lcams.push_back(lidx[h]);
+          const int u = h >= 0 ? lidx[h] : -1;
+          tp.obs_local[o] = u;
+          if (u >= 0) { lcams.push_back(u); lo = std::min(lo, u); hi = std::max(hi, u); }
         }
-        if (lcams.empty()) continue;
-        std::sort(lcams.begin(), lcams.end());
-        lcams.erase(std::unique(lcams.begin(), lcams.end()), lcams.end());
-        tp.urange[sl] = int2{lcams.front(), lcams.back()};
-        for (size_t a = 0; a < lcams.size(); ++a)
-          for (size_t b = a; b < lcams.size(); ++b) pst[(size_t)lcams[a] * cp + lcams[b]] = 1;
+        if (hi < 0) continue;
+        tp.urange[sl] = int2{lo, hi};
+        const size_t m = lcams.size();  // (a repeated camera only marks its pairs twice)
+        for (size_t a = 0; a < m; ++a)
+          for (size_t b = a; b < m; ++b) {
+            const int u = std::min(lcams[a], lcams[b]), v = std::max(lcams[a], lcams[b]);
+            pst[(size_t)u * cp + v] = 1;
+          }
       }
       for (int u = 0; u < cp; ++u)
         for (int v = u; v < cp; ++v) {
@@ -551,9 +658,13 @@ int prepare(sqlm_ctx *c, int level) {
     std::fprintf(stderr, "prepare %-12s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - pt0).count());
     pt0 = now;
   };
-  std::vector<uint8_t> pose_act(c->n_pose, 0), pt_act(c->n_pt, 0);
-  std::vector<int> kcount(c->n_pt, 0);
-  std::vector<int> span_lo(c->n_pt, std::numeric_limits<int>::max()), span_hi(c->n_pt, -1);
+  std::vector<uint8_t> &pose_act = c->h_pose_act, &pt_act = c->h_pt_act;
+  std::vector<int> &kcount = c->h_kcount, &span_lo = c->h_span_lo, &span_hi = c->h_span_hi;
+  pose_act.assign(c->n_pose, 0);
+  pt_act.assign(c->n_pt, 0);
+  kcount.assign(c->n_pt, 0);
+  span_lo.assign(c->n_pt, std::numeric_limits<int>::max());
+  span_hi.assign(c->n_pt, -1);
   int64_t n_ae = 0;
   {  // active set, track lengths and camera spans in one pass on host threads (relaxed atomics)
     const int nth = host_threads(c->n_obs);
@@ -561,16 +672,32 @@ int prepare(sqlm_ctx *c, int level) {
     run_threads(nth, [&](int t) {
       const int64_t e0 = c->n_obs * t / nth, e1 = c->n_obs * (t + 1) / nth;
       int64_t n = 0;
+      // runs of one landmark (the reference adds a point's edges together,
+      // g2oOptimizer.cc:213-281) are folded locally: one set of atomics per run
+      int rl = -1, rk = 0, rlo = 0, rhi = 0;
+      auto flush = [&] {
+        if (rl < 0) return;
+        __atomic_store_n(&pt_act[rl], (uint8_t)1, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&kcount[rl], rk, __ATOMIC_RELAXED);
+        __atomic_fetch_min(&span_lo[rl], rlo, __ATOMIC_RELAXED);
+        __atomic_fetch_max(&span_hi[rl], rhi, __ATOMIC_RELAXED);
+      };
       for (int64_t e = e0; e < e1; ++e) {
         if (c->obs_level[e] != level) continue;
         const int l = c->obs_pt[e], pp = c->obs_pose[e];
-        __atomic_store_n(&pose_act[pp], (uint8_t)1, __ATOMIC_RELAXED);
-        __atomic_store_n(&pt_act[l], (uint8_t)1, __ATOMIC_RELAXED);
-        __atomic_fetch_add(&kcount[l], 1, __ATOMIC_RELAXED);
-        __atomic_fetch_min(&span_lo[l], pp, __ATOMIC_RELAXED);
-        __atomic_fetch_max(&span_hi[l], pp, __ATOMIC_RELAXED);
+        if (!__atomic_load_n(&pose_act[pp], __ATOMIC_RELAXED)) __atomic_store_n(&pose_act[pp], (uint8_t)1, __ATOMIC_RELAXED);
+        if (l != rl) {
+          flush();
+          rl = l;
+          rk = 0;
+          rlo = rhi = pp;
+        }
+        ++rk;
+        rlo = std::min(rlo, pp);
+        rhi = std::max(rhi, pp);
         ++n;
       }
+      flush();
       cnt[t] = n;
     });
     for (int64_t v : cnt) n_ae += v;
@@ -603,7 +730,8 @@ int prepare(sqlm_ctx *c, int level) {
     auto wl = [](int k) { int w = seg_width(k), b = 0; while ((2 << b) < w) ++b; return b; };  // log2(W) - 1
     const int64_t nb = 7 * (int64_t)c->n_pose + 1;
     std::vector<int> bcnt(nb + 1, 0);
-    std::vector<int> key(c->n_pt, -1);
+    std::vector<int> &key = c->h_key;
+    key.assign(c->n_pt, -1);
     for (int l = 0; l < c->n_pt; ++l)
       if (pt_act[l]) { key[l] = (int)(wl(kcount[l]) * (int64_t)c->n_pose + span_lo[l]); ++bcnt[key[l] + 1]; }
     for (int64_t b = 0; b < nb; ++b) bcnt[b + 1] += bcnt[b];
@@ -633,7 +761,8 @@ int prepare(sqlm_ctx *c, int level) {
   const int nL = (int)pts.size();
   phase("active+sort");
   if (nP + nL == 0) return SQLM_ERR_STATE;  // "0 vertices to optimize"
-  std::vector<int> pt_slot(c->n_pt, -1);
+  std::vector<int> &pt_slot = c->h_pt_slot;
+  pt_slot.assign(c->n_pt, -1);
   for (int s = 0; s < nL; ++s) pt_slot[pts[s]] = s;
   c->slot_pt = pts;
   c->buckets.clear();
@@ -674,7 +803,8 @@ int prepare(sqlm_ctx *c, int level) {
   auto par = [&](auto &&fn) { run_threads(nth, fn); };
   {
     auto ebeg = [&](int t) { return c->n_obs * t / nth; };
-    std::vector<std::vector<int>> base(nth);
+    std::vector<std::vector<int>> &base = c->scat_base;
+    if ((int)base.size() < nth) base.resize(nth);
     par([&](int t) {
       std::vector<int> &cnt = base[t];
       cnt.assign(nL, 0);
@@ -789,10 +919,7 @@ int prepare(sqlm_ctx *c, int level) {
           rows[i] = row;
         }
       };
-      std::vector<std::thread> th;
-      for (int t = 1; t < nth; ++t) th.emplace_back(work, t);
-      work(0);
-      for (auto &t : th) t.join();
+      run_threads(nth, work);
     }
     if (sharded) {
       // every rank needs the same pattern: the union of the shards' patterns.
@@ -842,7 +969,7 @@ int prepare(sqlm_ctx *c, int level) {
     // band (+ border) superblock plan; the dense Cholesky otherwise
     if (!plan_rcs(nP, s_row, s_col, c->cr, c->cam_pos)) c->cr = CRPlan{};
   }
-  TilePlan tp;
+  TilePlan &tp = c->tp;
   // landmarks per tile: up to kTileMaxLm, fewer on small problems so that the
   // tiles still cover every CU twice (a local-BA window of 5k landmarks would
   // otherwise run ~40 long tiles on 256 CUs)

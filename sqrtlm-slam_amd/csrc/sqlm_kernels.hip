@@ -933,6 +933,7 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_t
   __shared__ double Lx[kTileMaxLm][3];            // landmarks at the linearization point
   __shared__ double Lc[kTileHardCams][16];        // window cameras: R t fx fy cx cy
   __shared__ double Lbf[ST ? kTileHardCams : 1];  // window cameras: bf (stereo edges)
+  __shared__ int2 Bs[(kTileMaxLm + kTileBL - 1) / kTileBL];  // column span of every batch (cmin, cmax)
   const int t = d.tile_order[cls_off + blockIdx.x], tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
   const int ncol = 6 * cp, nt = (ncol + 15) >> 4;
@@ -964,6 +965,14 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_t
     }
     if (ST)
       for (int u = tid; u < cp; u += TH) Lbf[u] = d.pose_bf[d.hidx_pose[d.tile_cams[cb + u]]];
+  }
+  for (int bt = tid; bt < nbatch; bt += TH) {  // batch spans from the landmarks' camera ranges
+    int cmin = 1 << 30, cmax = -1;
+    for (int li = BL * bt; li < min(BL * bt + BL, ntl); ++li) {
+      const int2 ur = d.lm_urange[l0 + li];
+      if (ur.x >= 0) { cmin = min(cmin, 6 * ur.x); cmax = max(cmax, 6 * ur.y + 6); }
+    }
+    Bs[bt] = int2{cmin, cmax};
   }
   __syncthreads();
   // prefetched raw inputs of one batch (fast path): thread tid owns observation b0 + tid
@@ -1044,11 +1053,8 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_t
     TP(1);
     if (bt + 1 < nbatch) fetch(bt + 1);  // in flight during the MFMAs below
     TP(2);
-    int cmin = 1 << 30, cmax = -1;
-    for (int li = 0; li < nl; ++li) {
-      const int2 ur = Lu[lb + li];
-      if (ur.x >= 0) { cmin = min(cmin, 6 * ur.x); cmax = max(cmax, 6 * ur.y + 6); }
-    }
+    const int2 bsp = Bs[bt];
+    const int cmin = bsp.x, cmax = bsp.y;
     TP(3);
     if (cmax > 0) {
       const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
