@@ -115,6 +115,10 @@ struct sqlm_ctx {
   std::vector<int> cam_pos;          // hidx -> band position or -(1 + border index)
   bool use_tiles = false;
   int tile_max_cp = 0, tile_max_k = 0;
+  // the last optimize()'s per-edge errors are still on the device only
+  // (fetched when an edge chi2 is asked for, or before the next prepare())
+  bool err_pending = false;
+  bool err_zero = false;  // obs_err is still to be sized and zeroed (a new problem: no error computed yet)
   // host plan scratch kept across calls (capacity reused: prepare() allocates
   // and first-touches none of its large arrays after the first call)
   TilePlan tp;
@@ -643,8 +647,13 @@ inline bool stopped(const volatile uint8_t *s) { return s && *s; }
 // initializeOptimization(level) + BlockSolver::buildStructure: active set,
 // index mapping (free poses by id, then points), landmark-sorted buckets,
 // camera CSR and the upper block pattern of the reduced camera system.
+int fetch_errors(sqlm_ctx *c);
+
 int prepare(sqlm_ctx *c, int level) {
   DevProblem &d = c->d;
+  // edges outside this call's level keep their last error (g2o semantics):
+  // bring the previous call's errors home before the device copies change
+  if (int s = fetch_errors(c)) return s;
   c->prepared = false;
   // the page-locked staging arrays are rewritten (or regrown) below: no DMA of
   // an earlier call, finished or abandoned on an error path, may still read them
@@ -1244,13 +1253,59 @@ int prepare(sqlm_ctx *c, int level) {
   return SQLM_OK;
 }
 
+// The per-edge errors of the last optimize() (computeActiveErrors' _error of
+// every active edge) into the caller-order host arrays: ~90 MB on config 4,
+// fetched only when a caller needs an edge chi2 (LBA outlier tags,
+// sqlm_get_edge_chi2) or before the next prepare() replaces them on the
+// device -- a GBA call that never asks does not pay for the copy.
+void ensure_host_errors(sqlm_ctx *c) {
+  if (!c->err_zero) return;
+  c->err_zero = false;
+  par_assign(c->obs_err, (const double *)nullptr, 2 * (size_t)c->n_obs);
+}
+
+int fetch_errors(sqlm_ctx *c) {
+  if (!c->err_pending) return SQLM_OK;
+  c->err_pending = false;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  ensure_host_errors(c);
+  DevProblem &d = c->d;
+  PinVec<double> err, err3, lerr;
+  std::vector<double> fallback[3];
+  auto stage = [&](int id, size_t n, PinVec<double> &v, int k) {
+    if (pinned(c, id, n, v) == SQLM_OK) return;
+    fallback[k].resize(std::max<size_t>(n, 1));
+    v.p = fallback[k].data();
+    v.n = n;
+  };
+  stage(P_RERR, 2 * (size_t)d.nE, err, 0);
+  stage(P_RERR3, d.obs_err3 ? (size_t)d.nE : 0, err3, 1);
+  stage(P_RLERR, (size_t)d.nLid, lerr, 2);
+  if (err3.size())
+    HIP_OK(hipMemcpyAsync(err3.data(), d.obs_err3, err3.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (d.nE) HIP_OK(hipMemcpyAsync(err.data(), d.obs_err, err.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (d.nLid)
+    HIP_OK(hipMemcpyAsync(lerr.data(), d.lid_err, lerr.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  const int nth = host_threads(d.nE);
+  run_threads(nth, [&](int t) {
+    for (int64_t o = d.nE * t / nth; o < d.nE * (t + 1) / nth; ++o) {
+      c->obs_err[2 * c->dev_edge[o]] = err[2 * o];
+      c->obs_err[2 * c->dev_edge[o] + 1] = err[2 * o + 1];
+      if (err3.size()) c->obs_err3[c->dev_edge[o]] = err3[o];
+    }
+  });
+  for (int64_t t = 0; t < d.nLid; ++t) c->lid_err[c->dev_lid_edge[t]] = lerr[t];
+  return SQLM_OK;
+}
+
 int finish(sqlm_ctx *c) {
   DevProblem &d = c->d;
   // device -> page-locked staging (one DMA each; pageable vectors if the
   // page-locked arena cannot grow), then the scatter back to caller order on
-  // host threads
-  PinVec<double> qt, X, err, err3, lerr;
-  std::vector<double> fallback[5];
+  // host threads; the edge errors stay on the device until asked for
+  PinVec<double> qt, X;
+  std::vector<double> fallback[2];
   auto stage = [&](int id, size_t n, PinVec<double> &v, int k) {
     if (pinned(c, id, n, v) == SQLM_OK) return;
     fallback[k].resize(std::max<size_t>(n, 1));
@@ -1259,32 +1314,19 @@ int finish(sqlm_ctx *c) {
   };
   stage(P_RQT, 8 * (size_t)c->n_pose, qt, 0);
   stage(P_RX, 4 * (size_t)d.nL, X, 1);
-  stage(P_RERR, 2 * (size_t)d.nE, err, 2);
-  stage(P_RERR3, d.obs_err3 ? (size_t)d.nE : 0, err3, 3);
-  stage(P_RLERR, (size_t)d.nLid, lerr, 4);
-  if (err3.size())
-    HIP_OK(hipMemcpyAsync(err3.data(), d.obs_err3, err3.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipMemcpyAsync(qt.data(), d.pose_qt[0], qt.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   if (d.nL) HIP_OK(hipMemcpyAsync(X.data(), d.X[0], X.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  if (d.nE) HIP_OK(hipMemcpyAsync(err.data(), d.obs_err, err.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  if (d.nLid)
-    HIP_OK(hipMemcpyAsync(lerr.data(), d.lid_err, lerr.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_OK(hipStreamSynchronize(c->stream));
   for (int p = 0; p < c->n_pose; ++p) {
     for (int k = 0; k < 4; ++k) c->pose_q[4 * p + k] = qt[8 * p + k];
     for (int k = 0; k < 3; ++k) c->pose_t[3 * p + k] = qt[8 * p + 4 + k];
   }
-  const int nth = host_threads(d.nE);
+  const int nth = host_threads(d.nL * 8);
   run_threads(nth, [&](int t) {
     for (int s = (int)((int64_t)d.nL * t / nth); s < (int)((int64_t)d.nL * (t + 1) / nth); ++s)
       for (int k = 0; k < 3; ++k) c->pt[3 * c->slot_pt[s] + k] = X[4 * s + k];
-    for (int64_t o = d.nE * t / nth; o < d.nE * (t + 1) / nth; ++o) {
-      c->obs_err[2 * c->dev_edge[o]] = err[2 * o];
-      c->obs_err[2 * c->dev_edge[o] + 1] = err[2 * o + 1];
-      if (err3.size()) c->obs_err3[c->dev_edge[o]] = err3[o];
-    }
   });
-  for (int64_t t = 0; t < d.nLid; ++t) c->lid_err[c->dev_lid_edge[t]] = lerr[t];
+  c->err_pending = d.nE > 0 || d.nLid > 0;
   return SQLM_OK;
 }
 
@@ -1735,7 +1777,8 @@ int sqlm_set_problem(sqlm_ctx *c, int n_pose, const double *pose_q, const double
   par_assign(c->obs_info, obs_info, (size_t)n_obs);
   par_assign(c->obs_delta, obs_delta, (size_t)n_obs);  // null: no robust kernel (zeros)
   par_assign(c->obs_level, obs_level, (size_t)n_obs);  // null: level 0
-  par_assign(c->obs_err, (const double *)nullptr, 2 * (size_t)n_obs);
+  c->err_pending = false;  // sized and zeroed when first read (ensure_host_errors)
+  c->err_zero = true;
   c->has_stereo = false;
   c->obs_ur.clear(); c->pose_bf.clear(); c->obs_err3.clear();
   c->n_lid = 0;
@@ -1747,6 +1790,7 @@ int sqlm_set_problem(sqlm_ctx *c, int n_pose, const double *pose_q, const double
 
 int sqlm_set_stereo(sqlm_ctx *c, const double *obs_ur, const double *pose_bf) {
   if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  if (int s = fetch_errors(c)) return s;  // the last call's errors, in the layout they were computed in
   c->has_stereo = false;
   c->obs_ur.clear(); c->pose_bf.clear(); c->obs_err3.clear();
   if (!obs_ur) return SQLM_OK;  // back to all-mono
@@ -1770,6 +1814,7 @@ int sqlm_set_lidar(sqlm_ctx *c, int64_t n, const int32_t *pose, const double *p_
   if (n && (!pose || !p_cam || !p_world || !normal || !info)) return SQLM_ERR_INVALID_ARG;
   for (int64_t e = 0; e < n; ++e)
     if (pose[e] < 0 || pose[e] >= c->n_pose) return SQLM_ERR_INVALID_ARG;
+  if (int s = fetch_errors(c)) return s;  // the last call's errors, in the layout they were computed in
   c->n_lid = n;
   c->lid_pose.assign(pose, pose + n);
   c->lid_pc.assign(p_cam, p_cam + 3 * n);
@@ -1818,6 +1863,8 @@ int sqlm_local_ba(sqlm_ctx *c, const volatile uint8_t *stop, uint8_t *outlier, s
   for (auto &l : c->lid_level) l = 255;  // LiDAR edges only exist in pass 3
   int n = 0, s = optimize_impl(c, 0, 5, 0.0, stop, &st[0], &n);
   if (s) return s;
+  if ((s = fetch_errors(c))) return s;
+  ensure_host_errors(c);
   if (!stopped(stop)) {  // :952-975
     std::vector<uint8_t> dp;
     depth_positive_host(c, dp);
@@ -1834,6 +1881,8 @@ int sqlm_local_ba(sqlm_ctx *c, const volatile uint8_t *stop, uint8_t *outlier, s
   if (outlier) {  // :1119-1136
     std::vector<uint8_t> dp;
     depth_positive_host(c, dp);
+    if ((s = fetch_errors(c))) return s;
+    ensure_host_errors(c);
     for (int64_t e = 0; e < c->n_obs; ++e) outlier[e] = (edge_chi2(c, e) > tag_threshold(c, e) || !dp[e]);
   }
   if (ran) *ran = 1;
@@ -1891,6 +1940,9 @@ int sqlm_get_points(sqlm_ctx *c, double *pt) {
 int sqlm_get_edge_chi2(sqlm_ctx *c, double *chi2) {
   if (!c || !c->has_problem) return SQLM_ERR_STATE;
   if (!chi2 && c->n_obs) return SQLM_ERR_INVALID_ARG;
+  if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
+  if (int s = fetch_errors(c)) return s;
+  ensure_host_errors(c);
   for (int64_t e = 0; e < c->n_obs; ++e) chi2[e] = edge_chi2(c, e);
   return SQLM_OK;
 }
