@@ -83,6 +83,16 @@ struct TilePlan {
 
 
 
+// Intermediate state of build_tiles between the tiles (passes 1-2) and the
+// reduction lists, which need the S pattern (built from the tiles' camera
+// pairs in between).
+struct TileBuild {
+  struct Red { int key, tile, code, j; };  // key: camera i until the pattern exists, then the S block
+  struct TileOut { std::vector<int> cams; std::vector<Red> red; };
+  std::vector<int> tstart;
+  std::vector<TileOut> out;
+};
+
 struct sqlm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -122,6 +132,7 @@ struct sqlm_ctx {
   // host plan scratch kept across calls (capacity reused: prepare() allocates
   // and first-touches none of its large arrays after the first call)
   TilePlan tp;
+  TileBuild tb;
   std::vector<std::vector<int>> scat_base;  // per-thread counting-sort bases (slots)
   std::vector<int> h_kcount, h_span_lo, h_span_hi, h_pt_slot, h_key;
   std::vector<uint8_t> h_pose_act, h_pt_act;
@@ -245,7 +256,7 @@ enum BufId {
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
-  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL
+  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL, B_CAMKEY0, B_CAMKEY1, B_CAMVAL, B_SORTTMP
 };
 
 // Persistent host worker pool for the setup passes (a prepare() runs ~20
@@ -350,8 +361,8 @@ void par_assign(std::vector<T> &v, const T *src, size_t n) {
   });
 }
 
-void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *obs_camh,
-                 const std::vector<int> &s_row, const std::vector<int> &s_col, int lm_cap, TilePlan &tp) {
+void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *obs_camh, int lm_cap, TilePlan &tp,
+                 TileBuild &tb) {
   const int64_t nE = lm_begin[nL];
   const bool ptime = std::getenv("SQLM_PREP_TIMING") != nullptr;
   auto pt0 = std::chrono::steady_clock::now();
@@ -370,7 +381,8 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
   // 128k observations, at most 16; a tile never crosses a chunk start), so the
   // tile plan -- and with it the fixed summation order of S -- is the same on
   // every host; the chunks are then dealt to however many threads there are.
-  std::vector<int> tstart;
+  std::vector<int> &tstart = tb.tstart;
+  tstart.clear();
   {
     const int nchunk = (int)std::max<int64_t>(1, std::min<int64_t>(16, nE / 131072));
     const int nth = std::min(nchunk, host_threads(nE));
@@ -418,9 +430,8 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
   const int nt = (int)tstart.size() - 1;
   // pass 2 (tiles on host threads): window cameras, local camera of every
   // observation, landmark spans, and the S blocks each tile contributes to
-  struct Red { int key, tile, code; };
-  struct TileOut { std::vector<int> cams; std::vector<Red> red; };
-  std::vector<TileOut> out(nt);
+    std::vector<TileBuild::TileOut> &out = tb.out;
+  out.assign(nt, TileBuild::TileOut{});
   const int nth = host_threads(nE);
   run_threads(nth, [&](int th) {
     std::vector<int> lidx(nP, -1), lcams;
@@ -455,24 +466,85 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
           }
       }
       for (int u = 0; u < cp; ++u)
-        for (int v = u; v < cp; ++v) {
-          if (!pst[(size_t)u * cp + v]) continue;
-          const int i = cur[u], j = cur[v];
-          const int *b0 = s_col.data() + s_row[i], *b1 = s_col.data() + s_row[i + 1];
-          const int sidx = (int)(std::lower_bound(b0, b1, j) - s_col.data());
-          out[t].red.push_back({sidx, t, tile_blk(u, v, cp)});
-        }
+        for (int v = u; v < cp; ++v)
+          if (pst[(size_t)u * cp + v]) out[t].red.push_back({cur[u], t, tile_blk(u, v, cp), cur[v]});
       for (int u = 0; u < cp; ++u) lidx[cur[u]] = -1;
     }
   });
   sub("pass 2");
+}
+
+// S pattern (upper, diagonal first) of the free cameras from the tiles'
+// camera pairs: every pair of cameras that co-observe a landmark is marked in
+// the tile that holds the landmark; plus every diagonal.
+void pattern_from_tiles(int nP, const TileBuild &tb, std::vector<int> &s_row, std::vector<int> &s_col) {
+  const int nt = (int)tb.out.size();
+  const int nth = host_threads((int64_t)nt * 256);
+  std::vector<std::vector<int>> cnt(nth, std::vector<int>(nP, 0));
+  run_threads(nth, [&](int th) {
+    for (int t = th; t < nt; t += nth)
+      for (const auto &r : tb.out[t].red)
+        if (r.j != r.key) ++cnt[th][r.key];
+  });
+  std::vector<int> ptr(nP + 1, 0);
+  for (int i = 0; i < nP; ++i) {
+    int b = ptr[i] + 1;  // the diagonal first
+    for (int th = 0; th < nth; ++th) { const int k = cnt[th][i]; cnt[th][i] = b; b += k; }
+    ptr[i + 1] = b;
+  }
+  std::vector<int> raw(ptr[nP]);
+  for (int i = 0; i < nP; ++i) raw[ptr[i]] = i;
+  run_threads(nth, [&](int th) {
+    for (int t = th; t < nt; t += nth)
+      for (const auto &r : tb.out[t].red)
+        if (r.j != r.key) raw[cnt[th][r.key]++] = r.j;
+  });
+  std::vector<int> len(nP);
+  run_threads(host_threads((int64_t)ptr[nP]), [&](int th) {
+    const int n = host_threads((int64_t)ptr[nP]);
+    for (int i = (int)((int64_t)nP * th / n); i < (int)((int64_t)nP * (th + 1) / n); ++i) {
+      int *b = raw.data() + ptr[i] + 1, *e = raw.data() + ptr[i + 1];
+      std::sort(b, e);
+      len[i] = 1 + (int)(std::unique(b, e) - b);
+    }
+  });
+  s_row.assign(nP + 1, 0);
+  for (int i = 0; i < nP; ++i) s_row[i + 1] = s_row[i] + len[i];
+  s_col.resize(s_row[nP]);
+  for (int i = 0; i < nP; ++i) std::copy(raw.begin() + ptr[i], raw.begin() + ptr[i] + len[i], s_col.begin() + s_row[i]);
+}
+
+// The reduction lists of the tiles (needs the final S pattern).
+void build_tiles_finish(int nP, const std::vector<int> &s_row, const std::vector<int> &s_col, TilePlan &tp,
+                        TileBuild &tb) {
+  const bool ptime = std::getenv("SQLM_PREP_TIMING") != nullptr;
+  auto pt0 = std::chrono::steady_clock::now();
+  auto sub = [&](const char *what) {
+    if (!ptime) return;
+    const auto now = std::chrono::steady_clock::now();
+    std::fprintf(stderr, "  tiles %-14s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(now - pt0).count());
+    pt0 = now;
+  };
+  using Red = TileBuild::Red;
+  std::vector<TileBuild::TileOut> &out = tb.out;
+  const std::vector<int> &tstart = tb.tstart;
+  const int nt = (int)out.size();
+  run_threads(host_threads((int64_t)nt * 256), [&](int th) {  // S block of every tile pair
+    const int n = host_threads((int64_t)nt * 256);
+    for (int t = th; t < nt; t += n)
+      for (Red &r : out[t].red) {
+        const int *b0 = s_col.data() + s_row[r.key], *b1 = s_col.data() + s_row[r.key + 1];
+        r.key = (int)(std::lower_bound(b0, b1, r.j) - s_col.data());
+      }
+  });
+  sub("keys");
   // pass 3 (tile order): offsets, camera lists, the reduction lists
   std::vector<Red> red, gred;
   for (int t = 0; t < nt; ++t) {
     const std::vector<int> &cur = out[t].cams;
     const int cp = (int)cur.size();
     red.insert(red.end(), out[t].red.begin(), out[t].red.end());
-    for (int u = 0; u < cp; ++u) gred.push_back({cur[u], t, u});
+    for (int u = 0; u < cp; ++u) gred.push_back({cur[u], t, u, 0});
     const int ld = (6 * cp + 15) / 16 * 16;
     tp.ld.push_back(ld);
     tp.part_ptr.push_back(tp.part_ptr.back() + 36 * (int64_t)(cp * (cp + 1) / 2));
@@ -845,9 +917,12 @@ int prepare(sqlm_ctx *c, int level) {
       }
     });
   }
-  // camera CSR (device obs in slot order), the same chunked counting sort
+  // camera CSR (device obs in slot order): on the device (launch_cam_csr,
+  // after the observation upload); on the host, the same chunked counting
+  // sort, only for a sharded run, whose S pattern union walks it
   std::vector<int> cam_ptr(nP + 1, 0), cam_obs;
-  {
+  int64_t n_cam_obs = 0;
+  if (sharded) {
     auto obeg = [&](int t) { return nE * t / nth; };
     std::vector<std::vector<int>> base(nth);
     par([&](int t) {
@@ -868,6 +943,15 @@ int prepare(sqlm_ctx *c, int level) {
       for (int64_t o = obeg(t); o < obeg(t + 1); ++o)
         if (obs_camh[o] >= 0) cam_obs[fill[obs_camh[o]]++] = (int)o;
     });
+    n_cam_obs = (int64_t)cam_obs.size();
+  } else {
+    std::vector<int64_t> cnt(nth, 0);
+    par([&](int t) {
+      int64_t k = 0;
+      for (int64_t o = nE * t / nth; o < nE * (t + 1) / nth; ++o) k += obs_camh[o] >= 0;
+      cnt[t] = k;
+    });
+    for (int64_t k : cnt) n_cam_obs += k;
   }
   {  // the observation arrays go to the device now, overlapped with the rest of the setup
     int e = 0;
@@ -905,9 +989,21 @@ int prepare(sqlm_ctx *c, int level) {
       }
     });
   }
-  // reduced-camera-system pattern (upper, diagonal first)
+  // RCS tiles (passes 1-2: windows, local cameras, camera pairs), then the
+  // reduced-camera-system pattern (upper, diagonal first) from the tiles'
+  // camera pairs, then the tiles' reduction lists over that pattern
+  TilePlan &tp = c->tp;
+  // landmarks per tile: up to kTileMaxLm, fewer on small problems so that the
+  // tiles still cover every CU twice (a local-BA window of 5k landmarks would
+  // otherwise run ~40 long tiles on 256 CUs)
+  const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
+  TileBuild &tb = c->tb;
+  build_tiles(nP, nL, lm_begin, obs_camh.data(), lm_cap, tp, tb);
+  phase("tiles");
   std::vector<int> s_row(nP + 1, 0), s_col;
-  {
+  if (!sharded) {
+    pattern_from_tiles(nP, tb, s_row, s_col);
+  } else {
     std::vector<std::vector<int>> rows(nP);
     {  // rows are independent: a few host threads, each with its own marks
       const int nth = host_threads(nE);
@@ -930,8 +1026,7 @@ int prepare(sqlm_ctx *c, int level) {
       };
       run_threads(nth, work);
     }
-    if (sharded) {
-      // every rank needs the same pattern: the union of the shards' patterns.
+    {  // every rank needs the same pattern: the union of the shards' patterns.
       // Blocks within kNearCams of the diagonal as one flag per (row, offset),
       // OR-ed by an all-reduce (max); the few far blocks (loop closures) as
       // (row, column) pairs all-gathered through a summed, zero-padded buffer
@@ -969,23 +1064,18 @@ int prepare(sqlm_ctx *c, int level) {
     }
     for (int i = 0; i < nP; ++i) s_row[i + 1] = s_row[i] + (int)rows[i].size();
     s_col.resize(s_row[nP]);
+    for (int i = 0; i < nP; ++i) std::copy(rows[i].begin(), rows[i].end(), s_col.begin() + s_row[i]);
+  }
+  {
     int mx = 0;
-    for (int i = 0; i < nP; ++i) {
-      std::copy(rows[i].begin(), rows[i].end(), s_col.begin() + s_row[i]);
-      mx = std::max(mx, (int)rows[i].size());
-    }
+    for (int i = 0; i < nP; ++i) mx = std::max(mx, s_row[i + 1] - s_row[i]);
     c->max_row_blocks = mx;
     // band (+ border) superblock plan; the dense Cholesky otherwise
     if (!plan_rcs(nP, s_row, s_col, c->cr, c->cam_pos)) c->cr = CRPlan{};
   }
-  TilePlan &tp = c->tp;
-  // landmarks per tile: up to kTileMaxLm, fewer on small problems so that the
-  // tiles still cover every CU twice (a local-BA window of 5k landmarks would
-  // otherwise run ~40 long tiles on 256 CUs)
-  const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
   phase("S pattern");
-  build_tiles(nP, nL, lm_begin, obs_camh.data(), s_row, s_col, lm_cap, tp);
-  phase("tiles");
+  build_tiles_finish(nP, s_row, s_col, tp, tb);
+  phase("tile lists");
   if (ptime) {  // plan shape: tile count, longest reduction lists, solver layout
     int rmax = 0, gmax = 0;
     for (size_t s = 0; s + 1 < tp.red_ptr.size(); ++s) rmax = std::max(rmax, tp.red_ptr[s + 1] - tp.red_ptr[s]);
@@ -1106,21 +1196,36 @@ int prepare(sqlm_ctx *c, int level) {
     AL(B_OBSP, 18 * (size_t)nE, d.obs_P);
   }
   AL(B_OBSERR, 2 * (size_t)nE, d.obs_err);
-  UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
-  UP(B_CAMOBS, cam_obs, d.cam_obs);
+  if (sharded) {
+    UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
+    UP(B_CAMOBS, cam_obs, d.cam_obs);
+  } else {  // the stable counting sort on the device (same result as the host's)
+    unsigned *k0 = nullptr, *k1 = nullptr;
+    int *v0 = nullptr;
+    unsigned char *tmp = nullptr;
+    const size_t tb = cam_csr_temp_bytes(nE, nP);
+    AL(B_CAMKEY0, (size_t)nE, k0);
+    AL(B_CAMKEY1, (size_t)nE, k1);
+    AL(B_CAMVAL, (size_t)nE, v0);
+    AL(B_SORTTMP, tb, tmp);
+    AL(B_CAMOBS, (size_t)nE, d.cam_obs);
+    AL(B_CAMPTR, (size_t)nP + 1, d.cam_obs_ptr);
+    if (launch_cam_csr(d.obs_camh, nE, nP, k0, k1, v0, d.cam_obs, d.cam_obs_ptr, tmp, tb, c->stream))
+      return SQLM_ERR_HIP;
+  }
   d.has_stereo = c->has_stereo ? 1 : 0;
   if (c->has_stereo) {
     UP(B_POSEBF, c->pose_bf, d.pose_bf);
     AL(B_OBSERR3, (size_t)nE, d.obs_err3);
-    AL(B_CAMUR, cam_obs.size(), d.cam_ur);
+    AL(B_CAMUR, (size_t)n_cam_obs, d.cam_ur);
   } else {
     d.obs_ur = d.obs_err3 = d.pose_bf = d.cam_ur = nullptr;
   }
   // camera-ordered copies of the camera pass inputs (one coalesced stream +
   // the X gather), gathered on the device from the slot-ordered arrays
-  AL(B_CAMSLOT, cam_obs.size(), d.cam_slot);
-  AL(B_CAMUV, 4 * cam_obs.size(), d.cam_uv);
-  launch_cam_gather(d, (int64_t)cam_obs.size(), c->stream);
+  AL(B_CAMSLOT, (size_t)n_cam_obs, d.cam_slot);
+  AL(B_CAMUV, 4 * (size_t)n_cam_obs, d.cam_uv);
+  launch_cam_gather(d, n_cam_obs, c->stream);
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
   {

@@ -223,6 +223,10 @@ void launch_camera_pass(const DevProblem &d, hipStream_t st, bool spec = false);
 void launch_pose_maxdiag(const DevProblem &d, hipStream_t st);
 void launch_pose_diag(const DevProblem &d, hipStream_t st);
 void launch_cam_gather(const DevProblem &d, int64_t n_cam_obs, hipStream_t st);
+// camera CSR of the device observations (stable: observation order within a camera)
+size_t cam_csr_temp_bytes(int64_t n, int nP);
+int launch_cam_csr(const int *camh, int64_t n, int nP, unsigned *keys_in, unsigned *keys_out, int *vals_in,
+                   int *cam_obs, int *cam_ptr, void *temp, size_t temp_bytes, hipStream_t st);
 // rank 0 of a sharded run: destination / source ranges of the gathered rows
 constexpr int kMaxRanks = 16;
 struct GatherTab {

@@ -24,6 +24,9 @@
 
 #include <algorithm>
 
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "se3_dev.h"
 #include "sqlm_internal.h"
 
@@ -610,6 +613,59 @@ __global__ __launch_bounds__(256) void k_cam_gather(DevProblem d, int64_t n) {
   u[2] = d.obs_info[o];
   u[3] = d.obs_delta[o];
   if (d.cam_ur) d.cam_ur[t] = d.obs_ur[o];
+}
+
+// ---- camera CSR on the device: the observations of every free camera in
+// observation (slot) order, = the host's stable counting sort. Keys are the
+// free camera id (fixed cameras -> nP, sorted last), values the observation;
+// a stable radix sort over the key bits, then each camera's start by binary
+// search over the sorted keys.
+__global__ __launch_bounds__(256) void k_cam_keys(const int *__restrict__ camh, int64_t n, int nP,
+                                                  unsigned *__restrict__ keys, int *__restrict__ vals) {
+  const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= n) return;
+  const int h = camh[o];
+  keys[o] = h >= 0 ? (unsigned)h : (unsigned)nP;
+  vals[o] = (int)o;
+}
+
+__global__ __launch_bounds__(256) void k_cam_ptr(const unsigned *__restrict__ keys, int64_t n, int nP,
+                                                 int *__restrict__ ptr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > nP) return;
+  int64_t lo = 0, hi = n;  // first position with key >= i
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < (unsigned)i) lo = mid + 1;
+    else hi = mid;
+  }
+  ptr[i] = (int)lo;
+}
+
+static unsigned cam_key_bits(int nP) {
+  unsigned b = 1;
+  while ((1u << b) <= (unsigned)nP) ++b;
+  return b;
+}
+
+size_t cam_csr_temp_bytes(int64_t n, int nP) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (unsigned *)nullptr, (unsigned *)nullptr, (int *)nullptr,
+                                  (int *)nullptr, (size_t)n, 0u, cam_key_bits(nP));
+  return std::max<size_t>(bytes, 16);
+}
+
+int launch_cam_csr(const int *camh, int64_t n, int nP, unsigned *keys_in, unsigned *keys_out, int *vals_in,
+                   int *cam_obs, int *cam_ptr, void *temp, size_t temp_bytes, hipStream_t st) {
+  if (n > 0) {
+    hipLaunchKernelGGL(k_cam_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, camh, n, nP, keys_in, vals_in);
+    size_t bytes = temp_bytes;
+    if (rocprim::radix_sort_pairs(temp, bytes, keys_in, keys_out, vals_in, cam_obs, (size_t)n, 0u, cam_key_bits(nP),
+                                  st) != hipSuccess)
+      return -2;
+  }
+  hipLaunchKernelGGL(k_cam_ptr, dim3((unsigned)((nP + 1 + 255) / 256)), dim3(256), 0, st, keys_out, n, nP, cam_ptr);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 void launch_cam_gather(const DevProblem &d, int64_t n, hipStream_t st) {
