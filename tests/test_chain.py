@@ -110,3 +110,28 @@ def test_chain_gpu_matches_oracle_every_stage(gpu_ctx, oracle):
     assert n_g == n and st_g["trace_trials"] == st["trace_trials"]
     np.testing.assert_allclose(st_g["trace_chi2"], st["trace_chi2"], rtol=tol)
     assert np.abs(q_g - q).max() < tol and _rel(t_g, t) < tol and _rel(X_g, X) < tol
+
+
+def test_kitti00_map_shape():
+    """The KITTI-00-scale stand-in of tests/test_chain_kitti.py (GPU test):
+    its size, the two loop closures (revisit keyframes co-observe landmarks
+    with the first-pass keyframes at their places), the stereo share, and the
+    odometry-drift initial error (neighbours consistent, the revisit far end
+    drifted)."""
+    from sqrtlm import synth
+    prob = CU.make_kitti00_map()
+    assert prob.n_pose == 1500 and 90_000 < prob.n_pt <= 100_000 and prob.n_obs > 1_000_000
+    assert 0.4 < float((prob.obs_ur >= 0).mean()) < 0.6
+    la, lb = CU.loop_pairs(prob, 0)
+    assert la.size == lb.size == 140 and set(lb[:40].tolist()) == set(range(700, 740))
+    # fused points: a revisit keyframe shares landmarks with its first-pass twin
+    obs_p, obs_l = prob.obs_pose, prob.obs_pt
+    shared = [np.intersect1d(obs_l[obs_p == a], obs_l[obs_p == b]).size for a, b in zip(la[::20], lb[::20])]
+    assert min(shared) > 50, shared
+
+    def centres(q, t):
+        return -np.einsum("nji,nj->ni", synth.quat_to_mat(q), t)
+    err = np.linalg.norm(centres(prob.pose_q, prob.pose_t) - centres(prob.meta["gt_q"], prob.meta["gt_t"]), axis=1)
+    step = np.linalg.norm(np.diff(centres(prob.pose_q, prob.pose_t), axis=0)
+                          - np.diff(centres(prob.meta["gt_q"], prob.meta["gt_t"]), axis=0), axis=1)
+    assert err[0] == 0.0 and err[1400:].mean() > 0.1 and np.median(step) < 0.05
