@@ -1065,20 +1065,56 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_t
         m.y = pr[3] * xl[0] + pr[4] * xl[1] + pr[5] * xl[2] + pr[10];
         m.z = pr[6] * xl[0] + pr[7] * xl[1] + pr[8] * xl[2] + pr[11];
         m.s = ps;
-        double jl[6], jp[12], jl3[3] = {0, 0, 0}, jp3[6] = {0, 0, 0, 0, 0, 0};
-        mono_jac(pr, m, jl, jp);
-        const bool st = ST && pur >= 0.0;
-        if (st) stereo_row(pr, m, Lbf[pu], jl, jp, jl3, jp3);
         const int row = 3 * (pli - lb), col = 6 * pu;
+        if (!(ST && pur >= 0.0)) {
+          // mono: jl = s J_pi R and jp = s J_pi [-[X_c]x | I] (types_six_dof_expmap.cpp:
+          // 103-139), so P = jl^T jp = [-B' [X_c]x | B'] with B' = R^T A,
+          // A = s^2 J_pi^T J_pi (3x3, five distinct entries), and Y = R'^-T P =
+          // [-B [X_c]x | B], B = R'^-T R^T A: ~45 % fewer FP64 operations than
+          // forming jl, jp and their 18 products
+          const double iz = 1.0 / m.z, xz = m.x * iz, yz = m.y * iz, fx = pr[12], fy = pr[13];
+          const double t00 = -iz * fx, t02 = (xz * iz) * fx, t11 = -iz * fy, t12 = (yz * iz) * fy;
+          const double s2 = ps * ps;
+          const double A00 = s2 * (t00 * t00), A02 = s2 * (t00 * t02), A11 = s2 * (t11 * t11),
+                       A12 = s2 * (t11 * t12), A22 = s2 * (t02 * t02 + t12 * t12);
+          double Q[3][3];  // R^T A
 #pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          double p0 = jl[0] * jp[c] + jl[3] * jp[6 + c];
-          double p1 = jl[1] * jp[c] + jl[4] * jp[6 + c];
-          double p2 = jl[2] * jp[c] + jl[5] * jp[6 + c];
-          if (st) { p0 += jl3[0] * jp3[c]; p1 += jl3[1] * jp3[c]; p2 += jl3[2] * jp3[c]; }
-          Y[row][col + c] = r[0] * p0;
-          Y[row + 1][col + c] = r[1] * p0 + r[3] * p1;
-          Y[row + 2][col + c] = r[2] * p0 + r[4] * p1 + r[5] * p2;
+          for (int i = 0; i < 3; ++i) {
+            Q[i][0] = pr[i] * A00 + pr[6 + i] * A02;
+            Q[i][1] = pr[3 + i] * A11 + pr[6 + i] * A12;
+            Q[i][2] = pr[i] * A02 + pr[3 + i] * A12 + pr[6 + i] * A22;
+          }
+#pragma unroll
+          for (int j = 0; j < 3; ++j) {  // B = R'^-T Q (R'^-1 upper: r0 r1 r2 / r3 r4 / r5)
+            const double b0 = r[0] * Q[0][j], b1 = r[1] * Q[0][j] + r[3] * Q[1][j],
+                         b2 = r[2] * Q[0][j] + r[4] * Q[1][j] + r[5] * Q[2][j];
+            Q[0][j] = b0;
+            Q[1][j] = b1;
+            Q[2][j] = b2;
+          }
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            double *yr = &Y[row + q][col];
+            yr[0] = Q[q][2] * m.y - Q[q][1] * m.z;
+            yr[1] = Q[q][0] * m.z - Q[q][2] * m.x;
+            yr[2] = Q[q][1] * m.x - Q[q][0] * m.y;
+            yr[3] = Q[q][0];
+            yr[4] = Q[q][1];
+            yr[5] = Q[q][2];
+          }
+        } else {  // stereo: the third row's Jacobians join the products
+          double jl[6], jp[12], jl3[3], jp3[6];
+          mono_jac(pr, m, jl, jp);
+          stereo_row(pr, m, Lbf[pu], jl, jp, jl3, jp3);
+#pragma unroll
+          for (int c = 0; c < 6; ++c) {
+            const double p0 = jl[0] * jp[c] + jl[3] * jp[6 + c] + jl3[0] * jp3[c];
+            const double p1 = jl[1] * jp[c] + jl[4] * jp[6 + c] + jl3[1] * jp3[c];
+            const double p2 = jl[2] * jp[c] + jl[5] * jp[6 + c] + jl3[2] * jp3[c];
+            Y[row][col + c] = r[0] * p0;
+            Y[row + 1][col + c] = r[1] * p0 + r[3] * p1;
+            Y[row + 2][col + c] = r[2] * p0 + r[4] * p1 + r[5] * p2;
+          }
         }
       }
     } else if (tid < 6) {  // repeated cameras / long tracks: serial, observation order
