@@ -140,6 +140,11 @@ struct sqlm_ctx {
   std::vector<DevBuf> bufs;
   std::vector<DevBuf> pins;  // page-locked host staging of the large uploads (async DMA)
   double *h_scalars = nullptr;  // pinned
+  // the trial scalars' mailbox (mapped, coherent page-locked memory written by
+  // k_reduce): the host polls its sequence number instead of a copy + stream
+  // synchronize; SQLM_NO_MBOX=1 (A/B), timing runs and sharded runs copy
+  double *mbox = nullptr, *mbox_dev = nullptr;
+  unsigned long long mbox_seq = 0;
   // ---- comm ----
   Comm comm;
   // ---- essential graph (sqlm_eg.hip) ----
@@ -1484,18 +1489,50 @@ struct TrialOut {
   bool ok;
 };
 
+// Wait for k_reduce's mailbox entry `seq`. The stream is polled now and then:
+// an error ends the wait, and so does a drained stream without the entry
+// (the copy path then takes over). Returns the scalars or null.
+const double *mbox_wait(sqlm_ctx *c, unsigned long long seq, int &err) {
+  err = SQLM_OK;
+  const unsigned long long *slot = reinterpret_cast<const unsigned long long *>(c->mbox + kMboxSeq);
+  for (unsigned it = 1;; ++it) {
+    if (__atomic_load_n(slot, __ATOMIC_ACQUIRE) == seq) return c->mbox;
+    if ((it & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) return __atomic_load_n(slot, __ATOMIC_ACQUIRE) == seq ? c->mbox : nullptr;
+      if (q != hipErrorNotReady) {
+        err = SQLM_ERR_HIP;
+        return nullptr;
+      }
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 int reduce_and_fetch(sqlm_ctx *c, TrialOut &o) {
   DevProblem &d = c->d;
-  launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream);
+  static const bool no_mbox = std::getenv("SQLM_NO_MBOX") != nullptr;
+  const bool mb = c->mbox && !no_mbox && !c->timing && !c->comm.enabled();
+  const unsigned long long seq = mb ? ++c->mbox_seq : 0;
+  launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream,
+                mb ? c->mbox_dev : nullptr, seq);
   int s = comm_allreduce_scalars(c->comm, d.scalars, c->need_maxdiag, c->stream);
   if (s) return s;
-  HIP_OK(hipMemcpyAsync(c->h_scalars, d.scalars, sizeof(double) * kNScalars, hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
-  o.chi_cur = c->h_scalars[kChiCur];
-  o.chi_new = c->h_scalars[kChiNew];
-  o.scale = c->h_scalars[kScale];
-  o.maxdiag = c->h_scalars[kMaxDiag];
-  o.ok = c->h_scalars[kSolveOk] > 0.5;
+  const double *h = nullptr;
+  if (mb) {
+    h = mbox_wait(c, seq, s);
+    if (s) return s;
+  }
+  if (!h) {
+    HIP_OK(hipMemcpyAsync(c->h_scalars, d.scalars, sizeof(double) * kNScalars, hipMemcpyDeviceToHost, c->stream));
+    HIP_OK(hipStreamSynchronize(c->stream));
+    h = c->h_scalars;
+  }
+  o.chi_cur = h[kChiCur];
+  o.chi_new = h[kChiNew];
+  o.scale = h[kScale];
+  o.maxdiag = h[kMaxDiag];
+  o.ok = h[kSolveOk] > 0.5;
   return SQLM_OK;
 }
 
@@ -1797,6 +1834,17 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
     delete c;
     return SQLM_ERR_HIP;
   }
+  // the mailbox is an optimisation: without it the trial scalars are copied
+  if (hipHostMalloc((void **)&c->mbox, sizeof(double) * kNScalars, hipHostMallocMapped | hipHostMallocCoherent) ==
+      hipSuccess) {
+    std::memset(c->mbox, 0, sizeof(double) * kNScalars);
+    if (hipHostGetDevicePointer((void **)&c->mbox_dev, c->mbox, 0) != hipSuccess) {
+      (void)hipHostFree(c->mbox);
+      c->mbox = c->mbox_dev = nullptr;
+    }
+  } else {
+    c->mbox = nullptr;
+  }
   // timing-only events: no system-scope fence, which would flush caches and
   // leave a ~10 us bubble between the kernels they separate
   for (auto &e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
@@ -1833,6 +1881,7 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
+  if (c->mbox) (void)hipHostFree(c->mbox);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_spec_fork) (void)hipEventDestroy(c->ev_spec_fork);

@@ -148,6 +148,7 @@ struct DevProblem {
 };
 
 enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kNScalars = 8 };
+constexpr int kMboxSeq = 7;  // host mailbox: the scalars, then the sequence number in slot 7
 
 // partial-sum slots
 enum PartialRegion {
@@ -279,7 +280,7 @@ void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda,
                             bool spec = false);
 void launch_lidar_chi2(const DevProblem &d, hipStream_t st);
 void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts,
-                   int n_lid_parts, hipStream_t st);
+                   int n_lid_parts, hipStream_t st, double *mbox = nullptr, unsigned long long seq = 0);
 void launch_depth_positive(const DevProblem &d, uint8_t *out_dev, hipStream_t st);
 
 int linearize_blocks(const Bucket &b);

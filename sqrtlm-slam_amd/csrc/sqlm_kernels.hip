@@ -1679,8 +1679,11 @@ void launch_lidar_chi2(const DevProblem &d, hipStream_t st) {
 // of four strides in flight together (one memory latency per 4096 partials,
 // not one per 64), then fixed-order wave and block sums (deterministic).
 constexpr int kReduceThreads = 1024;
+// mbox (optional): the host's mailbox in page-locked host memory; the scalars
+// are written there too, then seq (a fence apart), so the host can poll it
+// instead of copying and synchronizing the stream.
 __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam,
-                                                          int n_lid) {
+                                                          int n_lid, double *mbox, unsigned long long seq) {
   __shared__ double red[6][kReduceThreads / 64];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const double *p = d.partials;
@@ -1723,13 +1726,23 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
     d.scalars[kMaxDiag] = __longlong_as_double((long long)*d.maxdiag);
     *d.maxdiag = 0ull;  // ready for the next linearization's atomicMax
     d.scalars[kSolveOk] = (double)d.flags[0];
+    if (mbox) {
+      mbox[kChiCur] = part[0] + part[1];
+      mbox[kChiNew] = part[2] + part[3];
+      mbox[kScale] = part[4] + part[5];
+      mbox[kMaxDiag] = d.scalars[kMaxDiag];
+      mbox[kSolveOk] = (double)d.flags[0];
+      __threadfence_system();
+      __hip_atomic_store(reinterpret_cast<unsigned long long *>(mbox + kMboxSeq), seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
 void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts, int n_lid_parts,
-                   hipStream_t st) {
+                   hipStream_t st, double *mbox, unsigned long long seq) {
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(kReduceThreads), 0, st, d, n_lm_parts_cur, n_lm_parts_new, n_cam_parts,
-                     n_lid_parts);
+                     n_lid_parts, mbox, seq);
 }
 
 }  // namespace sqlm
