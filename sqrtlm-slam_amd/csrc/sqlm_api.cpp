@@ -145,6 +145,11 @@ struct sqlm_ctx {
   // synchronize; SQLM_NO_MBOX=1 (A/B), timing runs and sharded runs copy
   double *mbox = nullptr, *mbox_dev = nullptr;
   unsigned long long mbox_seq = 0;
+  // SQLM_HOST_TRACE=1: host-side time points of every trial (diagnostic)
+  bool htrace = false;
+  std::chrono::steady_clock::time_point ht_prev{};
+  double ht_acc[10] = {};
+  int ht_n = 0;
   // ---- comm ----
   Comm comm;
   // ---- essential graph (sqlm_eg.hip) ----
@@ -1495,12 +1500,14 @@ struct TrialOut {
 const double *mbox_wait(sqlm_ctx *c, unsigned long long seq, int &err) {
   err = SQLM_OK;
   const unsigned long long *slot = reinterpret_cast<const unsigned long long *>(c->mbox + kMboxSeq);
+  Timer t;
   for (unsigned it = 1;; ++it) {
     if (__atomic_load_n(slot, __ATOMIC_ACQUIRE) == seq) return c->mbox;
     if ((it & 1023) == 0) {
+      // bounded: a stream that never drains (an error the query does not report) ends the wait
       const hipError_t q = hipStreamQuery(c->stream);
       if (q == hipSuccess) return __atomic_load_n(slot, __ATOMIC_ACQUIRE) == seq ? c->mbox : nullptr;
-      if (q != hipErrorNotReady) {
+      if (q != hipErrorNotReady || t.ms() > 60000.0) {
         err = SQLM_ERR_HIP;
         return nullptr;
       }
@@ -1536,9 +1543,18 @@ int reduce_and_fetch(sqlm_ctx *c, TrialOut &o) {
   return SQLM_OK;
 }
 
+// host trace point i of the current trial: time since the previous point
+inline void hmark(sqlm_ctx *c, int i) {
+  if (!c->htrace) return;
+  const auto now = std::chrono::steady_clock::now();
+  if (i > 0 || c->ht_n > 0) c->ht_acc[i] += std::chrono::duration<double, std::micro>(now - c->ht_prev).count();
+  c->ht_prev = now;
+}
+
 // setLambda + BlockSolver::solve + update + restoreDiagonal + computeActiveErrors.
 int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   DevProblem &d = c->d;
+  hmark(c, 0);  // since the previous trial's scalars arrived: the host's decision
   tmark(c, 2, false);
   launch_damp(d, lambda, c->stream);
   tmark(c, 2, true);
@@ -1546,6 +1562,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   if (c->use_tiles) launch_rcs_tiles(d, lambda, c->tile_max_cp, c->tile_max_k, c->stream, &c->tiles);
   else launch_rcs(d, lambda, c->max_row_blocks, c->stream);
   tmark(c, 3, true);
+  hmark(c, 1);  // damp + tile launches
   tmark(c, 8, false);
   if (c->spec_outstanding) {  // H_pp / b_p (if swapped in) and the trial state buffers it reads
     HIP_OK(hipStreamWaitEvent(c->stream, c->ev_spec_join, 0));
@@ -1563,6 +1580,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
     launch_rcs_reduce(d, lambda, c->stream);
   }
   tmark(c, 8, true);
+  hmark(c, 2);  // RCS reduce
   int s = 0;
   const bool sharded = c->comm.enabled(), root = !sharded || c->comm.rank == 0;
   if (sharded) {  // gather every rank's S / g rows on rank 0
@@ -1593,6 +1611,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
     if (!root) launch_flag_pack(d, true, c->stream);
   }
   tmark(c, 4, true);
+  hmark(c, 3);  // solve launches
   tmark(c, 5, false);
   launch_pose_update(d, lambda, c->stream);
   tmark(c, 5, true);
@@ -1601,6 +1620,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
     launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream, c->spec);
   launch_lidar_chi2(d, c->stream);
   tmark(c, 6, true);
+  hmark(c, 4);  // pose + landmark updates
   if (c->spec) {  // camera pass at the trial state, overlapped with the host's decision and the next trial
     HIP_OK(hipEventRecord(c->ev_spec_fork, c->stream));
     HIP_OK(hipStreamWaitEvent(c->side, c->ev_spec_fork, 0));
@@ -1620,8 +1640,11 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
     c->spec_outstanding = true;
   }
   tmark(c, 7, false);
+  hmark(c, 5);  // speculative camera pass
   s = reduce_and_fetch(c, o);
   tmark(c, 7, true);
+  hmark(c, 6);  // reduce launch + wait for the scalars
+  if (c->htrace) ++c->ht_n;
   acc_events(c, 2, SQLM_NKERNEL_TIMERS);
   return s;
 }
@@ -1739,6 +1762,14 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
     c->spec_outstanding = false;
   }
   flush_cam_timers(c);
+  if (c->htrace && c->ht_n > 0) {
+    static const char *nm[7] = {"decide", "tiles", "reduce", "solve", "updates", "campass", "wait"};
+    std::fprintf(stderr, "host trace (%d trials, us/trial):", c->ht_n);
+    for (int i = 0; i < 7; ++i) std::fprintf(stderr, " %s %.1f", nm[i], c->ht_acc[i] / c->ht_n);
+    std::fprintf(stderr, "\n");
+    std::memset(c->ht_acc, 0, sizeof(c->ht_acc));
+    c->ht_n = 0;
+  }
   st->iterations = its;
   st->result = result;
   st->ms_total = tt.ms();
@@ -1828,6 +1859,7 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   sqlm_ctx *c = new (std::nothrow) sqlm_ctx();
   if (!c) return SQLM_ERR_OOM;
   c->device = dev;
+  c->htrace = std::getenv("SQLM_HOST_TRACE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return SQLM_ERR_HIP; }
   if (hipHostMalloc((void **)&c->h_scalars, sizeof(double) * kNScalars) != hipSuccess) {
     (void)hipStreamDestroy(c->stream);
