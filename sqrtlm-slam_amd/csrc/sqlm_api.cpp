@@ -256,7 +256,7 @@ int upload(sqlm_ctx *c, int idx, const PinVec<T> &v, T **out) {
   return SQLM_OK;
 }
 
-enum PinId { P_OBSLM, P_OBSCAM, P_OBSCAMH, P_OBSUV, P_OBSINFO, P_OBSDELTA, P_OBSUR, P_RQT, P_RX, P_RERR, P_RERR3, P_RLERR };
+enum PinId { P_OBSLM, P_OBSCAM, P_OBSCAMH, P_OBSUV, P_OBSINFO, P_OBSDELTA, P_OBSUR, P_RQT, P_RX, P_RERR, P_RERR3, P_RLERR, P_OBSQ };
 
 enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
@@ -266,7 +266,7 @@ enum BufId {
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
-  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL, B_CAMKEY0, B_CAMKEY1, B_CAMVAL, B_SORTTMP
+  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL, B_CAMKEY0, B_CAMKEY1, B_CAMVAL, B_SORTTMP, B_OBSQ, B_CAMQ
 };
 
 // Persistent host worker pool for the setup passes (a prepare() runs ~20
@@ -624,6 +624,30 @@ void build_tiles_finish(int nP, const std::vector<int> &s_row, const std::vector
 // that can hold it: per level, the odd superblocks whose right-hand side is
 // nonzero form Z = Linv G, the even ones next to them take the update.
 // Returns false when S should go to the dense solver (border too large).
+// Superblock width of a band-only S. Any B > bandwidth keeps S
+// block-tridiagonal; a wider superblock means fewer cyclic-reduction levels and
+// a longer factor chain per level. On small systems (a few superblocks) every
+// level is latency -- a factor launch whose diagonal chain grows with n / 16,
+// an update and a back-substitution launch -- so the estimate below (us per
+// launch, measured: tools/cr_bench and the local-BA solve trace,
+// profiles/r03/solve_trace_lba.txt) picks the cheapest B, ties to the
+// narrowest. Larger systems keep B = bandwidth + 1 (their first levels are
+// throughput-bound). SQLM_CR_B_MIN=1: always the narrowest (A/B only).
+int cr_superblock_width(int bmin, int nband) {
+  const bool keep = std::getenv("SQLM_CR_B_MIN") != nullptr;  // read per plan: tests switch it
+  auto cost = [&](int B) {
+    const int nt = (6 * B + 15) / 16, p = (nband + B - 1) / B;
+    int L = 0;
+    while ((1 << L) < p) ++L;
+    return (L + 1) * (2.0 + 2.6 * nt) + L * 5.5 + (L + 1) * 5.0;
+  };
+  if (keep || bmin <= 0 || (nband + bmin - 1) / bmin > 16) return bmin;
+  int best = bmin;
+  for (int B = bmin + 1; 6 * B <= kCRMaxN && B <= nband; ++B)
+    if (cost(B) < cost(best) - 1e-9) best = B;
+  return best;
+}
+
 bool plan_rcs(int nP, const std::vector<int> &s_row, const std::vector<int> &s_col, CRPlan &pl,
               std::vector<int> &cam_pos) {
   pl = CRPlan{};
@@ -671,7 +695,8 @@ bool plan_rcs(int nP, const std::vector<int> &s_row, const std::vector<int> &s_c
   for (int i = 0; i < nP; ++i)
     for (int k = s_row[i]; k < s_row[i + 1]; ++k)
       if (cam_pos[i] >= 0 && cam_pos[s_col[k]] >= 0) bw = std::max(bw, cam_pos[s_col[k]] - cam_pos[i]);
-  const int B = std::min(bw + 1, std::max(nband, 1));
+  int B = std::min(bw + 1, std::max(nband, 1));
+  if (nbc == 0) B = cr_superblock_width(B, nband);
   const int n = (6 * B + 15) / 16 * 16;
   if (n > kCRMaxN) return false;
   pl.enabled = true;
@@ -878,11 +903,11 @@ int prepare(sqlm_ctx *c, int level) {
   c->dev_edge.assign(nE, 0);
   PinVec<int> obs_lm, obs_cam, obs_camh;
   PinVec<double> obs_uv, obs_info, obs_delta, obs_ur;
+  PinVec<float> obs_q;  // u v info delta as float32, exact when obs_f32 (below)
   {
     int e = 0;
     if ((e = pinned(c, P_OBSLM, nE, obs_lm)) || (e = pinned(c, P_OBSCAM, nE, obs_cam)) ||
-        (e = pinned(c, P_OBSCAMH, nE, obs_camh)) || (e = pinned(c, P_OBSUV, 2 * nE, obs_uv)) ||
-        (e = pinned(c, P_OBSINFO, nE, obs_info)) || (e = pinned(c, P_OBSDELTA, nE, obs_delta)) ||
+        (e = pinned(c, P_OBSCAMH, nE, obs_camh)) || (e = pinned(c, P_OBSQ, 4 * nE, obs_q)) ||
         (e = pinned(c, P_OBSUR, c->has_stereo ? nE : 0, obs_ur)))
       return e;
   }
@@ -892,6 +917,7 @@ int prepare(sqlm_ctx *c, int level) {
   // kept), then every chunk scatters its edges; the camera CSR likewise.
   const int nth = host_threads(c->n_obs);
   auto par = [&](auto &&fn) { run_threads(nth, fn); };
+  std::vector<uint8_t> inexact(nth, 0);
   {
     auto ebeg = [&](int t) { return c->n_obs * t / nth; };
     std::vector<std::vector<int>> &base = c->scat_base;
@@ -911,6 +937,7 @@ int prepare(sqlm_ctx *c, int level) {
     });
     par([&](int t) {
       std::vector<int> &fill = base[t];
+      bool bad = false;
       for (int64_t e = ebeg(t); e < ebeg(t + 1); ++e) {
         if (c->obs_level[e] != level) continue;
         const int sl = pt_slot[c->obs_pt[e]];
@@ -919,11 +946,32 @@ int prepare(sqlm_ctx *c, int level) {
         obs_lm[o] = sl;
         obs_cam[o] = c->obs_pose[e];
         obs_camh[o] = phidx[c->obs_pose[e]];
-        obs_uv[2 * o] = c->obs_uv[2 * e];
-        obs_uv[2 * o + 1] = c->obs_uv[2 * e + 1];
-        obs_info[o] = c->obs_info[e];
-        obs_delta[o] = c->obs_delta[e];
+        const double u = c->obs_uv[2 * e], v = c->obs_uv[2 * e + 1], w = c->obs_info[e], dl = c->obs_delta[e];
+        const float fu = (float)u, fv = (float)v, fw = (float)w, fd = (float)dl;
+        obs_q[4 * (size_t)o] = fu;
+        obs_q[4 * (size_t)o + 1] = fv;
+        obs_q[4 * (size_t)o + 2] = fw;
+        obs_q[4 * (size_t)o + 3] = fd;
+        bad |= (double)fu != u || (double)fv != v || (double)fw != w || (double)fd != dl;
         if (c->has_stereo) obs_ur[o] = c->obs_ur[e];
+      }
+      inexact[t] = bad;
+    });
+  }
+  // inputs that are not all float32 values: the double arrays, from the same slot order
+  const bool obs_f32 = std::find(inexact.begin(), inexact.end(), 1) == inexact.end();
+  if (!obs_f32) {
+    int e = 0;
+    if ((e = pinned(c, P_OBSUV, 2 * nE, obs_uv)) || (e = pinned(c, P_OBSINFO, nE, obs_info)) ||
+        (e = pinned(c, P_OBSDELTA, nE, obs_delta)))
+      return e;
+    par([&](int t) {
+      for (int64_t o = nE * t / nth; o < nE * (t + 1) / nth; ++o) {
+        const int64_t ed = c->dev_edge[o];
+        obs_uv[2 * o] = c->obs_uv[2 * ed];
+        obs_uv[2 * o + 1] = c->obs_uv[2 * ed + 1];
+        obs_info[o] = c->obs_info[ed];
+        obs_delta[o] = c->obs_delta[ed];
       }
     });
   }
@@ -966,9 +1014,18 @@ int prepare(sqlm_ctx *c, int level) {
   {  // the observation arrays go to the device now, overlapped with the rest of the setup
     int e = 0;
     if ((e = upload(c, B_OBSLM, obs_lm, &d.obs_lm)) || (e = upload(c, B_OBSCAM, obs_cam, &d.obs_cam)) ||
-        (e = upload(c, B_OBSCAMH, obs_camh, &d.obs_camh)) || (e = upload(c, B_OBSUV, obs_uv, &d.obs_uv)) ||
-        (e = upload(c, B_OBSINFO, obs_info, &d.obs_info)) || (e = upload(c, B_OBSDELTA, obs_delta, &d.obs_delta)))
+        (e = upload(c, B_OBSCAMH, obs_camh, &d.obs_camh)))
       return e;
+    d.obs_f32 = obs_f32 ? 1 : 0;
+    if (obs_f32) {
+      if ((e = upload(c, B_OBSQ, obs_q, &d.obs_q))) return e;
+      d.obs_uv = d.obs_info = d.obs_delta = nullptr;
+    } else {
+      if ((e = upload(c, B_OBSUV, obs_uv, &d.obs_uv)) || (e = upload(c, B_OBSINFO, obs_info, &d.obs_info)) ||
+          (e = upload(c, B_OBSDELTA, obs_delta, &d.obs_delta)))
+        return e;
+      d.obs_q = nullptr;
+    }
     if (c->has_stereo && (e = upload(c, B_OBSUR, obs_ur, &d.obs_ur))) return e;
     (void)hipStreamQuery(c->stream);  // submit now: the runtime would otherwise batch them until the next sync
   }
@@ -1234,7 +1291,13 @@ int prepare(sqlm_ctx *c, int level) {
   // camera-ordered copies of the camera pass inputs (one coalesced stream +
   // the X gather), gathered on the device from the slot-ordered arrays
   AL(B_CAMSLOT, (size_t)n_cam_obs, d.cam_slot);
-  AL(B_CAMUV, 4 * (size_t)n_cam_obs, d.cam_uv);
+  if (d.obs_f32) {
+    AL(B_CAMQ, 4 * (size_t)n_cam_obs, d.cam_q);
+    d.cam_uv = nullptr;
+  } else {
+    AL(B_CAMUV, 4 * (size_t)n_cam_obs, d.cam_uv);
+    d.cam_q = nullptr;
+  }
   launch_cam_gather(d, n_cam_obs, c->stream);
   AL(B_HPP, 36 * (size_t)nP, d.Hpp);
   AL(B_BP, 8 * (size_t)nP, d.bp);
@@ -1601,8 +1664,10 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
     if (root) launch_gather_add(d, c->gather, c->stream);
   }
   tmark(c, 4, false);
+  // unsharded CR: the pose update reads dx off the CR solution (no gather launch)
+  const bool pose_from_cr = !sharded && c->cr.enabled;
   if (root) {
-    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream) : launch_dense_solve(d, c->stream);
+    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream, !pose_from_cr) : launch_dense_solve(d, c->stream);
     if (s) return s == -2 ? SQLM_ERR_HIP : SQLM_ERR_UNSUPPORTED;
   }
   if (sharded) {  // dx and the solve flag from rank 0
@@ -1613,7 +1678,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   tmark(c, 4, true);
   hmark(c, 3);  // solve launches
   tmark(c, 5, false);
-  launch_pose_update(d, lambda, c->stream);
+  launch_pose_update(d, lambda, c->stream, pose_from_cr);
   tmark(c, 5, true);
   tmark(c, 6, false);
   for (size_t b = 0; b < c->buckets.size(); ++b)

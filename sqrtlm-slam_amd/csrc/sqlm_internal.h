@@ -53,6 +53,13 @@ struct DevProblem {
   double *obs_uv = nullptr;                 // [nE][2]
   double *obs_info = nullptr;               // [nE]
   double *obs_delta = nullptr;              // [nE] Huber delta, 0 = none
+  // obs_f32: every u, v, info and delta of the problem is a float32 value (the
+  // reference's inputs are: kpUn.pt, mvInvLevelSigma2, the Huber thresholds),
+  // so they travel as one float4 per edge (u v info delta, 16 B instead of 32 B
+  // in three loads) and widen to the same doubles; obs_uv / info / delta null
+  int obs_f32 = 0;
+  float *obs_q = nullptr;                   // [nE][4] (obs_f32)
+  float *cam_q = nullptr;                   // [cam_obs][4] camera order (obs_f32)
   double *obs_s = nullptr;                  // [nE] sqrt(rho' info) at the linearization point
   double *obs_P = nullptr;                  // [18][nE] H_lp blocks, SoA: row-kernel fallback only (else null)
   double *obs_err = nullptr;                // [nE][2] last computed error (g2o _error)
@@ -252,7 +259,7 @@ int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase co
 #endif
 constexpr int kRedLong = 24;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st);  // zeroes + scatters unless cr_direct
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather = true);  // zeroes + scatters unless cr_direct
 // band + border layout: clear F^T / the border system before S is assembled into it
 void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st);
 // CR levels + top + back substitution on blocks already in CR layout (microbench / tests)
@@ -275,7 +282,9 @@ int launch_cr_multi(double *D, double *L, double *E, double *A, double *C, doubl
                     double *X, int *flags, int p, int n, int R, hipStream_t st);
 // P_I = A_I^T B_I for I < p, A_I / B_I [n][R] row-major, P_I [R][R] (R % 16 == 0).
 int launch_batched_atb(const double *A, const double *B, double *P, int p, int n, int R, hipStream_t st);
-void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st);
+// from_cr: dx taken from the cyclic-reduction solution (launch_cr_solve with
+// gather = false), written to d.dx on the way
+void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool from_cr = false);
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st,
                             bool spec = false);
 void launch_lidar_chi2(const DevProblem &d, hipStream_t st);

@@ -265,11 +265,19 @@ __device__ __forceinline__ ObsIn load_obs(const DevProblem &d, int e, bool ok) {
   if (ok) {
     o.cam = d.obs_cam[e];
     o.camh = d.obs_camh[e];
-    const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
-    o.u = uv.x;
-    o.v = uv.y;
-    o.info = d.obs_info[e];
-    o.delta = d.obs_delta[e];
+    if (d.obs_f32) {
+      const float4 q = *reinterpret_cast<const float4 *>(d.obs_q + 4 * (int64_t)e);
+      o.u = q.x;
+      o.v = q.y;
+      o.info = q.z;
+      o.delta = q.w;
+    } else {
+      const double2 uv = *reinterpret_cast<const double2 *>(d.obs_uv + 2 * e);
+      o.u = uv.x;
+      o.v = uv.y;
+      o.info = d.obs_info[e];
+      o.delta = d.obs_delta[e];
+    }
     if (ST) o.ur = d.obs_ur[e];
     if (WANT_S) o.s = d.obs_s[e];
   }
@@ -502,8 +510,15 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
     const double bf = ST ? d.pose_bf[d.hidx_pose[i]] : 0.0;
     for (int t = d.cam_obs_ptr[i] + lane; t < d.cam_obs_ptr[i + 1]; t += 64) {
       const double *X = d.X[sb] + 4 * d.cam_slot[t];
-      const double2 uv = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t);
-      const double2 id = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t + 2);
+      double2 uv, id;
+      if (d.obs_f32) {
+        const float4 q = *reinterpret_cast<const float4 *>(d.cam_q + 4 * (int64_t)t);
+        uv = make_double2(q.x, q.y);
+        id = make_double2(q.z, q.w);
+      } else {
+        uv = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t);
+        id = *reinterpret_cast<const double2 *>(d.cam_uv + 4 * t + 2);
+      }
       const double ur = ST ? d.cam_ur[t] : -1.0;
       const bool st = ST && ur >= 0.0;
       MonoEval m;
@@ -607,11 +622,15 @@ __global__ __launch_bounds__(256) void k_cam_gather(DevProblem d, int64_t n) {
   if (t >= n) return;
   const int o = d.cam_obs[t];
   d.cam_slot[t] = d.obs_lm[o];
-  double *u = d.cam_uv + 4 * t;
-  u[0] = d.obs_uv[2 * (int64_t)o];
-  u[1] = d.obs_uv[2 * (int64_t)o + 1];
-  u[2] = d.obs_info[o];
-  u[3] = d.obs_delta[o];
+  if (d.obs_f32) {
+    *reinterpret_cast<float4 *>(d.cam_q + 4 * t) = *reinterpret_cast<const float4 *>(d.obs_q + 4 * (int64_t)o);
+  } else {
+    double *u = d.cam_uv + 4 * t;
+    u[0] = d.obs_uv[2 * (int64_t)o];
+    u[1] = d.obs_uv[2 * (int64_t)o + 1];
+    u[2] = d.obs_info[o];
+    u[3] = d.obs_delta[o];
+  }
   if (d.cam_ur) d.cam_ur[t] = d.obs_ur[o];
 }
 
@@ -1436,6 +1455,10 @@ int launch_dense_solve(const DevProblem &d, hipStream_t st) {
 
 // ---------------------------------------------------------------- updates
 
+// CR: the pose's dx is read from the cyclic-reduction solution (band position
+// or border slot; 0 if the solve flagged a non-positive pivot) and written to
+// dx for the landmark update -- the k_cr_gather step folded into this launch.
+template <bool CR>
 __global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda) {
   __shared__ double red[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1445,8 +1468,21 @@ __global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda
     double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t[3] = {qt[4], qt[5], qt[6]};
     const int h = d.pose_hidx[p];
     if (h >= 0) {
-      const double *dx = d.dx + 6 * h;
-      const double dd[6] = {dx[0], dx[1], dx[2], dx[3], dx[4], dx[5]};
+      double dd[6];
+      if (CR) {
+        const int pi = d.cam_pos ? d.cam_pos[h] : h;
+        const double *x = pi >= 0 ? d.cr_x + (size_t)(pi / d.cr_B) * d.cr_n + 6 * (pi % d.cr_B)
+                                  : d.bd_x + 6 * (-1 - pi);
+        const bool ok = d.flags[0] != 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dd[k] = ok ? x[k] : 0.0;
+        double *dx = d.dx + 6 * h;
+        store2(dx, dd[0], dd[1]); store2(dx + 2, dd[2], dd[3]); store2(dx + 4, dd[4], dd[5]);
+      } else {
+        const double *dx = d.dx + 6 * h;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dd[k] = dx[k];
+      }
       se3_oplus(q, t, dd);
       // computeScale dx^T (lambda dx + b): sharded, b_p is summed over ranks and lambda counted once
       const double lam = (!d.sharded || d.rank == 0) ? lambda : 0.0;
@@ -1466,9 +1502,12 @@ __global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda
   if (threadIdx.x == 0) d.partials[kPartScaleCam + blockIdx.x] = s;
 }
 
-void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st) {
+void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool from_cr) {
   if (d.n_pose == 0) return;
-  hipLaunchKernelGGL(k_pose_update, dim3((d.n_pose + 255) / 256), dim3(256), 0, st, d, lambda);
+  if (from_cr)
+    hipLaunchKernelGGL(k_pose_update<true>, dim3((d.n_pose + 255) / 256), dim3(256), 0, st, d, lambda);
+  else
+    hipLaunchKernelGGL(k_pose_update<false>, dim3((d.n_pose + 255) / 256), dim3(256), 0, st, d, lambda);
 }
 
 // Back-substitution dl = M (b_l - sum_i H_lp,i dx_i), X' = X + dl, then the

@@ -1698,7 +1698,7 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
   }
 }
 
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather) {
   CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
   if (!d.cr_direct) {  // BSR S (sharded runs / row-kernel RCS): zero the superblocks and scatter
     const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
@@ -1709,7 +1709,7 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st) {
   }
   if (pl.R) launch_arrow_solve(d, pl, st);
   else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
-  hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
+  if (gather) hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }
 

@@ -50,17 +50,25 @@ def test_optimize_local_window(gpu_ctx, oracle, seed):
 
 
 @pytest.mark.parametrize("n_pose", [9, 16, 28, 43, 48])
-def test_small_rcs_superblock_counts(gpu_ctx, oracle, n_pose):
+@pytest.mark.parametrize("b_min", [True, False])
+def test_small_rcs_superblock_counts(gpu_ctx, oracle, n_pose, b_min, monkeypatch):
     """Local-BA-sized reduced camera systems of 2, 3, 5, 8 and 9 superblocks
     (cyclic reduction with 1..4 levels, odd and even counts) against the
-    oracle's Cholesky (linear_solver_eigen.h:94-124)."""
+    oracle's Cholesky (linear_solver_eigen.h:94-124). b_min: superblocks of
+    bandwidth + 1 cameras (SQLM_CR_B_MIN, the level counts above); otherwise
+    the width the planner's latency estimate picks (fewer, wider superblocks,
+    down to a single one)."""
+    if b_min:
+        monkeypatch.setenv("SQLM_CR_B_MIN", "1")
+    else:
+        monkeypatch.delenv("SQLM_CR_B_MIN", raising=False)
     prob = synth.make_problem(n_pose, 50 * n_pose, pair_window=4, n_fixed=3, seed=100 + n_pose, robust=True)
     ref = oracle.OracleGraph(prob)
     nr, sr = ref.optimize(0, 10)
     gpu_ctx.set_problem(prob)
     ng, sg = gpu_ctx.optimize(0, 10)
     lay = gpu_ctx.rcs_layout()
-    assert lay["kind"] == "band" and lay["p"] >= 2
+    assert lay["kind"] == "band" and (lay["p"] >= 2 or not b_min)
     print(f"n_pose {n_pose}: {lay['p']} superblocks of {lay['B']} cameras")
     assert ng == nr
     _compare_stats(sg, sr)
