@@ -1522,7 +1522,7 @@ constexpr int kUpdWin = 64;
 #define SQLM_UPD_OCC 1
 #endif
 template <int W, bool ST, bool SPEC>
-__global__ __launch_bounds__(256, SQLM_UPD_OCC) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
+__global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : 4) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
                                                          double lambda, int part_off, const int2 *rng) {
   __shared__ double red[4];
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
