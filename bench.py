@@ -65,24 +65,26 @@ def make_workload(name: str, scale: float):
 
 def algorithmic_bytes_linearize(p) -> float:
     """Bytes k_linearize must move per launch: per observation
-    it reads cam id, free-camera id, uv, info, delta (40 B) and writes the
+    it reads cam id, free-camera id and u v info delta as one float32 float4
+    (24 B; DevProblem::obs_f32) and writes the
     error (16 B) and the weight sqrt(rho' info) (8 B) from which the consumers
     recompute the H_lp blocks; per landmark it reads X (24 B) + offset (4 B)
     and writes the QR factor R (48 B) + b_l (24 B). Pose reads (<1 MB,
     L2-resident) excluded."""
     E, L = p.n_obs, p.n_pt
-    return E * (40 + 16 + 8) + L * (24 + 4 + 48 + 24)
+    return E * (24 + 16 + 8) + L * (24 + 4 + 48 + 24)
 
 
 def algorithmic_bytes_update(p) -> float:
     """Bytes k_landmark_update<SPEC> must move per trial (DESIGN.md §2 steps
-    6-7): per observation it reads cam id, free-camera id, uv, info, delta and
-    the linearization-point weight s (48 B) and writes the trial error (16 B)
+    6-7): per observation it reads cam id, free-camera id, u v info delta (one
+    float4: the inputs are float32 values, DevProblem::obs_f32) and the
+    linearization-point weight s (32 B) and writes the trial error (16 B)
     and the trial-state weight (8 B); per landmark it reads the offset, X, R
     and b_l (100 B) and writes X' and the trial-state R, b_l (96 B). Pose and
     dx reads (<1 MB, L2-resident) excluded."""
     E, L = p.n_obs, p.n_pt
-    return E * (48 + 16 + 8) + L * (100 + 96)
+    return E * (32 + 16 + 8) + L * (100 + 96)
 
 
 def algorithmic_flops_rcs(p) -> float:

@@ -1681,6 +1681,8 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   launch_pose_update(d, lambda, c->stream, pose_from_cr);
   tmark(c, 5, true);
   tmark(c, 6, false);
+  // (the buckets on three streams, like the tile classes, measured slower:
+  // 686 -> 647 it/s, the CR solve after them 0.54 -> 0.61 ms; profiles/r03/ab_upd_streams.log)
   for (size_t b = 0; b < c->buckets.size(); ++b)
     launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream, c->spec);
   launch_lidar_chi2(d, c->stream);

@@ -406,13 +406,18 @@ __device__ __forceinline__ void lin_butterfly(int lane, double R[6], double &b0,
 
 // ---------------------------------------------------------------- linearize
 
-constexpr int kMaxGrid = 2048;
+// per-landmark kernels: at most this many blocks per bucket launch (grid-stride
+// beyond); SQLM_UPD_GRID overrides it for A/B runs (read once per process)
+static int max_grid() {
+  static const int g = std::getenv("SQLM_UPD_GRID") ? std::max(256, std::min(4096, std::atoi(std::getenv("SQLM_UPD_GRID")))) : 2048;
+  return g;
+}
 
 int linearize_blocks(const Bucket &b) {
   const int nseg = b.slot_end - b.slot_begin;
   const int segs_per_block = kBlock / b.W;
   int tiles = (nseg + segs_per_block - 1) / segs_per_block;
-  return tiles < kMaxGrid ? tiles : kMaxGrid;
+  return tiles < max_grid() ? tiles : max_grid();
 }
 
 // One landmark per W-lane segment. Each lane folds its observations' two
@@ -1365,7 +1370,9 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     // one round of long-running workgroups) then 4 on the second
     int ncls = 0;
     for (int k = 0; k <= kTileNtMax; ++k) ncls += d.tile_cls_cnt[k] > 0;
-    const bool par = ts && ts->s[0] && ts->s[1] && ncls > 1;  // one class (small windows): no fork / join
+    // one class (small windows): no fork / join; SQLM_TILE_SERIAL=1: one stream (A/B only)
+    static const bool serial = std::getenv("SQLM_TILE_SERIAL") != nullptr;
+    const bool par = ts && ts->s[0] && ts->s[1] && ncls > 1 && !serial;
     if (par) {
       (void)hipEventRecord(ts->fork, st);
       (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
