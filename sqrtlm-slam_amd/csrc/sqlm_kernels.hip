@@ -1302,6 +1302,24 @@ __device__ __forceinline__ double red_sum(const double *src, const int64_t *off,
   return v;
 }
 
+// the same sum for the entry pair (e, e + 1), e even: one 16-byte load per
+// contribution (every contribution starts at a multiple of 36 doubles)
+__device__ __forceinline__ double2 red_sum2(const double *src, const int64_t *off, int k0, int k1, int e) {
+  double2 v = make_double2(0.0, 0.0);
+  for (int k = k0; k < k1; k += 8) {
+    double2 p8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      p8[u] = k + u < k1 ? *reinterpret_cast<const double2 *>(src + off[k + u] + e) : make_double2(0.0, 0.0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      v.x += p8[u].x;
+      v.y += p8[u].y;
+    }
+  }
+  return v;
+}
+
 constexpr int kRedThreads = 256;
 constexpr int kRedGroupsS = kRedThreads / 36, kRedGroupsG = kRedThreads / 6;
 
@@ -1333,12 +1351,16 @@ __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double
     return;
   }
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid < d.nnzb * 36) {
-    const int s = (int)(gid / 36), e = (int)(gid % 36);
+  if (gid < d.nnzb * 18) {  // entry pairs (e, e + 1) of a row of the 6x6 block
+    const int s = (int)(gid / 18), e = 2 * (int)(gid % 18);
     const int k0 = d.red_ptr[s], k1 = d.red_ptr[s + 1];
-    if (k1 - k0 <= kRedLong) rcs_put_s(d, s, e, red_sum(d.part, d.red_off, k0, k1, 1, e), lambda);
+    if (k1 - k0 <= kRedLong) {
+      const double2 v = red_sum2(d.part, d.red_off, k0, k1, e);
+      rcs_put_s(d, s, e, v.x, lambda);
+      rcs_put_s(d, s, e + 1, v.y, lambda);
+    }
   }
-  const int64_t g2 = gid - d.nnzb * 36;
+  const int64_t g2 = gid - d.nnzb * 18;
   if (g2 >= 0 && g2 < (int64_t)d.nP * 6) {
     const int i = (int)(g2 / 6), r = (int)(g2 % 6);
     const int k0 = d.gred_ptr[i], k1 = d.gred_ptr[i + 1];
@@ -1410,7 +1432,7 @@ int tile_profile_read(long long *out) {
 
 void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st) {
   if (d.nP == 0) return;
-  const int64_t items = d.nnzb * 36 + (int64_t)d.nP * 6 + (d.cr_direct ? (int64_t)d.cr_p * d.cr_n : 0);
+  const int64_t items = d.nnzb * 18 + (int64_t)d.nP * 6 + (d.cr_direct ? (int64_t)d.cr_p * d.cr_n : 0);
   const int short_blocks = (int)((items + kRedThreads - 1) / kRedThreads);
   hipLaunchKernelGGL(k_rcs_reduce, dim3((unsigned)(short_blocks + d.n_long_s + d.n_long_g)), dim3(kRedThreads), 0, st,
                      d, lambda, short_blocks);
