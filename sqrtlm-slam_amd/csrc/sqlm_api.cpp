@@ -174,6 +174,7 @@ struct sqlm_ctx {
   bool spec = false;
   bool lin_valid = false;          // the current buffers hold the linearization at the current state
   bool spec_outstanding = false;   // a speculative camera pass may still run on the side stream
+  bool cam_inline = false;         // small problem: the speculative camera pass on the context stream
   hipEvent_t ev_spec_fork = nullptr, ev_spec_join = nullptr;
   TileStreams tiles;  // RCS tile classes run on stream + these two
   hipEvent_t ev_cam[2][2] = {};    // timing of the speculative camera passes (ping-pong)
@@ -1304,6 +1305,12 @@ int prepare(sqlm_ctx *c, int level) {
   {
     const bool no_spec = getenv("SQLM_NO_SPEC") && atoi(getenv("SQLM_NO_SPEC")) != 0;
     c->spec = c->use_tiles && d.obs_P == nullptr && !no_spec;
+    // the side stream's fork / join (two event records, two waits: ~20 us of
+    // host API time per trial) pays only when the pass is long enough to hide;
+    // SQLM_CAM_INLINE=0/1 overrides (A/B)
+    const char *ci = std::getenv("SQLM_CAM_INLINE");
+    c->cam_inline = ci ? std::atoi(ci) != 0 : d.nE < (1 << 18);
+    if (sharded) c->cam_inline = false;
   }
   c->lin_valid = false;
   d.pc_lm = kPartChiCurLm;
@@ -1579,13 +1586,36 @@ const double *mbox_wait(sqlm_ctx *c, unsigned long long seq, int &err) {
   }
 }
 
-int reduce_and_fetch(sqlm_ctx *c, TrialOut &o) {
+// The speculative camera pass (H_pp / b_p at the trial state) on stream st,
+// with its HIP-event timing in the timing run.
+int spec_camera_pass(sqlm_ctx *c, hipStream_t st) {
+  const int p = c->cam_par;
+  if (c->timing && c->cam_pending[p]) {  // the pass two trials back is long complete
+    float ms = 0.f;
+    if (hipEventSynchronize(c->ev_cam[p][1]) == hipSuccess &&
+        hipEventElapsedTime(&ms, c->ev_cam[p][0], c->ev_cam[p][1]) == hipSuccess)
+      c->kernel_ms_acc[1] += ms;
+    c->cam_pending[p] = false;
+  }
+  if (c->timing) HIP_OK(hipEventRecord(c->ev_cam[p][0], st));
+  launch_camera_pass(c->d, st, true);
+  if (c->timing) { HIP_OK(hipEventRecord(c->ev_cam[p][1], st)); c->cam_pending[p] = true; }
+  c->cam_par ^= 1;
+  return SQLM_OK;
+}
+
+// cam_after: the speculative camera pass goes on the context stream right
+// behind k_reduce (it runs while the host waits for the scalars and decides)
+int reduce_and_fetch(sqlm_ctx *c, TrialOut &o, bool cam_after = false) {
   DevProblem &d = c->d;
   static const bool no_mbox = std::getenv("SQLM_NO_MBOX") != nullptr;
   const bool mb = c->mbox && !no_mbox && !c->timing && !c->comm.enabled();
   const unsigned long long seq = mb ? ++c->mbox_seq : 0;
   launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream,
                 mb ? c->mbox_dev : nullptr, seq);
+  if (cam_after) {
+    if (int e = spec_camera_pass(c, c->stream)) return e;
+  }
   int s = comm_allreduce_scalars(c->comm, d.scalars, c->need_maxdiag, c->stream);
   if (s) return s;
   const double *h = nullptr;
@@ -1688,27 +1718,26 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   launch_lidar_chi2(d, c->stream);
   tmark(c, 6, true);
   hmark(c, 4);  // pose + landmark updates
-  if (c->spec) {  // camera pass at the trial state, overlapped with the host's decision and the next trial
-    HIP_OK(hipEventRecord(c->ev_spec_fork, c->stream));
-    HIP_OK(hipStreamWaitEvent(c->side, c->ev_spec_fork, 0));
-    const int p = c->cam_par;
-    if (c->timing && c->cam_pending[p]) {  // the pass two trials back is long complete
-      float ms = 0.f;
-      if (hipEventSynchronize(c->ev_cam[p][1]) == hipSuccess &&
-          hipEventElapsedTime(&ms, c->ev_cam[p][0], c->ev_cam[p][1]) == hipSuccess)
-        c->kernel_ms_acc[1] += ms;
-      c->cam_pending[p] = false;
+  // camera pass at the trial state: on the side stream, overlapped with the
+  // host's decision and the next trial; small problems (cam_inline) keep it on
+  // the context stream behind k_reduce instead -- the fork / join costs the
+  // host more than the overlap saves there
+  const bool cam_after = c->spec && c->cam_inline && !c->timing;
+  if (c->spec && !cam_after) {
+    if (!c->cam_inline) {
+      HIP_OK(hipEventRecord(c->ev_spec_fork, c->stream));
+      HIP_OK(hipStreamWaitEvent(c->side, c->ev_spec_fork, 0));
     }
-    if (c->timing) HIP_OK(hipEventRecord(c->ev_cam[p][0], c->side));
-    launch_camera_pass(d, c->side, true);
-    if (c->timing) { HIP_OK(hipEventRecord(c->ev_cam[p][1], c->side)); c->cam_pending[p] = true; }
-    c->cam_par ^= 1;
-    HIP_OK(hipEventRecord(c->ev_spec_join, c->side));
-    c->spec_outstanding = true;
+    s = spec_camera_pass(c, c->cam_inline ? c->stream : c->side);
+    if (s) return s;
+    if (!c->cam_inline) {
+      HIP_OK(hipEventRecord(c->ev_spec_join, c->side));
+      c->spec_outstanding = true;
+    }
   }
   tmark(c, 7, false);
   hmark(c, 5);  // speculative camera pass
-  s = reduce_and_fetch(c, o);
+  s = reduce_and_fetch(c, o, cam_after);
   tmark(c, 7, true);
   hmark(c, 6);  // reduce launch + wait for the scalars
   if (c->htrace) ++c->ht_n;

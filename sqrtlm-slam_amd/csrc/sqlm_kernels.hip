@@ -1302,25 +1302,42 @@ __device__ __forceinline__ double red_sum(const double *src, const int64_t *off,
   return v;
 }
 
-// the same sum for the entry pair (e, e + 1), e even: one 16-byte load per
-// contribution (every contribution starts at a multiple of 36 doubles)
-__device__ __forceinline__ double2 red_sum2(const double *src, const int64_t *off, int k0, int k1, int e) {
-  double2 v = make_double2(0.0, 0.0);
+// the same sum for the entries e .. e + V - 1 (V = 2 or 4, e a multiple of V):
+// 16-byte loads per contribution (every contribution starts at a multiple of 36 doubles)
+template <int V>
+__device__ __forceinline__ void red_sumv(const double *src, const int64_t *off, int k0, int k1, int e, double *v) {
+#pragma unroll
+  for (int j = 0; j < V; ++j) v[j] = 0.0;
   for (int k = k0; k < k1; k += 8) {
-    double2 p8[8];
+    double2 p8[8][V / 2];
 #pragma unroll
     for (int u = 0; u < 8; ++u)
-      p8[u] = k + u < k1 ? *reinterpret_cast<const double2 *>(src + off[k + u] + e) : make_double2(0.0, 0.0);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      v.x += p8[u].x;
-      v.y += p8[u].y;
-    }
+      for (int j = 0; j < V / 2; ++j)
+        p8[u][j] = k + u < k1 ? *reinterpret_cast<const double2 *>(src + off[k + u] + e + 2 * j) : make_double2(0.0, 0.0);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int j = 0; j < V / 2; ++j) {
+        v[2 * j] += p8[u][j].x;
+        v[2 * j + 1] += p8[u][j].y;
+      }
   }
-  return v;
 }
 
-constexpr int kRedThreads = 256;
+// S entries per thread of k_rcs_reduce (2 or 4; A/B: -DSQLM_RED_V=4)
+#ifndef SQLM_RED_V
+#define SQLM_RED_V 2
+#endif
+constexpr int kRedV = SQLM_RED_V, kRedPer = 36 / kRedV;
+
+// threads per k_rcs_reduce workgroup: a long list (the cameras of a loop
+// closure, every block of a small local-BA system) is summed by kRedThreads / 36
+// groups, so the width sets that critical path (A/B: -DSQLM_RED_THREADS=1024)
+#ifndef SQLM_RED_THREADS
+#define SQLM_RED_THREADS 256
+#endif
+constexpr int kRedThreads = SQLM_RED_THREADS;
 constexpr int kRedGroupsS = kRedThreads / 36, kRedGroupsG = kRedThreads / 6;
 
 __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double lambda, int short_blocks) {
@@ -1351,16 +1368,17 @@ __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double
     return;
   }
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid < d.nnzb * 18) {  // entry pairs (e, e + 1) of a row of the 6x6 block
-    const int s = (int)(gid / 18), e = 2 * (int)(gid % 18);
+  if (gid < d.nnzb * kRedPer) {  // kRedV consecutive entries of the 6x6 block
+    const int s = (int)(gid / kRedPer), e = kRedV * (int)(gid % kRedPer);
     const int k0 = d.red_ptr[s], k1 = d.red_ptr[s + 1];
     if (k1 - k0 <= kRedLong) {
-      const double2 v = red_sum2(d.part, d.red_off, k0, k1, e);
-      rcs_put_s(d, s, e, v.x, lambda);
-      rcs_put_s(d, s, e + 1, v.y, lambda);
+      double v[kRedV];
+      red_sumv<kRedV>(d.part, d.red_off, k0, k1, e, v);
+#pragma unroll
+      for (int j = 0; j < kRedV; ++j) rcs_put_s(d, s, e + j, v[j], lambda);
     }
   }
-  const int64_t g2 = gid - d.nnzb * 18;
+  const int64_t g2 = gid - d.nnzb * kRedPer;
   if (g2 >= 0 && g2 < (int64_t)d.nP * 6) {
     const int i = (int)(g2 / 6), r = (int)(g2 % 6);
     const int k0 = d.gred_ptr[i], k1 = d.gred_ptr[i + 1];
@@ -1432,7 +1450,7 @@ int tile_profile_read(long long *out) {
 
 void launch_rcs_reduce(const DevProblem &d, double lambda, hipStream_t st) {
   if (d.nP == 0) return;
-  const int64_t items = d.nnzb * 18 + (int64_t)d.nP * 6 + (d.cr_direct ? (int64_t)d.cr_p * d.cr_n : 0);
+  const int64_t items = d.nnzb * kRedPer + (int64_t)d.nP * 6 + (d.cr_direct ? (int64_t)d.cr_p * d.cr_n : 0);
   const int short_blocks = (int)((items + kRedThreads - 1) / kRedThreads);
   hipLaunchKernelGGL(k_rcs_reduce, dim3((unsigned)(short_blocks + d.n_long_s + d.n_long_g)), dim3(kRedThreads), 0, st,
                      d, lambda, short_blocks);
