@@ -636,6 +636,10 @@ void build_tiles_finish(int nP, const std::vector<int> &s_row, const std::vector
 // throughput-bound). SQLM_CR_B_MIN=1: always the narrowest (A/B only).
 int cr_superblock_width(int bmin, int nband) {
   const bool keep = std::getenv("SQLM_CR_B_MIN") != nullptr;  // read per plan: tests switch it
+  if (const char *fb = std::getenv("SQLM_CR_B")) {  // a fixed width (A/B of the estimate only)
+    const int b = std::atoi(fb);
+    if (b >= bmin && 6 * b <= kCRMaxN) return std::min(b, std::max(nband, 1));
+  }
   auto cost = [&](int B) {
     const int nt = (6 * B + 15) / 16, p = (nband + B - 1) / B;
     int L = 0;
@@ -1064,7 +1068,9 @@ int prepare(sqlm_ctx *c, int level) {
   // landmarks per tile: up to kTileMaxLm, fewer on small problems so that the
   // tiles still cover every CU twice (a local-BA window of 5k landmarks would
   // otherwise run ~40 long tiles on 256 CUs)
-  const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
+  // (SQLM_TILE_LMDIV=k: nL / k instead of nL / 512, A/B only)
+  static const int lm_div = std::getenv("SQLM_TILE_LMDIV") ? std::max(1, std::atoi(std::getenv("SQLM_TILE_LMDIV"))) : 512;
+  const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / lm_div + 3) & ~3));
   TileBuild &tb = c->tb;
   build_tiles(nP, nL, lm_begin, obs_camh.data(), lm_cap, tp, tb);
   phase("tiles");
