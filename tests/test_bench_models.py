@@ -34,5 +34,11 @@ def test_eg_solve_flops_band_only():
 
 
 def test_update_bytes_model():
+    """56 B per observation (ids 8, float4 inputs 16, s 8 read; error 16, s' 8
+    written) and 196 B per landmark; the generator's inputs are float32 values,
+    so the library takes the float4 path (DevProblem::obs_f32) on them."""
     prob = synth.config4(scale=0.002, seed=4)
-    assert bench.algorithmic_bytes_update(prob) == prob.n_obs * 72 + prob.n_pt * 196
+    assert bench.algorithmic_bytes_update(prob) == prob.n_obs * 56 + prob.n_pt * 196
+    for a in (prob.obs_uv, prob.obs_info):
+        a = np.asarray(a, dtype=np.float64)
+        assert np.array_equal(a.astype(np.float32).astype(np.float64), a)
