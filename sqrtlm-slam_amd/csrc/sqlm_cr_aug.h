@@ -58,6 +58,7 @@ struct Shared {
   double Hp[kMaxNt][256];   // column J's tiles (J-1, J) and (J, J) through step J-3, handed to wave 0
   double Hq[kMaxNt][256];
   int fT[kMaxNt], fU[kPairs], fH[kMaxNt];
+  double by[kCRMaxN], bx[kCRMaxN], br[16];  // BACK: y, x and one block row's right-hand side
 };
 
 // (k, J), k < J < kMaxNt -> 0 .. kPairs-1
@@ -293,11 +294,57 @@ __device__ __forceinline__ bool takes_update(int type, int J, int k, int I) {
 
 }  // namespace aug
 
+// BACK (MODE 1, U layout, one superblock: the top of the cyclic reduction):
+// the g worker goes on to x = U^-1 y with U's tiles and the T_k still in LDS --
+// the arithmetic of k_cr_back_u<true> in the same order (bitwise equal), one
+// launch less per solve. Wave (block row) k's step in k_cr_back_u becomes
+// step k of a loop from the bottom: lane (q, r) sums U_kj[r][4q..4q+3] x_j over
+// j > k (j descending), the quarter sums are added by two xor shuffles, and
+// x_k = T_k^T (y_k - that).
+__device__ __forceinline__ void top_back(aug::Shared &sh, const CRView &v, int I, int nt, const d4 *t, int lane) {
+  using namespace aug;
+  const int n = v.n, q = lane >> 4, r = lane & 15, k4 = lane >> 4;
+#pragma unroll
+  for (int rr = 0; rr < kMaxNt; ++rr)
+    if (rr < nt && r == 0)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sh.by[16 * rr + k4 + 4 * j] = t[rr][j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int i = nt - 1; i >= 0; --i) {
+    double acc = 0.0;
+    for (int j = nt - 1; j > i; --j) {
+      const double *U = sh.U[pair_id(i, j)];  // U_ij[row][col] at [64 (row >> 2) + 16 (row & 3) + col]
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = fma(U[64 * (r >> 2) + 16 * (r & 3) + 4 * q + m], sh.bx[16 * j + 4 * q + m], acc);
+    }
+    acc += __shfl_xor(acc, 16, 64);
+    acc += __shfl_xor(acc, 32, 64);
+    if (q == 0) sh.br[r] = sh.by[16 * i + r] - acc;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double x = 0.0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) x = fma(sh.T[i][(4 * q + m) * kTp + r], sh.br[4 * q + m], x);  // T_i[4q+m][r]
+    x += __shfl_xor(x, 16, 64);
+    x += __shfl_xor(x, 32, 64);
+    if (q == 0) {
+      sh.bx[16 * i + r] = x;
+      v.x[(size_t)I * n + 16 * i + r] = x;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // MODE 0: level step (A_I, C_I, z_I and the back-substitution factor).
 // MODE 1: factor only (z_I and the factor). LINV: the factor is Linv_I
 // (lower, dense tiles); otherwise the upper U tiles with T_k on the diagonal.
 // Superblock I = I0 + stride * (blockIdx.x / split); workgroup sidx = blockIdx.x % split.
-template <int MODE, bool LINV>
+template <int MODE, bool LINV, bool BACK = false>
 __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I0, int stride, int split) {
   using namespace aug;
   extern __shared__ __attribute__((aligned(16))) unsigned char aug_lds[];
@@ -460,6 +507,7 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
         if (c == 0) v.g[(size_t)I * n + 16 * r + k4 + 4 * j] = t[r][j];
     }
   }
+  if (BACK && type == kColG) top_back(sh, v, I, nt, t, lane);
   AUG_PROF(16 + wave);
 }
 

@@ -1665,6 +1665,12 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
   }
 }
 
+// SQLM_CR_TOP_SPLIT=1: the top factor and its back substitution as two launches (A/B)
+static bool top_split() {
+  static const bool v = std::getenv("SQLM_CR_TOP_SPLIT") != nullptr;
+  return v;
+}
+
 // Levels, top solve and back substitution on D/E/g already in CR layout.
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p,
                     int n, hipStream_t st) {
@@ -1685,9 +1691,11 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
   const size_t back_lds = 3 * kCRMaxN * sizeof(double) + aug::kMaxNt * sizeof(int);
   if (cr_legacy()) {
     hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
-  } else {  // x_0 = U_0^-1 z_0
+  } else if (top_split()) {  // x_0 = U_0^-1 z_0 (A/B: factor and back substitution as two launches)
     launch_cr_factor(v, 0, 0, 0, 1, false, st);
     hipLaunchKernelGGL(k_cr_back_u<true>, dim3(1), dim3(64 * nt), back_lds, st, v, 0);
+  } else {  // x_0 = U_0^-1 z_0 by the top factor's workgroup
+    hipLaunchKernelGGL((k_cr_aug<1, false, true>), dim3(1), dim3(aug::kThreads), sizeof(aug::Shared), st, v, 0, 0, 0, 1);
   }
   for (h /= 2; h >= 1; h /= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
