@@ -34,6 +34,11 @@
 #include "sqrtlm_capture.h"
 
 namespace ORB_SLAM2 {
+
+// Defined in src/backend/g2oOptimizer.cc:59-66 (namespace ORB_SLAM2, external
+// linkage) and declared in no reference header.
+PointI PointIRT2PointI(const PointIRT &Pirt);
+
 namespace {
 
 // ---------------------------------------------------------------- context

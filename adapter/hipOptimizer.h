@@ -23,12 +23,16 @@
 #include "Eigen/Core"
 #include "LoopClosing.h"
 
+// global, as in the reference (include/utils/lidarconfig.h:7 declares it
+// outside namespace ORB_SLAM2; a forward declaration inside the namespace
+// would name a different, incomplete type)
+struct lidarConfig;
+
 namespace ORB_SLAM2 {
 
 class KeyFrame;
 class MapPoint;
 class Map;
-struct lidarConfig;
 
 class hipOptimizer {
  public:

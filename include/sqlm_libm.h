@@ -166,7 +166,12 @@ SQLM_LM double sqlm_lm_kcos(double x, double y) {
   return a - (hz - (z * r - x * y));
 }
 
-/* x = n pi/2 + y[0] + y[1], |y| <= pi/4; returns n */
+/* x = n pi/2 + y[0] + y[1], |y| <= pi/4; returns n. fdlibm's medium-range
+   reduction only: exact for |x| <= 2^20 pi/2 (SQLM_LM_PIO2_MAX). Beyond it
+   (fdlibm's Payne-Hanek range) y = NaN: sin / cos return NaN, so a wild LM
+   step (a rotation of more than 1.6e6 rad) yields a NaN chi2 and is rejected
+   cleanly instead of meeting the undefined int conversion below. */
+#define SQLM_LM_PIO2_MAX 0x413921fb
 SQLM_LM int sqlm_lm_rem_pio2(double x, double *y) {
   SQLM_LM_NOCONTRACT
   const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
@@ -177,6 +182,10 @@ SQLM_LM int sqlm_lm_rem_pio2(double x, double *y) {
   if (ix <= 0x3fe921fb) { /* |x| <= pi/4 */
     y[0] = x;
     y[1] = 0.0;
+    return 0;
+  }
+  if (ix > SQLM_LM_PIO2_MAX) { /* outside the medium range (and inf / NaN) */
+    y[0] = y[1] = __builtin_nan("");
     return 0;
   }
   double t = hx < 0 ? -x : x;

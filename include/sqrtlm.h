@@ -169,6 +169,16 @@ int sqlm_get_edge_level(sqlm_ctx *ctx, uint8_t *level);
  * cameras, out[7] = superblocks carrying band-border coupling. */
 int sqlm_get_rcs_layout(sqlm_ctx *ctx, int out[8]);
 
+/* Device paths the last optimize() ran (introspection for tests and tools; no
+ * reference counterpart): out[0] = 1 if the observation inputs (u, v,
+ * invSigma2, Huber delta) were all float32 values and travelled as float4,
+ * 0 if they took the double arrays; out[1] = reduced-camera solve: 0 none,
+ * 1 cyclic reduction as per-level launches, 2 cyclic reduction as one
+ * persistent launch (k_cr_persist), 3 band + border, 4 dense Cholesky;
+ * out[2] = tasks of the persistent solve, out[3] = its workgroups;
+ * out[4..7] = 0 (reserved). */
+int sqlm_get_exec_info(sqlm_ctx *ctx, int out[8]);
+
 /* Converter::toSE3Quat / toCvMat(SE3Quat) (src/utils/Converter.cc:55-79,98-109):
  * float32 row-major 4x4 T_cw <-> (q, t). */
 void sqlm_pose_from_Tcw_f32(const float T[16], double q[4], double t[3]);

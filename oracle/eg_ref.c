@@ -16,6 +16,17 @@
 #include "oracle.h"
 #include "se3_ref.h"
 #include "sqlm_libm.h" /* exp / log / sin / cos / acos, the same bits as the GPU (include/) */
+#ifdef ORC_GLIBC_LIBM
+/* liboracle_glibc.so: the platform libm instead, i.e. the arithmetic the
+ * reference's g2o (sim3.h through std::sin / cos / exp / log / acos) runs on
+ * -- pins the shared-libm oracle and the GPU to the reference's own libm
+ * (tests/test_eg_oracle.py, tests/test_eg_gpu.py) */
+#define sqlm_exp exp
+#define sqlm_log log
+#define sqlm_sin sin
+#define sqlm_cos cos
+#define sqlm_acos acos
+#endif
 #include "skyline_ref.h"
 
 /* ------------------------------------------------------------ Sim3 (sim3.h) */

@@ -15,6 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
 _LIB_OMP_PATH = os.path.join(_HERE, "_build", "liboracle_omp.so")  # all-cores variant (ORC_OMP)
+_LIB_GLIBC_PATH = os.path.join(_HERE, "_build", "liboracle_glibc.so")  # EG on glibc's libm (ORC_GLIBC_LIBM)
 TRACE_MAX = 256
 
 
@@ -55,11 +56,14 @@ def build() -> str:
     return _LIB_PATH
 
 
-def lib(omp: bool = False) -> C.CDLL:
+def lib(omp: bool = False, glibc: bool = False) -> C.CDLL:
     """The serial oracle, or (omp=True) the same restatement built with g2o's
-    OpenMP loops on every core (OMP_NUM_THREADS), bit-identical results."""
-    if omp not in _libs:
-        path = _LIB_OMP_PATH if omp else _LIB_PATH
+    OpenMP loops on every core (OMP_NUM_THREADS), bit-identical results, or
+    (glibc=True) the serial build whose Sim3 code calls the platform libm
+    instead of include/sqlm_libm.h."""
+    key = "glibc" if glibc else omp
+    if key not in _libs:
+        path = _LIB_GLIBC_PATH if glibc else _LIB_OMP_PATH if omp else _LIB_PATH
         if not os.path.exists(path):
             build()
         L = C.CDLL(path)
@@ -67,8 +71,8 @@ def lib(omp: bool = False) -> C.CDLL:
         L.orc_local_ba.restype = C.c_int
         L.orc_global_ba.restype = C.c_int
         L.orc_lidar_error.restype = C.c_double
-        _libs[omp] = L
-    return _libs[omp]
+        _libs[key] = L
+    return _libs[key]
 
 
 def omp_threads() -> int:
@@ -224,7 +228,8 @@ class OrcEgGraph(C.Structure):
 class OracleEG:
     """Owns numpy copies of a synth.PoseGraph and the orc_eg_graph view."""
 
-    def __init__(self, pg):
+    def __init__(self, pg, glibc: bool = False):
+        self._glibc = glibc
         self.Siw = pg.Siw.copy()
         self.fixed = pg.fixed.copy()
         self.ei, self.ej, self.Sji = pg.ei.copy(), pg.ej.copy(), pg.Sji.copy()
@@ -238,8 +243,9 @@ class OracleEG:
 
     def optimize(self, iterations=20, user_lambda=1e-16, stop=None):
         st = OrcStats()
-        lib().orc_eg_optimize.restype = C.c_int
-        n = lib().orc_eg_optimize(C.byref(self.g), iterations, C.c_double(user_lambda), _p(stop), C.byref(st))
+        L = lib(glibc=self._glibc)
+        L.orc_eg_optimize.restype = C.c_int
+        n = L.orc_eg_optimize(C.byref(self.g), iterations, C.c_double(user_lambda), _p(stop), C.byref(st))
         return n, st.as_dict()
 
     def edge_chi2(self):

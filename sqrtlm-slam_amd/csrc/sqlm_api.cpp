@@ -18,6 +18,7 @@
 #include <new>
 #include <queue>
 #include <thread>
+#include <unistd.h>
 #include <vector>
 
 #include "../../include/sqrtlm.h"
@@ -122,6 +123,8 @@ struct sqlm_ctx {
   int max_row_blocks = 0;
   int n_active_edges = 0;
   CRPlan cr;
+  CRPersist crp;                     // task graph of the persistent band solve (k_cr_persist)
+  int n_cu = 0;
   std::vector<int> cam_pos;          // hidx -> band position or -(1 + border index)
   bool use_tiles = false;
   int tile_max_cp = 0, tile_max_k = 0;
@@ -276,12 +279,17 @@ enum BufId {
 // preparing on another thread) falls back to threads of its own.
 class HostPool {
  public:
+  // never destroyed: a process (or a forked child, whose copy has no worker
+  // threads) exits without joining threads that may not exist
   static HostPool &get() {
-    static HostPool p;
-    return p;
+    static HostPool *p = new HostPool();
+    return *p;
   }
-  // fn(t) for t = 1 .. nth-1 on the workers while the caller runs fn(0)
+  // fn(t) for t = 1 .. nth-1 on the workers while the caller runs fn(0).
+  // In a child forked after the pool started (multiprocessing's default start
+  // method) the workers do not exist: false, the caller starts plain threads.
   bool try_run(int nth, const std::function<void(int)> &fn) {
+    if (getpid() != pid_) return false;
     std::unique_lock<std::mutex> busy(use_, std::try_to_lock);
     if (!busy.owns_lock()) return false;
     {
@@ -302,16 +310,8 @@ class HostPool {
     job_ = nullptr;
     return true;
   }
-  ~HostPool() {
-    {
-      std::lock_guard<std::mutex> lk(m_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto &t : th_) t.join();
-  }
-
  private:
+  HostPool() : pid_(getpid()) {}
   void worker(int id) {
     uint64_t seen = 0;
     std::unique_lock<std::mutex> lk(m_);
@@ -334,6 +334,7 @@ class HostPool {
   uint64_t gen_ = 0;
   int active_ = 0, pending_ = 0;
   bool stop_ = false;
+  const pid_t pid_;
 };
 
 // fn(t) for t = 0 .. nth-1 on nth host threads (t = 0 on the caller's)
@@ -1277,14 +1278,14 @@ int prepare(sqlm_ctx *c, int level) {
     unsigned *k0 = nullptr, *k1 = nullptr;
     int *v0 = nullptr;
     unsigned char *tmp = nullptr;
-    const size_t tb = cam_csr_temp_bytes(nE, nP);
+    const size_t sort_bytes = cam_csr_temp_bytes(nE, nP);
     AL(B_CAMKEY0, (size_t)nE, k0);
     AL(B_CAMKEY1, (size_t)nE, k1);
     AL(B_CAMVAL, (size_t)nE, v0);
-    AL(B_SORTTMP, tb, tmp);
+    AL(B_SORTTMP, sort_bytes, tmp);
     AL(B_CAMOBS, (size_t)nE, d.cam_obs);
     AL(B_CAMPTR, (size_t)nP + 1, d.cam_obs_ptr);
-    if (launch_cam_csr(d.obs_camh, nE, nP, k0, k1, v0, d.cam_obs, d.cam_obs_ptr, tmp, tb, c->stream))
+    if (launch_cam_csr(d.obs_camh, nE, nP, k0, k1, v0, d.cam_obs, d.cam_obs_ptr, tmp, sort_bytes, c->stream))
       return SQLM_ERR_HIP;
   }
   d.has_stereo = c->has_stereo ? 1 : 0;
@@ -1389,6 +1390,9 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_SCAL, (size_t)kNScalars, d.scalars);
   AL(B_MAXD, 1, d.maxdiag);
   AL(B_FLAGS, 4, d.flags);
+  HIP_OK(hipMemsetAsync(d.flags, 0, 4 * sizeof(int), c->stream));  // flags[1]: sticky device error of the solves
+  if (c->cr.enabled && !c->cr.R && cr_persist_enabled())
+    if (cr_persist_plan(c->crp, c->cr.p, c->cr.n, c->n_cu)) return SQLM_ERR_HIP;
   d.hdiag = nullptr;
   d.xstage = nullptr;
   if (c->comm.enabled()) {
@@ -1568,6 +1572,7 @@ int linearize(sqlm_ctx *c) {
 struct TrialOut {
   double chi_cur, chi_new, scale, maxdiag;
   bool ok;
+  bool dev_err;  // a solve kernel gave up a bounded wait (flags[1]): the result is not trusted
 };
 
 // Wait for k_reduce's mailbox entry `seq`. The stream is polled now and then:
@@ -1639,6 +1644,7 @@ int reduce_and_fetch(sqlm_ctx *c, TrialOut &o, bool cam_after = false) {
   o.scale = h[kScale];
   o.maxdiag = h[kMaxDiag];
   o.ok = h[kSolveOk] > 0.5;
+  o.dev_err = h[kDevErr] != 0.0;
   return SQLM_OK;
 }
 
@@ -1703,7 +1709,8 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   // unsharded CR: the pose update reads dx off the CR solution (no gather launch)
   const bool pose_from_cr = !sharded && c->cr.enabled;
   if (root) {
-    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream, !pose_from_cr) : launch_dense_solve(d, c->stream);
+    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream, !pose_from_cr, c->cr.R ? nullptr : &c->crp)
+                      : launch_dense_solve(d, c->stream);
     if (s) return s == -2 ? SQLM_ERR_HIP : SQLM_ERR_UNSUPPORTED;
   }
   if (sharded) {  // dx and the solve flag from rank 0
@@ -1818,6 +1825,7 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
       TrialOut o{};
       s = trial(c, lambda, o);
       if (s) return s;
+      if (o.dev_err) return SQLM_ERR_HIP;  // the step was rejected on the device too (flags[0] = 0)
       if (qmax == 0 && it > 0) { currentChi = o.chi_cur; iniChi = currentChi; }
       if (qmax == 0) acc_events(c, 0, c->lin_timers);
       tempChi = o.chi_new;
@@ -1961,6 +1969,8 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   sqlm_ctx *c = new (std::nothrow) sqlm_ctx();
   if (!c) return SQLM_ERR_OOM;
   c->device = dev;
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c->n_cu <= 0)
+    c->n_cu = 256;
   c->htrace = std::getenv("SQLM_HOST_TRACE") != nullptr;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) { delete c; return SQLM_ERR_HIP; }
   if (hipHostMalloc((void **)&c->h_scalars, sizeof(double) * kNScalars) != hipSuccess) {
@@ -2008,6 +2018,7 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   comm_destroy(c->comm);
   if (c->eg) eg_destroy(c->eg);
   if (c->orb) orb_destroy(c->orb);
+  cr_persist_free(c->crp);
   for (auto &b : c->bufs)
     if (b.p) (void)hipFree(b.p);
   for (auto &b : c->pins)
@@ -2073,11 +2084,13 @@ int sqlm_set_problem(sqlm_ctx *c, int n_pose, const double *pose_q, const double
   c->lid_pose.clear(); c->lid_pc.clear(); c->lid_pw.clear(); c->lid_n.clear(); c->lid_info.clear();
   c->lid_level.clear(); c->lid_err.clear();
   c->has_problem = true;
+  c->prepared = false;  // the CR layout of the previous problem no longer applies
   return SQLM_OK;
 }
 
 int sqlm_set_stereo(sqlm_ctx *c, const double *obs_ur, const double *pose_bf) {
   if (!c || !c->has_problem) return SQLM_ERR_STATE;
+  c->prepared = false;  // a setter changes what prepare() plans
   if (int s = fetch_errors(c)) return s;  // the last call's errors, in the layout they were computed in
   c->has_stereo = false;
   c->obs_ur.clear(); c->pose_bf.clear(); c->obs_err3.clear();
@@ -2099,6 +2112,7 @@ int sqlm_set_stereo(sqlm_ctx *c, const double *obs_ur, const double *pose_bf) {
 int sqlm_set_lidar(sqlm_ctx *c, int64_t n, const int32_t *pose, const double *p_cam, const double *p_world,
                    const double *normal, const double *info) {
   if (!c || !c->has_problem || n < 0) return SQLM_ERR_INVALID_ARG;
+  c->prepared = false;  // a setter changes what prepare() plans
   if (n && (!pose || !p_cam || !p_world || !normal || !info)) return SQLM_ERR_INVALID_ARG;
   for (int64_t e = 0; e < n; ++e)
     if (pose[e] < 0 || pose[e] >= c->n_pose) return SQLM_ERR_INVALID_ARG;
@@ -2116,18 +2130,21 @@ int sqlm_set_lidar(sqlm_ctx *c, int64_t n, const int32_t *pose, const double *p_
 
 int sqlm_set_edge_level(sqlm_ctx *c, const uint8_t *level) {
   if (!c || !c->has_problem || (!level && c->n_obs)) return SQLM_ERR_INVALID_ARG;
+  c->prepared = false;  // a setter changes what prepare() plans
   c->obs_level.assign(level, level + c->n_obs);
   return SQLM_OK;
 }
 
 int sqlm_set_lidar_level(sqlm_ctx *c, const uint8_t *level) {
   if (!c || !c->has_problem || (!level && c->n_lid)) return SQLM_ERR_INVALID_ARG;
+  c->prepared = false;  // a setter changes what prepare() plans
   c->lid_level.assign(level, level + c->n_lid);
   return SQLM_OK;
 }
 
 int sqlm_set_robust(sqlm_ctx *c, const double *delta) {
   if (!c || !c->has_problem) return SQLM_ERR_INVALID_ARG;
+  c->prepared = false;  // a setter changes what prepare() plans
   if (delta) c->obs_delta.assign(delta, delta + c->n_obs);
   else c->obs_delta.assign(c->n_obs, 0.0);
   return SQLM_OK;
@@ -2257,6 +2274,19 @@ int sqlm_get_rcs_layout(sqlm_ctx *c, int out[8]) {
   out[5] = pl.R;
   out[6] = nP;
   out[7] = pl.init_cnt;
+  return SQLM_OK;
+}
+
+int sqlm_get_exec_info(sqlm_ctx *c, int out[8]) {
+  if (!c || !out) return SQLM_ERR_INVALID_ARG;
+  if (!c->has_problem || !c->prepared) return SQLM_ERR_STATE;
+  const CRPlan &pl = c->cr;
+  const bool persist = pl.enabled && !pl.R && cr_persist_enabled() && c->crp.p == pl.p && c->crp.n == pl.n;
+  for (int k = 0; k < 8; ++k) out[k] = 0;
+  out[0] = c->d.obs_f32 ? 1 : 0;
+  out[1] = c->d.nP == 0 ? 0 : !pl.enabled ? 4 : pl.R ? 3 : persist ? 2 : 1;
+  out[2] = persist ? c->crp.ntasks : 0;
+  out[3] = persist ? c->crp.G : 0;
   return SQLM_OK;
 }
 

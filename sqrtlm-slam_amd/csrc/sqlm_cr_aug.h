@@ -51,6 +51,10 @@ constexpr int kWaves = 16, kThreads = 64 * kWaves, kMaxNt = kCRMaxN / 16, kWorke
 constexpr int kPairs = kMaxNt * (kMaxNt - 1) / 2;
 enum : int { kNone = 0, kColD = 1, kColI0 = 3, kColEt = 4, kColE = 5, kColG = 6 };
 
+#ifndef SQLM_SPIN_LIMIT
+#define SQLM_SPIN_LIMIT (1 << 20)
+#endif
+constexpr int kSpinLimit = SQLM_SPIN_LIMIT;
 constexpr int kTp = 17;  // padded row stride of the T_k images
 struct Shared {
   double T[kMaxNt][16 * kTp];  // T_k = L_kk^-1 of step k, row-major (the workers read it as an A operand)
@@ -118,11 +122,21 @@ __device__ __forceinline__ d4 identity_tile(int lane) {
 typedef __attribute__((address_space(3))) int lds_int;
 
 // Wait for a flag raised by another wave of the workgroup. Bounded (tens of
-// ms): a wave can never hang the device, whatever the schedule does.
-__device__ __forceinline__ void spin(int *f) {
+// ms): a wave can never hang the device, whatever the schedule does. Returns
+// false when the wait gave up: the caller then fails the solve (cr_fail) --
+// the data it goes on with is not the factor, and the trial must not use it.
+// -DSQLM_SPIN_FORCE_TIMEOUT (tests only): every wait reports a timeout after
+// it has completed, so the failure path runs on a correct factor.
+__device__ __forceinline__ bool spin(int *f) {
   lds_int *p = (lds_int *)f;
-  for (int it = 0; __atomic_load_n(p, __ATOMIC_RELAXED) == 0 && it < (1 << 20); ++it) __builtin_amdgcn_s_sleep(1);
+  int it = 0;
+  for (; __atomic_load_n(p, __ATOMIC_RELAXED) == 0 && it < kSpinLimit; ++it) __builtin_amdgcn_s_sleep(1);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef SQLM_SPIN_FORCE_TIMEOUT
+  return false;
+#else
+  return it < kSpinLimit;
+#endif
 }
 // Producer side: the DS instructions of one wave execute in order, so the flag
 // store lands after the data stores issued before it; only the compiler must
@@ -198,9 +212,9 @@ __device__ __forceinline__ void diag_groups(d4 Dg, d4 &P, d4 &Q, d4 &Tt, int lan
 
 // Row-k tile t <- T_k t (T_k = L_kk^-1 from wave 0, read from LDS as the A
 // operand: lane 16 b + i holds T_k[i][4 s + b] for K-step s).
-__device__ __forceinline__ void tile_trsm(Shared &sh, int k, d4 &t, int lane) {
+__device__ __forceinline__ void tile_trsm(Shared &sh, int k, d4 &t, int lane, bool &tmo) {
   const int b = lane >> 4, i = lane & 15;
-  spin(&sh.fT[k]);
+  tmo |= !spin(&sh.fT[k]);
   double ta[4];
 #pragma unroll
   for (int s4 = 0; s4 < 4; ++s4) ta[s4] = sh.T[k][i * kTp + 4 * s4 + b];
@@ -236,10 +250,11 @@ __device__ __forceinline__ d4 load_tile_sym(const double *P, int n, int r0, int 
   for (int j = 0; j < 4; ++j) t[j] = k4 + 4 * j >= c ? lo[j] : up[j];
   return t;
 }
+template <bool WT = false>
 __device__ __forceinline__ void store_tile(double *P, int n, int r0, int c0, const d4 &t, int lane) {
   const int k4 = lane >> 4, c = lane & 15;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) P[(size_t)(r0 + k4 + 4 * j) * n + c0 + c] = t[j];
+  for (int j = 0; j < 4; ++j) st_d<WT>(P + (size_t)(r0 + k4 + 4 * j) * n + c0 + c, t[j]);
 }
 
 // D columns carried by workers: J = 1 .. nt-1 (LINV: 0 .. nt-1, column 0 then
@@ -301,6 +316,7 @@ __device__ __forceinline__ bool takes_update(int type, int J, int k, int I) {
 // step k of a loop from the bottom: lane (q, r) sums U_kj[r][4q..4q+3] x_j over
 // j > k (j descending), the quarter sums are added by two xor shuffles, and
 // x_k = T_k^T (y_k - that).
+template <bool WT>
 __device__ __forceinline__ void top_back(aug::Shared &sh, const CRView &v, int I, int nt, const d4 *t, int lane) {
   using namespace aug;
   const int n = v.n, q = lane >> 4, r = lane & 15, k4 = lane >> 4;
@@ -332,7 +348,7 @@ __device__ __forceinline__ void top_back(aug::Shared &sh, const CRView &v, int I
     x += __shfl_xor(x, 32, 64);
     if (q == 0) {
       sh.bx[16 * i + r] = x;
-      v.x[(size_t)I * n + 16 * i + r] = x;
+      st_d<WT>(v.x + (size_t)I * n + 16 * i + r, x);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -340,19 +356,32 @@ __device__ __forceinline__ void top_back(aug::Shared &sh, const CRView &v, int I
   }
 }
 
+// A wait gave up (aug::spin, or a dependency wait of k_cr_persist): the
+// solve is marked failed (flags[0] = 0: the trial is rejected, as for a
+// non-positive pivot) and flags[1] keeps the error for the host, which returns
+// SQLM_ERR_HIP (never a silently wrong factor).
+constexpr int kCrErrTimeout = 1;
+__device__ __forceinline__ void cr_fail(const CRView &v, int lane) {
+  if (lane == 0) {
+    __hip_atomic_store(v.flags, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(v.flags + 1, kCrErrTimeout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // MODE 0: level step (A_I, C_I, z_I and the back-substitution factor).
 // MODE 1: factor only (z_I and the factor). LINV: the factor is Linv_I
 // (lower, dense tiles); otherwise the upper U tiles with T_k on the diagonal.
-// Superblock I = I0 + stride * (blockIdx.x / split); workgroup sidx = blockIdx.x % split.
-template <int MODE, bool LINV, bool BACK = false>
-__global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I0, int stride, int split) {
+// Superblock I, workgroup sidx of the split that serve it. Every thread of the
+// workgroup enters; waves return as their role ends (no barrier after the
+// first). WT: results stored write-through (sc1) for in-launch consumers in
+// other workgroups (k_cr_persist).
+template <int MODE, bool LINV, bool BACK, bool WT>
+__device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h, int I, int split, int sidx) {
   using namespace aug;
-  extern __shared__ __attribute__((aligned(16))) unsigned char aug_lds[];
-  Shared &sh = *reinterpret_cast<Shared *>(aug_lds);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ob = blockIdx.x / split, sidx = blockIdx.x - ob * split;
-  const int I = I0 + stride * ob, n = v.n, nt = n >> 4;
+  const int n = v.n, nt = n >> 4;
   const bool level = MODE == 0, right = level && I + h < v.p, first = sidx == 0;
+  bool tmo = false;
   for (int t = threadIdx.x; t < 2 * kMaxNt + kPairs; t += blockDim.x) {
     if (t < kMaxNt) sh.fT[t] = 0;
     else if (t < kMaxNt + kPairs) sh.fU[t - kMaxNt] = 0;
@@ -387,18 +416,18 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
 #pragma unroll
         for (int j = 0; j < 4; ++j) sh.T[k][(k4 + 4 * j) * kTp + c] = Tt[j];
         raise_flag(&sh.fT[k], lane);
-        if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * k, Tt, lane);
+        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * k, Tt, lane);
       }
       AUG_PROF(2 + k);
       if (k + 1 < nt) {  // U_k,k+1 feeds the trailing updates of row k+1
         put_tile(sh.U[pair_id(k, k + 1)], P, lane);
         raise_flag(&sh.fU[pair_id(k, k + 1)], lane);
-        if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * (k + 1), P, lane);
+        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * (k + 1), P, lane);
       }
       if (k + 2 < nt) {  // the next step's P = (k+1, k+2) and Q = (k+2, k+2) through step k
-        spin(&sh.fH[k + 2]);
+        tmo |= !spin(&sh.fH[k + 2]);
         d4 P2 = get_tile(sh.Hp[k + 2], lane), Q2 = get_tile(sh.Hq[k + 2], lane);
-        spin(&sh.fU[pair_id(k, k + 2)]);
+        tmo |= !spin(&sh.fU[pair_id(k, k + 2)]);
         const d4 X = get_tile(sh.U[pair_id(k, k + 2)], lane);
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) Q2 = mfma(-X[s4], X[s4], Q2);
@@ -412,6 +441,7 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
       }
     }
     if (bad && lane == 0) v.flags[0] = 0;
+    if (tmo) cr_fail(v, lane);
     return;
   }
   if ((wave & 3) == 0) return;  // the diagonal wave's SIMD partners stay idle
@@ -451,7 +481,7 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
       for (int r = k + 1; r < kMaxNt; ++r) {
         if (r >= nt || !takes_update<LINV>(type, J, k - 1, r)) continue;
         const int pid = pair_id(k - 1, r);
-        spin(&sh.fU[pid]);
+        tmo |= !spin(&sh.fU[pid]);
         const double *U = sh.U[pid];
 #pragma unroll
         for (int s = 0; s < 4; ++s) t[r] = mfma(-U[64 * s + lane], t[k - 1][s], t[r]);
@@ -467,7 +497,7 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
     const bool dtile = type == kColD && k <= J - 2;
     const bool rowk = type == kColD ? (dtile || (LINV && k > J)) : type != kNone;
     if (rowk) {
-      tile_trsm(sh, k, t[k], lane);
+      tile_trsm(sh, k, t[k], lane, tmo);
       if (dtile) {  // U_kJ feeds the trailing updates of row J
         put_tile(sh.U[pair_id(k, J)], t[k], lane);
         raise_flag(&sh.fU[pair_id(k, J)], lane);
@@ -477,7 +507,7 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
     // trailing of step k, row k+1 (the next step's row)
     if (k + 1 < nt && rowk && takes_update<LINV>(type, J, k, k + 1)) {
       const int pid = pair_id(k, k + 1);
-      spin(&sh.fU[pid]);
+      tmo |= !spin(&sh.fU[pid]);
       const double *U = sh.U[pid];
 #pragma unroll
       for (int s = 0; s < 4; ++s) t[k + 1] = mfma(-U[64 * s + lane], t[k][s], t[k + 1]);
@@ -490,25 +520,34 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I
     if (r >= nt) continue;
     if (type == kColD) {
       if (LINV) {
-        if (first && r > J) store_tile(Lb, n, 16 * r, 16 * (J + 1), t[r], lane);  // Linv block column J+1
+        if (first && r > J) store_tile<WT>(Lb, n, 16 * r, 16 * (J + 1), t[r], lane);  // Linv block column J+1
       } else {
-        if (first && r <= J - 2) store_tile(Lb, n, 16 * r, 16 * J, t[r], lane);  // U tile (r, J); (J-1, J): wave 0
+        if (first && r <= J - 2) store_tile<WT>(Lb, n, 16 * r, 16 * J, t[r], lane);  // U tile (r, J); (J-1, J): wave 0
       }
     } else if (type == kColI0) {
-      if (first) store_tile(Lb, n, 16 * r, 0, t[r], lane);
+      if (first) store_tile<WT>(Lb, n, 16 * r, 0, t[r], lane);
     } else if (type == kColEt) {
-      store_tile(blk(v.A, I, n), n, 16 * r, 16 * J, t[r], lane);
+      store_tile<WT>(blk(v.A, I, n), n, 16 * r, 16 * J, t[r], lane);
     } else if (type == kColE) {
-      store_tile(blk(v.C, I, n), n, 16 * r, 16 * J, t[r], lane);
+      store_tile<WT>(blk(v.C, I, n), n, 16 * r, 16 * J, t[r], lane);
     } else if (type == kColG) {
       const int k4 = lane >> 4, c = lane & 15;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (c == 0) v.g[(size_t)I * n + 16 * r + k4 + 4 * j] = t[r][j];
+        if (c == 0) st_d<WT>(v.g + (size_t)I * n + 16 * r + k4 + 4 * j, t[r][j]);
     }
   }
-  if (BACK && type == kColG) top_back(sh, v, I, nt, t, lane);
+  if (BACK && type == kColG) top_back<WT>(sh, v, I, nt, t, lane);
+  if (tmo) cr_fail(v, lane);
   AUG_PROF(16 + wave);
+}
+
+// Superblock I = I0 + stride * (blockIdx.x / split); workgroup sidx = blockIdx.x % split.
+template <int MODE, bool LINV, bool BACK = false>
+__global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I0, int stride, int split) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char aug_lds[];
+  const int ob = blockIdx.x / split, sidx = blockIdx.x - ob * split;
+  aug_body<MODE, LINV, BACK, false>(*reinterpret_cast<aug::Shared *>(aug_lds), v, h, I0 + stride * ob, split, sidx);
 }
 
 // Workgroups per odd superblock for the augmented factor: enough to hold the

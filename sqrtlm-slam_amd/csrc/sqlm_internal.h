@@ -154,7 +154,7 @@ struct DevProblem {
   int *flags = nullptr;                     // [4] solve_ok ...
 };
 
-enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kNScalars = 8 };
+enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kDevErr = 5, kNScalars = 8 };
 constexpr int kMboxSeq = 7;  // host mailbox: the scalars, then the sequence number in slot 7
 
 // partial-sum slots
@@ -259,12 +259,44 @@ int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase co
 #endif
 constexpr int kRedLong = 24;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather = true);  // zeroes + scatters unless cr_direct
+struct CRPersist;
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather = true,
+                    CRPersist *ps = nullptr);  // zeroes + scatters unless cr_direct
 // band + border layout: clear F^T / the border system before S is assembled into it
 void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st);
-// CR levels + top + back substitution on blocks already in CR layout (microbench / tests)
+// Persistent cyclic reduction (k_cr_persist, sqlm_rcs_solve.hip): the whole
+// band solve -- every level's factors, eliminations and updates, the top
+// superblock and the back substitution -- as ONE launch of workgroups that
+// take tasks from an in-launch queue in dependency order and hand results
+// over through completion words (agent-scope release / acquire). The task
+// graph of a (p, n) system is built on the host once per plan.
+enum CRTaskType : int { kTkF = 0, kTkFO = 1, kTkTR = 2, kTkUP = 3, kTkTOP = 4, kTkBK = 5 };
+struct CRTask {
+  int type, I, h;
+  int a, b;               // F: split index / split; UP: first item / items; TR: first strip / strips
+  int dep_off, dep_cnt;   // predecessors: deps[dep_off .. +dep_cnt) (task ids)
+  int pad;
+};
+struct CRPersist {
+  int p = -1, n = -1, ntasks = 0, ndeps = 0, G = 0;
+  std::vector<CRTask> h_tasks;
+  std::vector<int> h_deps;
+  CRTask *tasks = nullptr;
+  int *deps = nullptr;
+  int *done = nullptr;                 // [ntasks] epoch of the launch that finished the task
+  unsigned long long *head = nullptr;  // queue head, monotonic over launches
+  unsigned long long qbase = 0;        // head value at the start of the next launch
+  int epoch = 0;
+  size_t cap_tasks = 0, cap_deps = 0;
+};
+// SQLM_CR_PERSIST=1 selects it (until validated on MI355X: per-level launches by default)
+bool cr_persist_enabled();
+int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu);  // 0 ok, -2 HIP error
+void cr_persist_free(CRPersist &ps);
+// CR levels + top + back substitution on blocks already in CR layout; ps
+// (planned for this p, n): one persistent launch, else the per-level launches
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
-                    hipStream_t st);
+                    hipStream_t st, CRPersist *ps = nullptr);
 // Dense SPD solve (sqlm_rcs_solve.hip): A (n x n, lower, n % kCRMaxN == 0) is
 // factored in place into L (+ diagonal block inverses Linv), r is consumed,
 // x = A^-1 r; flags[0] is cleared on a non-positive pivot. band > 0: A is a

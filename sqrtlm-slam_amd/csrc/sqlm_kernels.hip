@@ -1812,12 +1812,14 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
     d.scalars[kMaxDiag] = __longlong_as_double((long long)*d.maxdiag);
     *d.maxdiag = 0ull;  // ready for the next linearization's atomicMax
     d.scalars[kSolveOk] = (double)d.flags[0];
+    d.scalars[kDevErr] = (double)d.flags[1];
     if (mbox) {
       mbox[kChiCur] = part[0] + part[1];
       mbox[kChiNew] = part[2] + part[3];
       mbox[kScale] = part[4] + part[5];
       mbox[kMaxDiag] = d.scalars[kMaxDiag];
       mbox[kSolveOk] = (double)d.flags[0];
+      mbox[kDevErr] = (double)d.flags[1];
       __threadfence_system();
       __hip_atomic_store(reinterpret_cast<unsigned long long *>(mbox + kMboxSeq), seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);

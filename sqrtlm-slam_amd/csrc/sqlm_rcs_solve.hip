@@ -40,6 +40,15 @@ namespace sqlm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Result stores. WT (the persistent solve, k_cr_persist): write-through (sc1),
+// so a consumer workgroup elsewhere on the chip reads them after its agent
+// acquire without a release fence (L2 write-back) by the producer.
+template <bool WT>
+__device__ __forceinline__ void st_d(double *p, double v) {
+  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 // Phase timestamps for tools/cr_bench (compiled with -DSQLM_CR_PROF only).
 #ifdef SQLM_CR_PROF
 __device__ long long *g_cr_prof;
@@ -471,7 +480,10 @@ __global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
 
 // One wavefront computes one 16x16 tile acc = op(A) op(B) over K = n,
 // skipping K blocks that are zero because A is lower triangular (LA).
-template <bool TA, bool TB, bool LA>
+// CH: K pairs whose operands are loaded together (all of them by default;
+// the persistent solve's 128-VGPR budget takes them in chunks -- the MFMA
+// order, and so the result, is the same)
+template <bool TA, bool TB, bool LA, int CH = kCRMaxN / 8>
 __device__ __forceinline__ d4 tile_gemm(const double *A, const double *B, int n, int ti, int tj) {
   // K order within each pair of MFMA steps m: lane k4 feeds k = 8m + 2 k4 to the
   // first and k + 1 to the second, so row-contiguous operands (A untransposed,
@@ -480,42 +492,48 @@ __device__ __forceinline__ d4 tile_gemm(const double *A, const double *B, int n,
   const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
   const int ar = ti * 16 + r16, bc = tj * 16 + r16;
   const int kend = LA ? 16 * (ti + 1) : n;
-  d2 av[kCRMaxN / 8], bv[kCRMaxN / 8];
+  d4 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-  for (int m = 0; m < kCRMaxN / 8; ++m) {
-    const int k = 8 * m + 2 * k4;
-    if (8 * m < kend) {
-      if (TA) {
-        av[m].x = A[k * n + ar];
-        av[m].y = A[(k + 1) * n + ar];
-      } else {
-        av[m] = *reinterpret_cast<const d2 *>(A + ar * n + k);
+  for (int m0 = 0; m0 < kCRMaxN / 8; m0 += CH) {
+    d2 av[CH], bv[CH];
+#pragma unroll
+    for (int mm = 0; mm < CH; ++mm) {
+      const int m = m0 + mm, k = 8 * m + 2 * k4;
+      if (m < kCRMaxN / 8 && 8 * m < kend) {
+        if (TA) {
+          av[mm].x = A[k * n + ar];
+          av[mm].y = A[(k + 1) * n + ar];
+        } else {
+          av[mm] = *reinterpret_cast<const d2 *>(A + ar * n + k);
+        }
+        if (TB) {
+          bv[mm] = *reinterpret_cast<const d2 *>(B + bc * n + k);
+        } else {
+          bv[mm].x = B[k * n + bc];
+          bv[mm].y = B[(k + 1) * n + bc];
+        }
       }
-      if (TB) {
-        bv[m] = *reinterpret_cast<const d2 *>(B + bc * n + k);
-      } else {
-        bv[m].x = B[k * n + bc];
-        bv[m].y = B[(k + 1) * n + bc];
+    }
+#pragma unroll
+    for (int mm = 0; mm < CH; ++mm) {
+      const int m = m0 + mm;
+      if (m < kCRMaxN / 8 && 8 * m < kend) {
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mm].x, bv[mm].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[mm].y, bv[mm].y, acc, 0, 0, 0);
       }
     }
   }
-  d4 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-  for (int m = 0; m < kCRMaxN / 8; ++m)
-    if (8 * m < kend) {
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].x, bv[m].x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[m].y, bv[m].y, acc, 0, 0, 0);
-    }
   return acc;
 }
 
+template <bool WT = false>
 __device__ __forceinline__ void tile_store(double *C, int n, int ti, int tj, const d4 &acc, double alpha,
                                            bool accumulate) {
   const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double *c = C + (ti * 16 + k4 + 4 * j) * n + tj * 16 + r16;
-    *c = accumulate ? *c + alpha * acc[j] : alpha * acc[j];
+    st_d<WT>(c, accumulate ? *c + alpha * acc[j] : alpha * acc[j]);
   }
 }
 
@@ -634,6 +652,7 @@ inline int cr_split(int n_odd, int nt) { return std::max(1, std::min(2 * nt, 256
 // D_J -= A_{J+h}^T A_{J+h} + C_{J-h}^T C_{J-h} (lower tiles only);
 // E_J = -A_{J+h}^T C_{J+h}; g_J -= A_{J+h}^T z_{J+h} + C_{J-h}^T z_{J-h}.
 // Work items per even block: nt(nt+1)/2 D tiles, nt^2 E tiles, nt g slices.
+template <bool WT = false, int CH = kCRMaxN / 8>
 __device__ __forceinline__ void cr_update_item(const CRView &v, int h, int lb) {
   const int n = v.n, nt = n >> 4, nd = nt * (nt + 1) / 2, items = nd + nt * nt + nt;
   const int ev = lb / items, rem = lb - ev * items;
@@ -644,17 +663,17 @@ __device__ __forceinline__ void cr_update_item(const CRView &v, int h, int lb) {
     int ti = 0, tj = rem;
     while (tj > ti) { tj -= ti + 1; ++ti; }
     d4 acc = {0.0, 0.0, 0.0, 0.0};
-    if (right) acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.A, J + h, n), n, ti, tj);
+    if (right) acc = tile_gemm<true, false, false, CH>(blk(v.A, J + h, n), blk(v.A, J + h, n), n, ti, tj);
     if (left) {
-      const d4 a2 = tile_gemm<true, false, false>(blk(v.C, J - h, n), blk(v.C, J - h, n), n, ti, tj);
+      const d4 a2 = tile_gemm<true, false, false, CH>(blk(v.C, J - h, n), blk(v.C, J - h, n), n, ti, tj);
       acc += a2;
     }
-    if (right || left) tile_store(blk(v.D, J, n), n, ti, tj, acc, -1.0, true);
+    if (right || left) tile_store<WT>(blk(v.D, J, n), n, ti, tj, acc, -1.0, true);
   } else if (rem < nd + nt * nt) {
     const int t = rem - nd, ti = t / nt, tj = t - ti * nt;
     if (right && J + 2 * h < v.p) {
-      const d4 acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.C, J + h, n), n, ti, tj);
-      tile_store(blk(v.E, J, n), n, ti, tj, acc, -1.0, false);
+      const d4 acc = tile_gemm<true, false, false, CH>(blk(v.A, J + h, n), blk(v.C, J + h, n), n, ti, tj);
+      tile_store<WT>(blk(v.E, J, n), n, ti, tj, acc, -1.0, false);
     }
   } else {  // right-hand side rows 16 ti .. +16
     const int ar = 16 * (rem - nd - nt * nt) + r16;
@@ -676,7 +695,7 @@ __device__ __forceinline__ void cr_update_item(const CRView &v, int h, int lb) {
       }
     }
     s = k4_sum(s);
-    if (k4 == 0) v.g[(size_t)J * n + ar] -= s;
+    if (k4 == 0) st_d<WT>(v.g + (size_t)J * n + ar, v.g[(size_t)J * n + ar] - s);
   }
 }
 
@@ -812,12 +831,11 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
 // Wave i owns block row i: its U tiles and T_i are loaded up front, each U_ij x_j
 // term is added as soon as x_j is flagged in LDS, so after x_{i+1} only one
 // 16x16 product, two 16-lane sums and T_i^T remain on the chain.
-template <bool TOP>
-__global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
+template <bool TOP, bool WT>
+__device__ __forceinline__ void back_u_body(double *sm, const CRView &v, int h, int I) {
   double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN;
   int *fx = reinterpret_cast<int *>(sm + 3 * kCRMaxN);
-  const int I = TOP ? 0 : h + 2 * h * blockIdx.x, n = v.n, nt = n >> 4;
+  const int n = v.n, nt = n >> 4;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
   if (threadIdx.x < aug::kMaxNt) fx[threadIdx.x] = 0;
   // this wave's U row and T_i first: in flight during the right-hand side
@@ -839,11 +857,12 @@ __global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
     cr_back_body<false>(v, h, I, y);  // ends with a barrier (also covers fx)
   }
   if (wave >= nt) return;
+  bool tmo = false;
   double acc = 0.0;
 #pragma unroll
   for (int j = aug::kMaxNt - 1; j > 0; --j)
     if (j > i && j < nt) {
-      aug::spin(&fx[j]);
+      tmo |= !aug::spin(&fx[j]);
 #pragma unroll
       for (int m = 0; m < 4; ++m) acc = fma(u[j][m], xs[16 * j + 4 * q + m], acc);
     }
@@ -860,9 +879,16 @@ __global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
   x += __shfl_xor(x, 32, 64);
   if (q == 0) {
     xs[16 * i + r] = x;
-    v.x[(size_t)I * n + 16 * i + r] = x;
+    st_d<WT>(v.x + (size_t)I * n + 16 * i + r, x);
   }
   aug::raise_flag(&fx[i], lane);
+  if (tmo) cr_fail(v, lane);
+}
+
+template <bool TOP>
+__global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  back_u_body<TOP, false>(sm, v, h, TOP ? 0 : h + 2 * h * blockIdx.x);
 }
 
 
@@ -1304,11 +1330,9 @@ __global__ __launch_bounds__(512) void k_cr_factor_at(CRView v, int I) {
 // k_cr_aug. One wavefront per 16-column strip: the levels with many odd
 // superblocks (the fused kernel would need more workgroups than CUs) run the
 // factor and this kernel instead.
-__global__ __launch_bounds__(256) void k_cr_trsm(CRView v, int h, int total) {
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gw >= total) return;
+template <bool WT>
+__device__ __forceinline__ void trsm_strip(const CRView &v, int h, int I, int s) {
   const int n = v.n, nt = n >> 4, lane = threadIdx.x & 63, b = lane >> 4, i16 = lane & 15;
-  const int ob = gw / (2 * nt), s = gw - ob * 2 * nt, I = h + 2 * h * ob;
   const bool et = s < nt;
   const int J = et ? s : s - nt;
   if (!et && I + h >= v.p) return;
@@ -1340,7 +1364,14 @@ __global__ __launch_bounds__(256) void k_cr_trsm(CRView v, int h, int total) {
   double *out = blk(et ? v.A : v.C, I, n);
 #pragma unroll
   for (int r = 0; r < aug::kMaxNt; ++r)
-    if (r < nt) aug::store_tile(out, n, 16 * r, 16 * J, t[r], lane);
+    if (r < nt) aug::store_tile<WT>(out, n, 16 * r, 16 * J, t[r], lane);
+}
+
+__global__ __launch_bounds__(256) void k_cr_trsm(CRView v, int h, int total) {
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= total) return;
+  const int nt = v.n >> 4, ob = gw / (2 * nt), s = gw - ob * 2 * nt;
+  trsm_strip<false>(v, h, h + 2 * h * ob, s);
 }
 
 // SQLM_CR_LEGACY=1: the round-2 factor (panel Cholesky + explicit Linv in LDS,
@@ -1665,6 +1696,304 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
   }
 }
 
+// ---- persistent cyclic reduction ---------------------------------------------
+// One launch runs the whole band solve of launch_cr_core (the SimplicialLDLT
+// solve of linear_solver_eigen.h:94-124 on the block-tridiagonal S): the
+// per-level kernels cost >= 4.5 us each as dependent launches (28 per config-4
+// solve) and every level waited for its slowest workgroup. Here each
+// workgroup (16 waves, the k_cr_aug geometry, one per CU) takes the next task
+// of a host-built list in dependency order from a queue word, waits for the
+// task's predecessors' completion words, runs the body of the kernel the
+// task replaces (same device code, same order of operations: the solution is
+// bit-identical to the per-level launches), and publishes.
+//   F   k_cr_aug<0> share sidx of odd superblock I at level h (factor, A, C, z)
+//   FO  k_cr_aug<1> on I (wide levels: factor and z only), then
+//   TR  k_cr_trsm strips a .. a+b-1 of I (A_I, C_I from the factor)
+//   UP  cr_update_item a .. a+b-1 of even superblock I (one wave per item)
+//   TOP k_cr_aug<1, BACK> on superblock 0;  BK  k_cr_back_u<false> on I
+// Hand-off (MI355X: per-XCD L2s, per-CU L1s): results are stored
+// write-through (sc1) and drained (s_waitcnt vmcnt(0)) by every storing wave,
+// a barrier, then one lane stores the task's completion word = epoch (sc1).
+// A consumer's wave 0 polls its predecessors' words relaxed (one lane each,
+// s_sleep between polls), then ONE agent acquire (L1 invalidate) + vmcnt(0) +
+// barrier before any load. Tasks are dequeued in list order, so every
+// predecessor of a dequeued task is held by a running workgroup: no deadlock
+// at any residency. Every wait is bounded; a timeout fails the solve loudly
+// (cr_fail). Completion words carry the launch's epoch and the queue head is
+// monotonic (the host adds the launch's dequeues), so nothing is reset.
+constexpr int kPersistUpdItems = 16;  // UP task: one item per wave
+
+// the task bodies as separate functions: inlined into one switch they share
+// one register allocation (the union of their live ranges spills)
+__device__ __noinline__ void pt_f(aug::Shared &sh, const CRView &v, int h, int I, int split, int sidx) {
+  aug_body<0, false, false, true>(sh, v, h, I, split, sidx);
+}
+__device__ __noinline__ void pt_fo(aug::Shared &sh, const CRView &v, int h, int I) {
+  aug_body<1, false, false, true>(sh, v, h, I, 1, 0);
+}
+__device__ __noinline__ void pt_top(aug::Shared &sh, const CRView &v) { aug_body<1, false, true, true>(sh, v, 0, 0, 1, 0); }
+__device__ __noinline__ void pt_tr(const CRView &v, int h, int I, int s) { trsm_strip<true>(v, h, I, s); }
+__device__ __noinline__ void pt_up(const CRView &v, int h, int lb) { cr_update_item<true, 4>(v, h, lb); }
+
+// k_cr_back_u<false> for the persistent solve (16 waves, <= 128 VGPRs): the
+// neighbours' solutions staged in LDS, y = z_I - A_I x_{I-h} - C_I x_{I+h}
+// with one 8-row slice per wave, then the blocked backward substitution of
+// back_u_body.
+__device__ __noinline__ void pt_bk(double *sm, const CRView &v, int h, int I) {
+  double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN, *xl = sm + 3 * kCRMaxN, *xr = sm + 4 * kCRMaxN;
+  int *fx = reinterpret_cast<int *>(sm + 5 * kCRMaxN);
+  const int n = v.n, nt = n >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
+  const bool right = I + h < v.p;
+  if (threadIdx.x < aug::kMaxNt) fx[threadIdx.x] = 0;
+  for (int k = threadIdx.x; k < 2 * n; k += blockDim.x) {
+    if (k < n) xl[k] = v.x[(size_t)(I - h) * n + k];
+    else xr[k - n] = right ? v.x[(size_t)(I + h) * n + k - n] : 0.0;
+  }
+  // this wave's U row and T_i (waves < nt): in flight during the right-hand side
+  const int i = wave < nt ? wave : nt - 1;
+  const double *Lb = blk(v.L, I, n);
+  double u[aug::kMaxNt][4], tv[4];
+#pragma unroll
+  for (int j = 0; j < aug::kMaxNt; ++j)
+    if (j > i && j < nt) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) u[j][m] = Lb[(size_t)(16 * i + r) * n + 16 * j + 4 * q + m];  // U_ij[r][4q+m]
+    }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) tv[m] = Lb[(size_t)(16 * i + 4 * q + m) * n + 16 * i + r];  // T_i[4q+m][r]
+  __syncthreads();
+  if (wave < 2 * nt) {  // row 8 wave + (lane >> 3), columns 16 u + 2 lo (+1)
+    using d2 = HIP_vector_type<double, 2>;
+    const int lo = lane & 7, row = 8 * wave + (lane >> 3), hn = n >> 1;
+    const d2 *A = reinterpret_cast<const d2 *>(blk(v.A, I, n)), *C = reinterpret_cast<const d2 *>(blk(v.C, I, n));
+    d2 a[kCRMaxN / 16], c[kCRMaxN / 16];
+#pragma unroll
+    for (int uu = 0; uu < kCRMaxN / 16; ++uu) {
+      const int cc = kclamp(16 * uu + 2 * lo, n) >> 1;
+      a[uu] = A[row * hn + cc];
+      c[uu] = right ? C[row * hn + cc] : d2{0.0, 0.0};
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int uu = 0; uu < kCRMaxN / 16; ++uu)
+      if (16 * uu < n) {
+        const int cc = 16 * uu + 2 * lo;
+        s += a[uu].x * xl[cc] + a[uu].y * xl[cc + 1];
+        if (right) s += c[uu].x * xr[cc] + c[uu].y * xr[cc + 1];
+      }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) s += __shfl_xor(s, m, 64);
+    if (lo == 0) y[row] = v.g[(size_t)I * n + row] - s;
+  }
+  __syncthreads();
+  if (wave >= nt) return;
+  bool tmo = false;
+  double acc = 0.0;
+#pragma unroll
+  for (int j = aug::kMaxNt - 1; j > 0; --j)
+    if (j > i && j < nt) {
+      tmo |= !aug::spin(&fx[j]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = fma(u[j][m], xs[16 * j + 4 * q + m], acc);
+    }
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  if (q == 0) rr[16 * i + r] = y[16 * i + r] - acc;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double x = 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) x = fma(tv[m], rr[16 * i + 4 * q + m], x);  // lane (q, c = r)
+  x += __shfl_xor(x, 16, 64);
+  x += __shfl_xor(x, 32, 64);
+  if (q == 0) {
+    xs[16 * i + r] = x;
+    st_d<true>(v.x + (size_t)I * n + 16 * i + r, x);
+  }
+  aug::raise_flag(&fx[i], lane);
+  if (tmo) cr_fail(v, lane);
+}
+
+__global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CRTask *__restrict__ tasks,
+                                                             const int *__restrict__ deps, int ntasks, int *done,
+                                                             unsigned long long *head, unsigned long long qbase,
+                                                             int epoch) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  __shared__ CRTask s_task;
+  __shared__ int s_id;
+  aug::Shared &sh = *reinterpret_cast<aug::Shared *>(lds_raw);
+  double *lds_d = reinterpret_cast<double *>(lds_raw);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (;;) {
+    if (tid == 0) {
+      const unsigned long long q = __hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const long long t = (long long)(q - qbase);
+      s_id = t < ntasks ? (int)t : -1;
+      if (t < ntasks) s_task = tasks[t];
+    }
+    __syncthreads();
+    const int id = s_id;
+    if (id < 0) break;
+    const CRTask tk = s_task;
+    if (wave == 0 && tk.dep_cnt > 0) {
+      bool ok = true;
+      for (int base = 0; base < tk.dep_cnt; base += 64) {
+        const int k = base + lane;
+        int *f = k < tk.dep_cnt ? done + deps[tk.dep_off + k] : nullptr;
+        for (int it = 0;; ++it) {
+          const bool mine = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+          if (__all(mine)) break;
+          if (it >= aug::kSpinLimit) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (!ok) cr_fail(v, lane);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    switch (tk.type) {
+      case kTkF:
+        pt_f(sh, v, tk.h, tk.I, tk.b, tk.a);
+        break;
+      case kTkFO:
+        pt_fo(sh, v, tk.h, tk.I);
+        break;
+      case kTkTR:
+        if (wave < tk.b) pt_tr(v, tk.h, tk.I, tk.a + wave);
+        break;
+      case kTkUP: {
+        const int nt = v.n >> 4, items = nt * (nt + 1) / 2 + nt * nt + nt;
+        if (wave < tk.b) pt_up(v, tk.h, (tk.I / (2 * tk.h)) * items + tk.a + wave);
+        break;
+      }
+      case kTkTOP:
+        pt_top(sh, v);
+        break;
+      default:  // kTkBK
+        pt_bk(lds_d, v, tk.h, tk.I);
+        break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(done + id, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+bool cr_persist_enabled() {
+  static const bool on = std::getenv("SQLM_CR_PERSIST") && std::atoi(std::getenv("SQLM_CR_PERSIST")) != 0;
+  return on && !cr_legacy();
+}
+
+void cr_persist_free(CRPersist &ps) {
+  if (ps.tasks) (void)hipFree(ps.tasks);
+  if (ps.deps) (void)hipFree(ps.deps);
+  if (ps.done) (void)hipFree(ps.done);
+  if (ps.head) (void)hipFree(ps.head);
+  ps = CRPersist{};
+}
+
+// The task list of launch_cr_core's schedule for p superblocks of n rows, in
+// the order of its launches (a task's predecessors come before it).
+int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu) {
+  if (ps.p == p && ps.n == n && ps.tasks) return 0;
+  const int nt = n / 16, items = nt * (nt + 1) / 2 + nt * nt + nt;
+  std::vector<CRTask> T;
+  std::vector<int> D;
+  std::vector<std::vector<int>> lastw(p), prod(p);  // last writers of D/E/g_I; producers of L/A/C/z_I
+  std::vector<int> xprod(p, -1);
+  auto add = [&](CRTask t, std::vector<int> dp) {
+    std::sort(dp.begin(), dp.end());
+    dp.erase(std::unique(dp.begin(), dp.end()), dp.end());
+    t.dep_off = (int)D.size();
+    t.dep_cnt = (int)dp.size();
+    t.pad = 0;
+    D.insert(D.end(), dp.begin(), dp.end());
+    T.push_back(t);
+    return (int)T.size() - 1;
+  };
+  auto cat = [](std::vector<int> a, const std::vector<int> &b) {
+    a.insert(a.end(), b.begin(), b.end());
+    return a;
+  };
+  int h = 1;
+  for (; h < p; h *= 2) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h), n_even = (p + 2 * h - 1) / (2 * h);
+    const bool wide = cr_level_wide(n_odd, nt, false);
+    const int sp = aug_split(n_odd, nt, false, aug::extra_columns(nt, true, true));
+    for (int o = 0; o < n_odd; ++o) {
+      const int I = h + 2 * h * o;
+      const std::vector<int> dp = cat(lastw[I], lastw[I - h]);
+      if (wide) {
+        const int f = add(CRTask{kTkFO, I, h, 0, 1}, dp);
+        const int tr = add(CRTask{kTkTR, I, h, 0, 2 * nt}, {f});
+        prod[I] = {f, tr};
+      } else {
+        for (int s = 0; s < sp; ++s) prod[I].push_back(add(CRTask{kTkF, I, h, s, sp}, dp));
+      }
+    }
+    for (int e = 0; e < n_even; ++e) {
+      const int J = 2 * h * e;
+      const bool right = J + h < p, left = J >= h;
+      if (!right && !left) continue;
+      std::vector<int> dp = lastw[J];
+      if (right) dp = cat(dp, prod[J + h]);
+      if (left) dp = cat(dp, prod[J - h]);
+      std::vector<int> ids;
+      for (int a = 0; a < items; a += kPersistUpdItems)
+        ids.push_back(add(CRTask{kTkUP, J, h, a, std::min(kPersistUpdItems, items - a)}, dp));
+      lastw[J] = ids;
+    }
+  }
+  xprod[0] = add(CRTask{kTkTOP, 0, 0, 0, 1}, lastw[0]);
+  for (h /= 2; h >= 1; h /= 2) {
+    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
+    for (int o = 0; o < n_odd; ++o) {
+      const int I = h + 2 * h * o;
+      std::vector<int> dp = cat(prod[I], {xprod[I - h]});
+      if (I + h < p) dp.push_back(xprod[I + h]);
+      xprod[I] = add(CRTask{kTkBK, I, h, 0, 1}, dp);
+    }
+  }
+  if (T.size() > ps.cap_tasks || D.size() > ps.cap_deps || !ps.head) {
+    cr_persist_free(ps);
+    ps.cap_tasks = std::max<size_t>(T.size(), 64);
+    ps.cap_deps = std::max<size_t>(D.size(), 64);
+    if (hipMalloc(&ps.tasks, ps.cap_tasks * sizeof(CRTask)) != hipSuccess ||
+        hipMalloc(&ps.deps, ps.cap_deps * sizeof(int)) != hipSuccess ||
+        hipMalloc(&ps.done, ps.cap_tasks * sizeof(int)) != hipSuccess ||
+        hipMalloc(&ps.head, sizeof(unsigned long long)) != hipSuccess)
+      return -2;
+    if (hipMemset(ps.done, 0, ps.cap_tasks * sizeof(int)) != hipSuccess ||
+        hipMemset(ps.head, 0, sizeof(unsigned long long)) != hipSuccess)
+      return -2;
+    ps.qbase = 0;
+  }
+  if (hipMemcpy(ps.tasks, T.data(), T.size() * sizeof(CRTask), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(ps.deps, D.data(), std::max<size_t>(D.size(), 1) * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+    return -2;
+  ps.p = p;
+  ps.n = n;
+  ps.ntasks = (int)T.size();
+  ps.ndeps = (int)D.size();
+  ps.G = std::max(1, std::min(n_cu, ps.ntasks));
+  ps.h_tasks = std::move(T);
+  ps.h_deps = std::move(D);
+  return 0;
+}
+
+static void launch_cr_persist(const CRView &v, CRPersist &ps, hipStream_t st) {
+  ++ps.epoch;
+  hipLaunchKernelGGL(k_cr_persist, dim3(ps.G), dim3(aug::kThreads), sizeof(aug::Shared), st, v, ps.tasks, ps.deps,
+                     ps.ntasks, ps.done, ps.head, ps.qbase, ps.epoch);
+  ps.qbase += (unsigned long long)ps.ntasks + (unsigned long long)ps.G;  // every workgroup's last dequeue overshoots once
+}
+
 // SQLM_CR_TOP_SPLIT=1: the top factor and its back substitution as two launches (A/B)
 static bool top_split() {
   static const bool v = std::getenv("SQLM_CR_TOP_SPLIT") != nullptr;
@@ -1673,8 +2002,12 @@ static bool top_split() {
 
 // Levels, top solve and back substitution on D/E/g already in CR layout.
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p,
-                    int n, hipStream_t st) {
+                    int n, hipStream_t st, CRPersist *ps) {
   CRView v{p, n, 0, 0, D, E, A, C, g, x, flags, L};
+  if (ps && ps->p == p && ps->n == n && ps->tasks && cr_persist_enabled()) {
+    launch_cr_persist(v, *ps, st);
+    return;
+  }
   const size_t lds = cr_factor_lds(n);
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt;
   // SQLM_CR_UNFUSED=1: separate factor and elimination launches (A/B only)
@@ -1706,7 +2039,7 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
   }
 }
 
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather) {
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather, CRPersist *ps) {
   CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
   if (!d.cr_direct) {  // BSR S (sharded runs / row-kernel RCS): zero the superblocks and scatter
     const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
@@ -1716,7 +2049,7 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool 
     hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
   }
   if (pl.R) launch_arrow_solve(d, pl, st);
-  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
+  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st, ps);
   if (gather) hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }

@@ -33,7 +33,7 @@ EXPORTS = [
     "sqlm_kernel_timer_name", "sqlm_set_stereo",
     "sqlm_eg_set_problem", "sqlm_eg_optimize", "sqlm_eg_get_poses", "sqlm_eg_get_edge_chi2",
     "sqlm_eg_get_jacobians",
-    "sqlm_get_rcs_layout",
+    "sqlm_get_rcs_layout", "sqlm_get_exec_info",
 ]
 # every symbol include/sqrtlm_capture.h declares
 CAPTURE_EXPORTS = ["sqlm_capture_write", "sqlm_capture_read", "sqlm_capture_free", "sqlm_capture_replay",

@@ -104,6 +104,13 @@ class Context:
         return dict(kind=kind, B=out[1], p=out[2], n=out[3], border_cams=out[4], R=out[5], n_free=out[6],
                     coupled_superblocks=out[7])
 
+    def exec_info(self) -> dict:
+        """Device paths of the last optimize() (sqlm_get_exec_info)."""
+        out = (C.c_int * 8)()
+        check(lib().sqlm_get_exec_info(self._h, out), "sqlm_get_exec_info")
+        solve = {0: "none", 1: "cr_levels", 2: "cr_persistent", 3: "band+border", 4: "dense"}[out[1]]
+        return dict(obs_f32=bool(out[0]), solve=solve, persist_tasks=out[2], persist_grid=out[3])
+
     def bench(self, warmup: int, n: int, timers: bool = True):
         """(ms per LM iteration, per-phase ms from HIP events or {} without
         timers, stats). timers=False runs without the phase events."""

@@ -188,6 +188,13 @@ def test_eg_bench_size_first_iteration(gpu_ctx, oracle, monkeypatch):
     dense = gpu_ctx.eg_poses().copy()
     assert _rel(arrow, ref.Siw) < 1e-6 and _rel(dense, ref.Siw) < 1e-6
     assert _rel(arrow, dense) < 1e-9
+    # and against the oracle built on glibc's sin / cos / exp / log / acos (the
+    # reference's own libm; the oracle above shares the GPU's include/sqlm_libm.h)
+    ref_glibc = oracle.OracleEG(pg, glibc=True)
+    _, sgl = ref_glibc.optimize(1, 1e-16)
+    assert sgl["trace_trials"] == sg["trace_trials"]
+    assert _rel(arrow, ref_glibc.Siw) < 1e-6 and _rel(dense, ref_glibc.Siw) < 1e-6
+    assert abs(sg["chi2_end"] - sgl["chi2_end"]) <= 1e-8 * sgl["chi2_begin"]
 
 
 def _oracle_jacobians(oracle, pg):

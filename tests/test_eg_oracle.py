@@ -118,3 +118,62 @@ def test_shared_libm_within_one_ulp_of_glibc(oracle):
         y, r = oracle.libm(fn, x), ref[fn](x)
         ulp = np.abs(y.view(np.int64) - r.view(np.int64))
         assert ulp.max() <= 1, (fn, x[ulp.argmax()], y[ulp.argmax()], r[ulp.argmax()])
+
+
+def test_shared_libm_trig_range_limit(oracle):
+    """sqlm_sin / sqlm_cos reduce with fdlibm's medium-range algorithm only:
+    within 1 ulp of glibc up to 2^20 pi/2, NaN beyond (a rotation that large is
+    a wild trial step: its chi2 is NaN and the step is rejected)."""
+    lim = np.ldexp(np.pi / 2, 20)
+    x = np.array([np.ldexp(np.pi / 2, 19), lim * (1 - 1e-15), -lim * (1 - 1e-15), 1.3e6, -1.6e6, 12345.678])
+    for fn, ref in (("sin", np.sin), ("cos", np.cos)):
+        y, r = oracle.libm(fn, x), ref(x)
+        ulp = np.abs(y.view(np.int64) - r.view(np.int64))
+        assert ulp.max() <= 1, (fn, x[ulp.argmax()])
+        big = np.array([lim * (1 + 1e-6), 2.0 ** 31, -1e9, 1e300])
+        assert np.all(np.isnan(oracle.libm(fn, big))), fn
+
+
+def test_glibc_build_uses_platform_libm(oracle):
+    """liboracle_glibc.so really computes with glibc (orc_libm there = np's)."""
+    import ctypes as C
+    x = np.linspace(-3.0, 3.0, 4097)
+    y = np.zeros_like(x)
+    oracle.lib(glibc=True).orc_libm(2, x.ctypes.data_as(C.c_void_p), y.ctypes.data_as(C.c_void_p), x.size)
+    np.testing.assert_array_equal(y, np.sin(x))
+
+
+@pytest.mark.parametrize("fix_scale", [True, False])
+def test_shared_libm_oracle_matches_glibc_oracle_first_iteration(oracle, fix_scale):
+    """The essential-graph oracle on include/sqlm_libm.h (the GPU's libm)
+    against the same restatement on glibc (the reference's libm) on the
+    1,500-keyframe bench graph: the first LM iteration (lambda 1e-16, a
+    Gauss-Newton step) within the north-star 1e-6, chi2 within 1e-8 -- the
+    shared-libm change cannot hide a divergence from the reference's
+    arithmetic (tests/test_eg_gpu.py pins the GPU to this build too).
+    Free scale (monocular Sim3) is the exception the reference itself makes:
+    there ONE input moved by one ulp moves the first step by 4e-4 (measured:
+    the 7-DoF system of this graph is far worse conditioned), so the two libms
+    are held to 10x that own spread instead (measured 8.9e-4 vs 4.3e-4); the
+    fixed-scale bench graph differs by 1.0e-7."""
+    pg = synth.make_pose_graph(1500, window=8, n_loops=20, seed=5, fix_scale=fix_scale)
+    a, b = oracle.OracleEG(pg), oracle.OracleEG(pg, glibc=True)
+    na, sa = a.optimize(1, 1e-16)
+    nb, sb = b.optimize(1, 1e-16)
+    assert na == nb and sa["trace_trials"] == sb["trace_trials"]
+
+    def rel(x, y):
+        return np.abs(x - y).max() / max(1.0, np.abs(y).max())
+
+    if fix_scale:
+        assert rel(a.Siw, b.Siw) < 1e-6, rel(a.Siw, b.Siw)
+        assert abs(sa["chi2_end"] - sb["chi2_end"]) <= 1e-8 * sb["chi2_begin"]
+    else:
+        spread = 0.0
+        for r, c in ((0, 4), (5, 0), (100, 2)):
+            p2 = pg.copy()
+            p2.Sji[r, c] = np.nextafter(p2.Sji[r, c], 1e9)
+            g = oracle.OracleEG(p2)
+            g.optimize(1, 1e-16)
+            spread = max(spread, rel(g.Siw, a.Siw))
+        assert rel(a.Siw, b.Siw) < 10.0 * spread, (rel(a.Siw, b.Siw), spread)

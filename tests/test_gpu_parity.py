@@ -210,3 +210,36 @@ def test_config4_full_size_gba_schedule(gpu_ctx, oracle):
     # size-independent properties of the full run: chi2 falls, every edge active
     assert sg["trace_chi2"][-1] < sg["trace_chi2"][0] < sg["chi2_begin"]
     assert sg["n_active_edges"] == prob.n_obs
+
+
+@pytest.mark.parametrize("what", ["uv", "info", "delta"])
+def test_double_inputs_path(gpu_ctx, oracle, what):
+    """Observation inputs that are not all float32 values (a keypoint, an
+    invSigma2 or a Huber threshold computed in double by a caller) take the
+    double arrays instead of the float4 stream (DevProblem::obs_f32 = 0: the
+    second gather into the obs_uv / obs_info / obs_delta arrays, cam_uv, the
+    double branches of load_obs, k_camera_pass and k_cam_gather). One value
+    nudged off float32 by one double ulp: same oracle parity as the float
+    path, and sqlm_get_exec_info confirms which path ran."""
+    prob = synth.make_problem(14, 400, pair_window=4, n_fixed=3, seed=5, robust=True)
+    if what == "uv":
+        prob.obs_uv[7, 0] = np.nextafter(prob.obs_uv[7, 0], np.inf)
+    elif what == "info":
+        prob.obs_info[11] = np.nextafter(prob.obs_info[11], np.inf)
+    else:
+        k = int(np.flatnonzero(prob.obs_delta > 0)[3])
+        prob.obs_delta[k] = np.nextafter(prob.obs_delta[k], np.inf)
+    assert np.float32(prob.obs_uv[7, 0]) != prob.obs_uv[7, 0] or what != "uv"
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(0, 10)
+    gpu_ctx.set_problem(prob)
+    ng, sg = gpu_ctx.optimize(0, 10)
+    assert gpu_ctx.exec_info()["obs_f32"] is False
+    assert ng == nr
+    _compare_stats(sg, sr)
+    _compare_state(gpu_ctx, ref)
+    np.testing.assert_allclose(gpu_ctx.edge_chi2(), ref.edge_chi2(), rtol=1e-6, atol=1e-9)
+    # the unmodified problem runs the float4 path
+    gpu_ctx.set_problem(synth.make_problem(14, 400, pair_window=4, n_fixed=3, seed=5, robust=True))
+    gpu_ctx.optimize(0, 2)
+    assert gpu_ctx.exec_info()["obs_f32"] is True

@@ -137,15 +137,21 @@ int main(int argc, char **argv) {
                   emax, zmax);
     }
   }
-  const int one = 1;
+  const int one[4] = {1, 0, 0, 0};
+  // the persistent solve (one launch; SQLM_CR_PERSIST=0: the per-level launches)
+  sqlm::CRPersist ps;
+  int ncu = 0;
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  if (sqlm::cr_persist_plan(ps, p, n, ncu)) { std::printf("persist plan failed\n"); return 2; }
+  std::printf("{\"persist_tasks\": %d, \"persist_deps\": %d, \"persist_grid\": %d}\n", ps.ntasks, ps.ndeps, ps.G);
   double best = 1e30, sum = 0.0;
   for (int it = 0; it < reps + 2; ++it) {  // 2 warmups
     CK(hipMemcpyAsync(dD, D.data(), nb * 8, hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(dE, E.data(), nb * 8, hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice, st));
-    CK(hipMemcpyAsync(dflags, &one, 4, hipMemcpyHostToDevice, st));
+    CK(hipMemcpyAsync(dflags, one, 16, hipMemcpyHostToDevice, st));
     CK(hipEventRecord(e0, st));
-    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st);
+    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st, &ps);
     CK(hipEventRecord(e1, st));
     CK(hipStreamSynchronize(st));
     CK(hipGetLastError());
@@ -154,9 +160,28 @@ int main(int argc, char **argv) {
     if (it >= 2) { best = std::min(best, (double)ms); sum += ms; }
   }
   std::vector<double> x(g.size());
-  int flag = 0;
+  int flag = 0, fl[4] = {0, 0, 0, 0};
   CK(hipMemcpy(x.data(), dx, x.size() * 8, hipMemcpyDeviceToHost));
-  CK(hipMemcpy(&flag, dflags, 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(fl, dflags, 16, hipMemcpyDeviceToHost));
+  flag = fl[0];
+  {  // the same system through the per-level launches: the persistent solve must give the same bits
+    CK(hipMemcpy(dD, D.data(), nb * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dE, E.data(), nb * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dflags, one, 16, hipMemcpyHostToDevice));
+    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st, nullptr);
+    CK(hipStreamSynchronize(st));
+    std::vector<double> x2(g.size());
+    CK(hipMemcpy(x2.data(), dx, x2.size() * 8, hipMemcpyDeviceToHost));
+    size_t ndiff = 0;
+    double dmax = 0.0;
+    for (size_t k = 0; k < x.size(); ++k) {
+      ndiff += x[k] != x2[k];
+      dmax = std::max(dmax, std::fabs(x[k] - x2[k]));
+    }
+    std::printf("{\"persist_vs_levels\": {\"differing\": %zu, \"max_abs\": %.3e}, \"dev_err\": %d}\n", ndiff, dmax,
+                fl[1]);
+  }
   if (p == 2 && std::getenv("SQLM_CR_LEGACY")) {  // stage-by-stage host check of the one-level solve (Linv layout)
     std::vector<double> dDh(nb), dLh(nb), dAh(nb), dgh(g.size());
     CK(hipMemcpy(dDh.data(), dD, nb * 8, hipMemcpyDeviceToHost));
