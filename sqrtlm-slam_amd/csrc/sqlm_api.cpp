@@ -148,6 +148,10 @@ struct sqlm_ctx {
   // synchronize; SQLM_NO_MBOX=1 (A/B), timing runs and sharded runs copy
   double *mbox = nullptr, *mbox_dev = nullptr;
   unsigned long long mbox_seq = 0;
+  // device-side LM loop: the control state on the device, its page-locked
+  // host image, and a mapped word the host mirrors the caller's stop flag into
+  LMCtl *ctl_dev = nullptr, *ctl_host = nullptr;
+  int *stop_map = nullptr, *stop_map_dev = nullptr;
   // SQLM_HOST_TRACE=1: host-side time points of every trial (diagnostic)
   bool htrace = false;
   std::chrono::steady_clock::time_point ht_prev{};
@@ -1656,8 +1660,10 @@ inline void hmark(sqlm_ctx *c, int i) {
   c->ht_prev = now;
 }
 
-// setLambda + BlockSolver::solve + update + restoreDiagonal + computeActiveErrors.
-int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
+// setLambda + BlockSolver::solve + update + restoreDiagonal + computeActiveErrors,
+// enqueued up to (not including) the trial scalars' reduction. cam_after: the
+// speculative camera pass is still to go behind k_reduce.
+int trial_launch(sqlm_ctx *c, double lambda, bool &cam_after) {
   DevProblem &d = c->d;
   hmark(c, 0);  // since the previous trial's scalars arrived: the host's decision
   tmark(c, 2, false);
@@ -1735,7 +1741,7 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
   // host's decision and the next trial; small problems (cam_inline) keep it on
   // the context stream behind k_reduce instead -- the fork / join costs the
   // host more than the overlap saves there
-  const bool cam_after = c->spec && c->cam_inline && !c->timing;
+  cam_after = c->spec && c->cam_inline && !c->timing;
   if (c->spec && !cam_after) {
     if (!c->cam_inline) {
       HIP_OK(hipEventRecord(c->ev_spec_fork, c->stream));
@@ -1748,6 +1754,13 @@ int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
       c->spec_outstanding = true;
     }
   }
+  return SQLM_OK;
+}
+
+int trial(sqlm_ctx *c, double lambda, TrialOut &o) {
+  bool cam_after = false;
+  int s = trial_launch(c, lambda, cam_after);
+  if (s) return s;
   tmark(c, 7, false);
   hmark(c, 5);  // speculative camera pass
   s = reduce_and_fetch(c, o, cam_after);
@@ -1787,6 +1800,93 @@ void flush_cam_timers(sqlm_ctx *c) {
   }
 }
 
+// Host loop: every trial's scalars come back before the next trial is
+// enqueued, and the host applies lm_decide (the timing run, sharded runs, the
+// row-kernel RCS fallback, SQLM_NO_DLM=1).
+int lm_host(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
+  while (!L.done) {
+    if (L.qmax == 0 && L.its > 0) {  // the next iteration (sparse_optimizer.cpp:376-414)
+      if (stopped(stop)) break;
+      c->need_maxdiag = false;
+      if (int s = linearize(c)) return s;
+    }
+    TrialOut o{};
+    if (int s = trial(c, L.lambda, o)) return s;
+    if (o.dev_err) return SQLM_ERR_HIP;  // a solve gave up a bounded wait (the step was rejected on the device too)
+    if (L.qmax == 0) acc_events(c, 0, c->lin_timers);
+    if (lm_decide(L, o.chi_cur, o.chi_new, o.scale, o.ok, stopped(stop))) swap_state(c);
+    if (L.qmax == 0) c->kernel_ms_n++;  // an iteration ended
+  }
+  return SQLM_OK;
+}
+
+// Device loop: k_reduce applies lm_decide to each trial on the device and the
+// trial kernels take lambda, the state parity and the done flag from
+// DevProblem::ctl, so the host enqueues trial t+1 while trial t runs (no
+// host round trip between trials: the ~25 us turnaround of a local-BA trial).
+// At most two trials are outstanding; the one enqueued past the end returns
+// from every kernel at once. The caller's stop flag is mirrored into a mapped
+// word the decision reads.
+bool dlm_ok(const sqlm_ctx *c) {
+  static const bool off = std::getenv("SQLM_NO_DLM") != nullptr;
+  return !off && c->ctl_dev && c->ctl_host && c->mbox && c->stop_map_dev && c->spec && c->use_tiles && !c->timing && !c->htrace &&
+         !c->comm.enabled();
+}
+
+int lm_device(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
+  constexpr int kAhead = 2;
+  DevProblem &d = c->d;
+  *c->stop_map = stopped(stop) ? 1 : 0;
+  L.stop_src = c->stop_map_dev;
+  L.par = L.par_trial = 0;
+  HIP_OK(hipMemcpyAsync(c->ctl_dev, &L, sizeof(LMCtl), hipMemcpyHostToDevice, c->stream));
+  d.ctl = c->ctl_dev;
+  const long long max_trials = 10LL * L.iterations;
+  const unsigned long long *slot = reinterpret_cast<const unsigned long long *>(c->mbox + kMboxSeq);
+  long long enq = 0, obs = 0;
+  unsigned long long last_seq = 0;
+  int s = SQLM_OK;
+  bool dev_err = false;
+  while (s == SQLM_OK) {
+    while (enq < max_trials && enq - obs < kAhead) {
+      bool cam_after = false;
+      if ((s = trial_launch(c, L.lambda, cam_after))) break;
+      last_seq = ++c->mbox_seq;
+      launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream,
+                    c->mbox_dev, last_seq);
+      if (cam_after && (s = spec_camera_pass(c, c->stream))) break;
+      ++enq;
+    }
+    if (s || obs == enq) break;
+    // the mailbox of trial `obs` (or of a later one: the done flag is sticky)
+    const unsigned long long want = last_seq - (unsigned long long)(enq - obs - 1);
+    Timer t;
+    for (unsigned it = 1; __atomic_load_n(slot, __ATOMIC_ACQUIRE) < want; ++it) {
+      if ((it & 1023) == 0) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q == hipSuccess && __atomic_load_n(slot, __ATOMIC_ACQUIRE) < want) { s = SQLM_ERR_HIP; break; }
+        if ((q != hipSuccess && q != hipErrorNotReady) || t.ms() > 60000.0) { s = SQLM_ERR_HIP; break; }
+        *c->stop_map = stopped(stop) ? 1 : 0;
+      }
+      __builtin_ia32_pause();
+    }
+    if (s) break;
+    obs = enq - (long long)(last_seq - __atomic_load_n(slot, __ATOMIC_ACQUIRE));
+    *c->stop_map = stopped(stop) ? 1 : 0;
+    if (c->mbox[kDevErr] != 0.0) dev_err = true;
+    if (dev_err || c->mbox[kLmDone] != 0.0) break;
+  }
+  d.ctl = nullptr;
+  // the state the device ended in (traces, parity), after every enqueued trial
+  HIP_OK(hipMemcpyAsync(&L, c->ctl_dev, sizeof(LMCtl), hipMemcpyDeviceToHost, c->stream));
+  HIP_OK(hipStreamSynchronize(c->stream));
+  if (s) return s;
+  if (dev_err || c->mbox[kDevErr] != 0.0) return SQLM_ERR_HIP;
+  if (L.par & 1) swap_state(c);  // the host's view of the buffers follows the device's parity
+  c->kernel_ms_n += L.its;
+  return SQLM_OK;
+}
+
 // The Levenberg–Marquardt loop of g2o (levenberg.cpp:61-164 inside
 // sparse_optimizer.cpp:376-414). `bench` keeps iterating after Terminate so a
 // fixed number of iterations can be timed.
@@ -1796,76 +1896,32 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
   if (!st) st = &local;
   std::memset(st, 0, sizeof(*st));
   st->n_active_edges = c->n_active_edges;
-  double lambda = -1., ni = 2.;
-  int nbad = 0, its = 0, result = 0;
   c->lin_valid = false;  // iteration 0 linearizes in full (lambda_0 needs max diag H)
   Timer tt;
-  for (int it = 0; it < iterations && !stopped(stop) && (result == 0 || bench); ++it) {
+  static thread_local LMCtl local_ctl;  // (no page-locked image: host loop only)
+  LMCtl &L = c->ctl_host ? *c->ctl_host : local_ctl;
+  std::memset(&L, 0, sizeof(LMCtl));
+  L.iterations = iterations;
+  L.bench = bench ? 1 : 0;
+  L.done = iterations <= 0 || stopped(stop);
+  if (!L.done) {
     Timer tl;
-    c->need_maxdiag = it == 0;
+    c->need_maxdiag = true;
     int s = linearize(c);
     if (s) return s;
-    double currentChi = 0.0;
-    if (it == 0) {
-      TrialOut o0{};
-      s = reduce_and_fetch(c, o0);
-      c->need_maxdiag = false;
-      if (s) return s;
-      currentChi = o0.chi_cur;
-      st->chi2_begin = currentChi;
-      lambda = user_lambda > 0 ? user_lambda : 1e-5 * o0.maxdiag;
-      ni = 2;
-      nbad = 0;
-    }
+    TrialOut o0{};
+    s = reduce_and_fetch(c, o0);
+    c->need_maxdiag = false;
+    if (s) return s;
+    L.currentChi = L.iniChi = o0.chi_cur;  // computeActiveErrors at iteration 0 (levenberg.cpp:66-97)
+    st->chi2_begin = o0.chi_cur;
+    L.lambda = user_lambda > 0 ? user_lambda : 1e-5 * o0.maxdiag;  // computeLambdaInit
+    L.ni = 2;
     st->ms_linearize += tl.ms();
     Timer tr;
-    double iniChi = currentChi, tempChi = currentChi, rho = 0;
-    int qmax = 0;
-    do {
-      TrialOut o{};
-      s = trial(c, lambda, o);
-      if (s) return s;
-      if (o.dev_err) return SQLM_ERR_HIP;  // the step was rejected on the device too (flags[0] = 0)
-      if (qmax == 0 && it > 0) { currentChi = o.chi_cur; iniChi = currentChi; }
-      if (qmax == 0) acc_events(c, 0, c->lin_timers);
-      tempChi = o.chi_new;
-      if (!o.ok) tempChi = std::numeric_limits<double>::max();
-      rho = (currentChi - tempChi);
-      double scale = o.ok ? o.scale : 0.0;
-      scale += 1e-3;
-      rho /= scale;
-      if (rho > 0 && std::isfinite(tempChi)) {
-        double alpha = 1. - std::pow((2 * rho - 1), 3);
-        alpha = std::min(alpha, 2. / 3.);
-        const double scaleFactor = std::max(1. / 3., alpha);
-        lambda *= scaleFactor;
-        ni = 2;
-        currentChi = tempChi;
-        swap_state(c);
-      } else {
-        lambda *= ni;
-        ni *= 2;
-      }
-      qmax++;
-      st->trials++;
-    } while (rho < 0 && qmax < 10 && !stopped(stop));
+    s = dlm_ok(c) ? lm_device(c, L, stop) : lm_host(c, L, stop);
+    if (s) return s;
     st->ms_trials += tr.ms();
-    c->kernel_ms_n++;
-    if (qmax == 10 || rho == 0) result = 1;
-    else {
-      if ((iniChi - currentChi) * 1e3 < iniChi) nbad++;
-      else nbad = 0;
-      if (nbad >= 3) result = 1;
-    }
-    if (its < SQLM_TRACE_MAX) {
-      st->trace_chi2[its] = currentChi;
-      st->trace_lambda[its] = lambda;
-      st->trace_trials[its] = qmax;
-      st->trace_len = its + 1;
-    }
-    st->chi2_end = currentChi;
-    st->lambda_end = lambda;
-    ++its;
   }
   if (c->spec_outstanding) {  // nothing of a speculative pass outlives the run
     HIP_OK(hipStreamWaitEvent(c->stream, c->ev_spec_join, 0));
@@ -1880,10 +1936,19 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
     std::memset(c->ht_acc, 0, sizeof(c->ht_acc));
     c->ht_n = 0;
   }
-  st->iterations = its;
-  st->result = result;
+  st->iterations = L.its;
+  st->trials = L.trials;
+  st->result = L.result;
+  st->chi2_end = L.chi2_end;
+  st->lambda_end = L.lambda_end;
+  st->trace_len = std::min(L.its, SQLM_TRACE_MAX);
+  for (int k = 0; k < st->trace_len; ++k) {
+    st->trace_chi2[k] = L.trace_chi2[k];
+    st->trace_lambda[k] = L.trace_lambda[k];
+    st->trace_trials[k] = L.trace_trials[k];
+  }
   st->ms_total = tt.ms();
-  if (n_iter) *n_iter = its;
+  if (n_iter) *n_iter = L.its;
   return SQLM_OK;
 }
 
@@ -1989,6 +2054,13 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   } else {
     c->mbox = nullptr;
   }
+  if (hipMalloc((void **)&c->ctl_dev, sizeof(LMCtl)) != hipSuccess ||
+      hipHostMalloc((void **)&c->ctl_host, sizeof(LMCtl)) != hipSuccess)
+    c->ctl_dev = nullptr;  // no device loop: the host decides every trial
+  if (hipHostMalloc((void **)&c->stop_map, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+    *c->stop_map = 0;
+    if (hipHostGetDevicePointer((void **)&c->stop_map_dev, c->stop_map, 0) != hipSuccess) c->stop_map_dev = nullptr;
+  }
   // timing-only events: no system-scope fence, which would flush caches and
   // leave a ~10 us bubble between the kernels they separate
   for (auto &e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
@@ -2027,6 +2099,9 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
   if (c->mbox) (void)hipHostFree(c->mbox);
+  if (c->ctl_dev) (void)hipFree(c->ctl_dev);
+  if (c->ctl_host) (void)hipHostFree(c->ctl_host);
+  if (c->stop_map) (void)hipHostFree(c->stop_map);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_spec_fork) (void)hipEventDestroy(c->ev_spec_fork);

@@ -4,7 +4,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cfloat>
+#include <cmath>
 #include <vector>
+
+#include "../../include/sqrtlm.h"
 
 namespace sqlm {
 
@@ -19,6 +23,87 @@ constexpr int kTileMaxCams = SQLM_TILE_MAXCAMS, kTileHardCams = 24, kTileMaxLm =
 constexpr int kTileNtMax = (6 * kTileHardCams + 15) / 16;  // widest tile class (9)
 
 constexpr int kBlock = 256;
+
+// ---- Levenberg-Marquardt control (optimization_algorithm_levenberg.cpp:61-164
+// inside sparse_optimizer.cpp:376-414) -------------------------------------
+// One state for the host loop and the device loop (k_reduce decides on the
+// device when the trials are enqueued ahead, DevProblem::ctl): both apply the
+// same lm_decide, so both make the same decisions bit for bit.
+struct LMCtl {
+  double lambda, ni, currentChi, iniChi;
+  double chi2_end, lambda_end;
+  int qmax, nbad, its, result, trials, iterations, bench;
+  int par;        // device loop: state buffers swapped iff odd (flipped on accept)
+  int par_trial;  // the parity the current trial's kernels run under (written by k_pose_update)
+  int done;       // the run is over: the kernels of a later trial return at once
+  int accepted;   // the last trial was accepted
+  int stop;       // the caller's stop flag as the device saw it
+  const volatile int *stop_src;  // mapped page-locked word the host mirrors the stop flag into
+  double trace_chi2[SQLM_TRACE_MAX], trace_lambda[SQLM_TRACE_MAX];
+  int trace_trials[SQLM_TRACE_MAX];
+};
+
+// (2 rho - 1)^3 of levenberg.cpp:136 (std::pow there): the exact cube rounded
+// once (two-product error terms), one formula for host and device
+__host__ __device__ inline double lm_cube(double x) {
+  const double p = x * x, e = fma(x, x, -p);   // x^2 = p + e exactly
+  const double q = p * x, f = fma(p, x, -q);   // p x = q + f exactly
+  if (!isfinite(q)) return q;                   // +-inf / NaN as pow gives them
+  return q + (f + e * x);
+}
+
+// One trial's outcome (computeActiveErrors chi2 at the trial state, the
+// predicted reduction scale, the solve status) applied to the LM state:
+// levenberg.cpp:110-160 (rho, lambda update, accept) and the iteration end of
+// sparse_optimizer.cpp:376-414 with levenberg.cpp:150-163 (Terminate on
+// qmax == 10 or rho == 0, Raul's criterion). Returns true if the trial state
+// is accepted (the caller swaps the state buffers).
+__host__ __device__ inline bool lm_decide(LMCtl &c, double chi_cur, double chi_new, double scale, bool ok, bool stop) {
+  if (c.qmax == 0 && c.its > 0) {  // a fresh linearization's computeActiveErrors
+    c.currentChi = chi_cur;
+    c.iniChi = chi_cur;
+  }
+  const double tempChi = ok ? chi_new : DBL_MAX;
+  double rho = c.currentChi - tempChi;
+  const double scl = (ok ? scale : 0.0) + 1e-3;
+  rho /= scl;
+  bool acc = false;
+  if (rho > 0 && isfinite(tempChi)) {
+    double alpha = 1. - lm_cube(2 * rho - 1);
+    alpha = (2. / 3. < alpha) ? 2. / 3. : alpha;         // std::min(alpha, 2/3)
+    const double sf = (1. / 3. < alpha) ? alpha : 1. / 3.;  // std::max(1/3, alpha)
+    c.lambda *= sf;
+    c.ni = 2;
+    c.currentChi = tempChi;
+    acc = true;
+  } else {
+    c.lambda *= c.ni;
+    c.ni *= 2;
+  }
+  c.qmax++;
+  c.trials++;
+  c.accepted = acc ? 1 : 0;
+  if (!(rho < 0 && c.qmax < 10 && !stop)) {  // the iteration ends
+    if (c.qmax == 10 || rho == 0) {
+      c.result = 1;
+    } else {
+      if ((c.iniChi - c.currentChi) * 1e3 < c.iniChi) c.nbad++;
+      else c.nbad = 0;
+      if (c.nbad >= 3) c.result = 1;
+    }
+    if (c.its < SQLM_TRACE_MAX) {
+      c.trace_chi2[c.its] = c.currentChi;
+      c.trace_lambda[c.its] = c.lambda;
+      c.trace_trials[c.its] = c.qmax;
+    }
+    c.chi2_end = c.currentChi;
+    c.lambda_end = c.lambda;
+    c.its++;
+    c.qmax = 0;
+    c.done = c.its >= c.iterations || stop || (c.result != 0 && !c.bench);
+  }
+  return acc;
+}
 
 // HBM layout of one optimize() call. Everything is FP64 except indices.
 //   poses     : all problem poses, index = pose id (ascending id = g2o order)
@@ -151,10 +236,13 @@ struct DevProblem {
   int px_lm = 0, px_lid = 0;                //   ... and of the speculative one (swapped on accept)
   double *scalars = nullptr;                // [8] see Scalar
   unsigned long long *maxdiag = nullptr;    // bit pattern of a non-negative double
-  int *flags = nullptr;                     // [4] solve_ok ...
+  int *flags = nullptr;                     // [4] solve_ok, device error, ...
+  // device-side LM loop (trials enqueued ahead of their decisions): the trial
+  // kernels take lambda, the state parity and the done flag from here
+  LMCtl *ctl = nullptr;
 };
 
-enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kDevErr = 5, kNScalars = 8 };
+enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kDevErr = 5, kLmDone = 6, kNScalars = 8 };
 constexpr int kMboxSeq = 7;  // host mailbox: the scalars, then the sequence number in slot 7
 
 // partial-sum slots
@@ -292,11 +380,12 @@ struct CRPersist {
 // SQLM_CR_PERSIST=1 selects it (until validated on MI355X: per-level launches by default)
 bool cr_persist_enabled();
 int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu);  // 0 ok, -2 HIP error
+void cr_persist_graph(int p, int n, std::vector<CRTask> &tasks, std::vector<int> &deps);  // host only
 void cr_persist_free(CRPersist &ps);
 // CR levels + top + back substitution on blocks already in CR layout; ps
 // (planned for this p, n): one persistent launch, else the per-level launches
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
-                    hipStream_t st, CRPersist *ps = nullptr);
+                    hipStream_t st, CRPersist *ps = nullptr, const int *skip = nullptr);
 // Dense SPD solve (sqlm_rcs_solve.hip): A (n x n, lower, n % kCRMaxN == 0) is
 // factored in place into L (+ diagonal block inverses Linv), r is consumed,
 // x = A^-1 r; flags[0] is cleared on a non-positive pivot. band > 0: A is a

@@ -32,6 +32,40 @@
 
 namespace sqlm {
 
+// ---- device-side LM loop (DevProblem::ctl) ------------------------------------
+// The trials are enqueued ahead of their decisions (k_reduce decides), so the
+// state buffer pairs cannot be swapped on the host: a trial kernel swaps its
+// own copy of the pointers when the parity it runs under is odd, takes lambda
+// from ctl, and returns at once when the run is over (a trial enqueued past
+// the end must change nothing a caller can read).
+__device__ __forceinline__ void lm_swap(DevProblem &d, int par) {
+  if (!(par & 1)) return;
+  auto sw = [](auto &a, auto &b) {
+    const auto t = a;
+    a = b;
+    b = t;
+  };
+  sw(d.pose_qt[0], d.pose_qt[1]);
+  sw(d.pose_rt[0], d.pose_rt[1]);
+  sw(d.X[0], d.X[1]);
+  sw(d.lm_R, d.lm_R_nx);
+  sw(d.lm_b, d.lm_b_nx);
+  sw(d.obs_s, d.obs_s_nx);
+  sw(d.Hpp, d.Hpp_nx);
+  sw(d.bp, d.bp_nx);
+  sw(d.pc_lm, d.px_lm);
+  sw(d.pc_lid, d.px_lid);
+}
+// false: the run is over, return. trial_par: the parity of the trial the
+// speculative camera pass belongs to (the decision may already have flipped par)
+__device__ __forceinline__ bool lm_enter(DevProblem &d, bool trial_par = false) {
+  if (!d.ctl) return true;
+  if (d.ctl->done) return false;
+  lm_swap(d, trial_par ? d.ctl->par_trial : d.ctl->par);
+  return true;
+}
+__device__ __forceinline__ double lm_lam(const DevProblem &d, double lambda) { return d.ctl ? d.ctl->lambda : lambda; }
+
 // ---------------------------------------------------------------- helpers
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -502,8 +536,10 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
 // into Hpp_nx / bp_nx, launched after k_landmark_update<SPEC>.
 template <bool ST>
 __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
+  if (!lm_enter(d, true)) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int sb = spec ? 1 : 0;
+  const double *pose_rt_s = spec ? d.pose_rt[1] : d.pose_rt[0], *X_s = spec ? d.X[1] : d.X[0];
+  const double *pose_qt_s = spec ? d.pose_qt[1] : d.pose_qt[0];
   const int i = blockIdx.x * 4 + wave;
   double H[21], b[6], chi = 0.0;
 #pragma unroll
@@ -511,10 +547,10 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
 #pragma unroll
   for (int k = 0; k < 6; ++k) b[k] = 0.0;
   if (i < d.nP) {
-    const double *prt = d.pose_rt[sb] + 16 * d.hidx_pose[i];
+    const double *prt = pose_rt_s + 16 * d.hidx_pose[i];
     const double bf = ST ? d.pose_bf[d.hidx_pose[i]] : 0.0;
     for (int t = d.cam_obs_ptr[i] + lane; t < d.cam_obs_ptr[i + 1]; t += 64) {
-      const double *X = d.X[sb] + 4 * d.cam_slot[t];
+      const double *X = X_s + 4 * d.cam_slot[t];
       double2 uv, id;
       if (d.obs_f32) {
         const float4 q = *reinterpret_cast<const float4 *>(d.cam_q + 4 * (int64_t)t);
@@ -555,7 +591,7 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
     }
     if (d.nLid > 0) {
       const int p = d.hidx_pose[i];
-      const double *qt = d.pose_qt[sb] + 8 * p;
+      const double *qt = pose_qt_s + 8 * p;
       const double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t3[3] = {qt[4], qt[5], qt[6]};
       for (int t = d.lid_cam_ptr[i] + lane; t < d.lid_cam_ptr[i + 1]; t += 64) {
         const double *L = d.lid_data + 12 * t;
@@ -999,6 +1035,8 @@ constexpr int tile_occ() {
 template <int NT, bool ST>
 __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_tile(DevProblem d, double lambda,
                                                                                    int cls_off) {
+  if (!lm_enter(d)) return;
+  lambda = lm_lam(d, lambda);
   // wave w owns the accumulator tiles q with q % kTileWaves == w; 3 waves per SIMD
   // for mono problems (167 VGPRs), 2 with the stereo row (spill-free)
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
@@ -1341,6 +1379,8 @@ constexpr int kRedThreads = SQLM_RED_THREADS;
 constexpr int kRedGroupsS = kRedThreads / 36, kRedGroupsG = kRedThreads / 6;
 
 __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double lambda, int short_blocks) {
+  if (!lm_enter(d)) return;
+  lambda = lm_lam(d, lambda);
   if ((int)blockIdx.x >= short_blocks) {  // one long S block or g row per workgroup
     __shared__ double part[kRedThreads];
     const int w = blockIdx.x - short_blocks, tid = threadIdx.x;
@@ -1507,6 +1547,14 @@ int launch_dense_solve(const DevProblem &d, hipStream_t st) {
 // dx for the landmark update -- the k_cr_gather step folded into this launch.
 template <bool CR>
 __global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda) {
+  if (d.ctl) {
+    if (d.ctl->done) return;
+    // the parity this trial runs under, for its speculative camera pass (which
+    // may run after the decision has flipped par)
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctl->par_trial = d.ctl->par;
+  }
+  lm_enter(d);
+  lambda = lm_lam(d, lambda);
   __shared__ double red[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double sc = 0.0;
@@ -1571,6 +1619,8 @@ constexpr int kUpdWin = 64;
 template <int W, bool ST, bool SPEC>
 __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : 4) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
                                                          double lambda, int part_off, const int2 *rng) {
+  if (!lm_enter(d)) return;
+  lambda = lm_lam(d, lambda);
   __shared__ double red[4];
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
   constexpr int SPB = kBlock / W;
@@ -1737,6 +1787,7 @@ void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda,
 }
 
 __global__ __launch_bounds__(256) void k_lidar_chi2(DevProblem d) {
+  if (!lm_enter(d)) return;
   __shared__ double red[4];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double chi = 0.0;
@@ -1771,6 +1822,8 @@ constexpr int kReduceThreads = 1024;
 __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam,
                                                           int n_lid, double *mbox, unsigned long long seq) {
   __shared__ double red[6][kReduceThreads / 64];
+  const bool dlm = d.ctl != nullptr, live = dlm && !d.ctl->done;
+  if (live) lm_swap(d, d.ctl->par);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const double *p = d.partials;
   const double *base[6] = {p + d.pc_lm, p + d.pc_lid, p + kPartChiNewLm, p + kPartChiNewLid, p + kPartScaleCam,
@@ -1813,6 +1866,14 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
     *d.maxdiag = 0ull;  // ready for the next linearization's atomicMax
     d.scalars[kSolveOk] = (double)d.flags[0];
     d.scalars[kDevErr] = (double)d.flags[1];
+    if (live) {  // the trial's decision on the device (the host only watches)
+      LMCtl &c = *d.ctl;
+      const int stop = c.stop_src ? __hip_atomic_load(c.stop_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+      c.stop = stop;
+      const bool ok = d.flags[0] != 0 && d.flags[1] == 0;
+      if (lm_decide(c, part[0] + part[1], part[2] + part[3], part[4] + part[5], ok, stop != 0)) c.par ^= 1;
+    }
+    d.scalars[kLmDone] = dlm ? (double)d.ctl->done : 0.0;
     if (mbox) {
       mbox[kChiCur] = part[0] + part[1];
       mbox[kChiNew] = part[2] + part[3];
@@ -1820,6 +1881,7 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
       mbox[kMaxDiag] = d.scalars[kMaxDiag];
       mbox[kSolveOk] = (double)d.flags[0];
       mbox[kDevErr] = (double)d.flags[1];
+      mbox[kLmDone] = d.scalars[kLmDone];
       __threadfence_system();
       __hip_atomic_store(reinterpret_cast<unsigned long long *>(mbox + kMboxSeq), seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);

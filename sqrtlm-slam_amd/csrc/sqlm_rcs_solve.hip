@@ -358,6 +358,7 @@ struct CRView {
   int *flags;
   double *L;  // [p][n][n]: Linv_I of every factored superblock
   int ld;     // k_cr_aug<1, *> only: nonzero = D is one block with this row stride (dense solve)
+  const int *skip = nullptr;  // k_cr_persist: nonzero *skip = the LM run is over (LMCtl::done), solve nothing
 };
 
 __device__ __forceinline__ double *blk(double *base, int I, int n) { return base + (size_t)I * n * n; }
@@ -1826,6 +1827,9 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CR
   aug::Shared &sh = *reinterpret_cast<aug::Shared *>(lds_raw);
   double *lds_d = reinterpret_cast<double *>(lds_raw);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // a trial enqueued past the end of a device-side LM run: take the tasks (the
+  // queue head must advance as the host counts) but run none
+  const bool skip = v.skip && *v.skip;
   for (;;) {
     if (tid == 0) {
       const unsigned long long q = __hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1837,6 +1841,10 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CR
     const int id = s_id;
     if (id < 0) break;
     const CRTask tk = s_task;
+    if (skip) {
+      __syncthreads();  // s_task / s_id are rewritten by the next dequeue
+      continue;
+    }
     if (wave == 0 && tk.dep_cnt > 0) {
       bool ok = true;
       for (int base = 0; base < tk.dep_cnt; base += 64) {
@@ -1900,11 +1908,10 @@ void cr_persist_free(CRPersist &ps) {
 
 // The task list of launch_cr_core's schedule for p superblocks of n rows, in
 // the order of its launches (a task's predecessors come before it).
-int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu) {
-  if (ps.p == p && ps.n == n && ps.tasks) return 0;
+void cr_persist_graph(int p, int n, std::vector<CRTask> &T, std::vector<int> &D) {
   const int nt = n / 16, items = nt * (nt + 1) / 2 + nt * nt + nt;
-  std::vector<CRTask> T;
-  std::vector<int> D;
+  T.clear();
+  D.clear();
   std::vector<std::vector<int>> lastw(p), prod(p);  // last writers of D/E/g_I; producers of L/A/C/z_I
   std::vector<int> xprod(p, -1);
   auto add = [&](CRTask t, std::vector<int> dp) {
@@ -1960,6 +1967,13 @@ int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu) {
       xprod[I] = add(CRTask{kTkBK, I, h, 0, 1}, dp);
     }
   }
+}
+
+int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu) {
+  if (ps.p == p && ps.n == n && ps.tasks) return 0;
+  std::vector<CRTask> T;
+  std::vector<int> D;
+  cr_persist_graph(p, n, T, D);
   if (T.size() > ps.cap_tasks || D.size() > ps.cap_deps || !ps.head) {
     cr_persist_free(ps);
     ps.cap_tasks = std::max<size_t>(T.size(), 64);
@@ -1975,7 +1989,7 @@ int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu) {
     ps.qbase = 0;
   }
   if (hipMemcpy(ps.tasks, T.data(), T.size() * sizeof(CRTask), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(ps.deps, D.data(), std::max<size_t>(D.size(), 1) * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+      (!D.empty() && hipMemcpy(ps.deps, D.data(), D.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess))
     return -2;
   ps.p = p;
   ps.n = n;
@@ -2002,8 +2016,9 @@ static bool top_split() {
 
 // Levels, top solve and back substitution on D/E/g already in CR layout.
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p,
-                    int n, hipStream_t st, CRPersist *ps) {
+                    int n, hipStream_t st, CRPersist *ps, const int *skip) {
   CRView v{p, n, 0, 0, D, E, A, C, g, x, flags, L};
+  v.skip = skip;
   if (ps && ps->p == p && ps->n == n && ps->tasks && cr_persist_enabled()) {
     launch_cr_persist(v, *ps, st);
     return;
@@ -2041,6 +2056,7 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
 
 int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather, CRPersist *ps) {
   CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
+  v.skip = d.ctl ? &d.ctl->done : nullptr;
   if (!d.cr_direct) {  // BSR S (sharded runs / row-kernel RCS): zero the superblocks and scatter
     const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
     if (hipMemsetAsync(d.cr_D, 0, blkbytes, st) != hipSuccess) return -2;
@@ -2049,7 +2065,7 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool 
     hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
   }
   if (pl.R) launch_arrow_solve(d, pl, st);
-  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st, ps);
+  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st, ps, v.skip);
   if (gather) hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }
