@@ -20,7 +20,7 @@ timeout -k 10 60 ./tools/cr_bench 278 112 20 2>&1 | grep -v "aug_wave\|aug_phase
 echo "== forced timeout" >> $out
 timeout -k 10 60 ./tools/cr_bench_tmo 9 112 2 2>&1 | grep -v "aug_wave\|aug_phase\|top_phase" >> $out; echo "tmo rc=$?" >> $out
 timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  tests/test_gpu_parity.py tests/test_gpu_spec.py tests/test_gpu_cr_fuse.py tests/test_gpu_concurrent.py \
+  tests/test_gpu_schedules.py tests/test_gpu_parity.py tests/test_gpu_spec.py tests/test_gpu_cr_fuse.py tests/test_gpu_concurrent.py \
   "tests/test_eg_gpu.py::test_eg_bench_size_first_iteration" > gpurun_out/pytest_persist.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> $out

@@ -179,6 +179,7 @@ struct sqlm_ctx {
   // iteration starts without a linearization pass (g2o linearizes at exactly
   // that state: same device code, same bits). SQLM_NO_SPEC=1 turns it off.
   bool spec = false;
+  bool no_pose_fuse = false;       // SQLM_NO_POSE_FUSE=1 (per prepare): the pose update as its own launch
   bool lin_valid = false;          // the current buffers hold the linearization at the current state
   bool spec_outstanding = false;   // a speculative camera pass may still run on the side stream
   bool cam_inline = false;         // small problem: the speculative camera pass on the context stream
@@ -1065,6 +1066,11 @@ int prepare(sqlm_ctx *c, int level) {
         upd_rng[k] = hi < 0 ? int2{1, 0} : int2{lo, hi};
       }
     });
+    for (Bucket &b : c->buckets) {
+      const size_t k1 = b.rng_off + (b.slot_end - b.slot_begin + kBlock / b.W - 1) / (kBlock / b.W);
+      b.wide = false;
+      for (size_t k = b.rng_off; k < k1 && k < nb; ++k) b.wide |= upd_rng[k].y - upd_rng[k].x + 1 > kUpdWin;
+    }
   }
   // RCS tiles (passes 1-2: windows, local cameras, camera pairs), then the
   // reduced-camera-system pattern (upper, diagonal first) from the tiles'
@@ -1315,6 +1321,7 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_BP, 8 * (size_t)nP, d.bp);
   {
     const bool no_spec = getenv("SQLM_NO_SPEC") && atoi(getenv("SQLM_NO_SPEC")) != 0;
+    c->no_pose_fuse = getenv("SQLM_NO_POSE_FUSE") != nullptr;
     c->spec = c->use_tiles && d.obs_P == nullptr && !no_spec;
     // the side stream's fork / join (two event records, two waits: ~20 us of
     // host API time per trial) pays only when the pass is long enough to hide;
@@ -1726,14 +1733,20 @@ int trial_launch(sqlm_ctx *c, double lambda, bool &cam_after) {
   }
   tmark(c, 4, true);
   hmark(c, 3);  // solve launches
+  // the pose update folded into the first landmark-update launch (one launch
+  // less per trial; SQLM_NO_POSE_FUSE=1 keeps it separate, A/B and tests)
+  const bool no_fuse = c->no_pose_fuse;
+  // (small problems only: the fused variant runs at lower occupancy, which the
+  // latency-bound config-4 update pays for more than one launch saves)
+  const bool fuse = pose_from_cr && c->cam_inline && !no_fuse && !c->buckets.empty() && !c->buckets[0].wide;
   tmark(c, 5, false);
-  launch_pose_update(d, lambda, c->stream, pose_from_cr);
+  if (!fuse) launch_pose_update(d, lambda, c->stream, pose_from_cr);
   tmark(c, 5, true);
   tmark(c, 6, false);
   // (the buckets on three streams, like the tile classes, measured slower:
   // 686 -> 647 it/s, the CR solve after them 0.54 -> 0.61 ms; profiles/r03/ab_upd_streams.log)
   for (size_t b = 0; b < c->buckets.size(); ++b)
-    launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream, c->spec);
+    launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream, c->spec, fuse && b == 0);
   launch_lidar_chi2(d, c->stream);
   tmark(c, 6, true);
   hmark(c, 4);  // pose + landmark updates
@@ -1828,7 +1841,7 @@ int lm_host(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
 // from every kernel at once. The caller's stop flag is mirrored into a mapped
 // word the decision reads.
 bool dlm_ok(const sqlm_ctx *c) {
-  static const bool off = std::getenv("SQLM_NO_DLM") != nullptr;
+  const bool off = std::getenv("SQLM_NO_DLM") != nullptr;  // read per run: tests switch it
   return !off && c->ctl_dev && c->ctl_host && c->mbox && c->stop_map_dev && c->spec && c->use_tiles && !c->timing && !c->htrace &&
          !c->comm.enabled();
 }

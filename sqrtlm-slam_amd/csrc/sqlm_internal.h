@@ -305,11 +305,15 @@ constexpr int kObsPerLane = SQLM_OBS_PER_LANE;
 #endif
 constexpr int kObsPreload = SQLM_OBS_PRELOAD;
 
+// k_landmark_update stages a block tile's pose window in LDS when it spans at
+// most kUpdWin poses (wider: loop-closure landmarks, global reads)
+constexpr int kUpdWin = 64;
 struct Bucket {
   int W;            // segment width
   int slot_begin;   // first landmark slot
   int slot_end;
   int rng_off = 0;  // first entry of this bucket's tiles in DevProblem::upd_rng
+  bool wide = false;  // some block tile's pose window is wider than kUpdWin
 };
 
 // kernel launchers (sqlm_kernels.hip). All asynchronous on `st`.
@@ -406,8 +410,10 @@ int launch_batched_atb(const double *A, const double *B, double *P, int p, int n
 // from_cr: dx taken from the cyclic-reduction solution (launch_cr_solve with
 // gather = false), written to d.dx on the way
 void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool from_cr = false);
+// fuse_pose: the launch also does launch_pose_update(from_cr = true)'s work
+// (band / border CR solves, a bucket without wide windows)
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st,
-                            bool spec = false);
+                            bool spec = false, bool fuse_pose = false);
 void launch_lidar_chi2(const DevProblem &d, hipStream_t st);
 void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts,
                    int n_lid_parts, hipStream_t st, double *mbox = nullptr, unsigned long long seq = 0);

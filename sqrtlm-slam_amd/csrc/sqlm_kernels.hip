@@ -1545,54 +1545,79 @@ int launch_dense_solve(const DevProblem &d, hipStream_t st) {
 // CR: the pose's dx is read from the cyclic-reduction solution (band position
 // or border slot; 0 if the solve flagged a non-positive pivot) and written to
 // dx for the landmark update -- the k_cr_gather step folded into this launch.
+// The trial pose of pose p (VertexSE3Expmap::oplusImpl, exp(dx) * T) into q, t;
+// dd = its dx (zero for a fixed pose), h = its free index or -1.
 template <bool CR>
-__global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda) {
+__device__ __forceinline__ void trial_pose(const DevProblem &d, int p, double q[4], double t[3], double dd[6], int &h) {
+  const double *qt = d.pose_qt[0] + 8 * p;
+  q[0] = qt[0]; q[1] = qt[1]; q[2] = qt[2]; q[3] = qt[3];
+  t[0] = qt[4]; t[1] = qt[5]; t[2] = qt[6];
+  h = d.pose_hidx[p];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dd[k] = 0.0;
+  if (h < 0) return;
+  if (CR) {
+    const int pi = d.cam_pos ? d.cam_pos[h] : h;
+    const double *x = pi >= 0 ? d.cr_x + (size_t)(pi / d.cr_B) * d.cr_n + 6 * (pi % d.cr_B) : d.bd_x + 6 * (-1 - pi);
+    const bool ok = d.flags[0] != 0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) dd[k] = ok ? x[k] : 0.0;
+  } else {
+    const double *dx = d.dx + 6 * h;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) dd[k] = dx[k];
+  }
+  se3_oplus(q, t, dd);
+}
+
+// k_pose_update's work for pose p: the trial pose rows, dx (CR), and this
+// pose's computeScale term dx^T (lambda dx + b) (sharded: b_p is summed over
+// ranks and lambda counted once)
+template <bool CR>
+__device__ __forceinline__ double pose_update_item(const DevProblem &d, double lambda, int p) {
+  double q[4], t[3], dd[6];
+  int h;
+  trial_pose<CR>(d, p, q, t, dd, h);
+  double sc = 0.0;
+  if (h >= 0) {
+    if (CR) {
+      double *dx = d.dx + 6 * h;
+      store2(dx, dd[0], dd[1]); store2(dx + 2, dd[2], dd[3]); store2(dx + 4, dd[4], dd[5]);
+    }
+    const double lam = (!d.sharded || d.rank == 0) ? lambda : 0.0;
+    for (int k = 0; k < 6; ++k) sc += dd[k] * (lam * dd[k] + d.bp[8 * h + k]);
+  }
+  double *o = d.pose_qt[1] + 8 * p;
+  store2(o, q[0], q[1]); store2(o + 2, q[2], q[3]); store2(o + 4, t[0], t[1]); store2(o + 6, t[2], 0.0);
+  double R[9];
+  q_to_mat(q, R);
+  double *rt = d.pose_rt[1] + 16 * p;
+#pragma unroll
+  for (int k = 0; k < 9; ++k) rt[k] = R[k];
+  rt[9] = t[0]; rt[10] = t[1]; rt[11] = t[2];
+  rt[12] = d.intr[4 * p]; rt[13] = d.intr[4 * p + 1]; rt[14] = d.intr[4 * p + 2]; rt[15] = d.intr[4 * p + 3];
+  return sc;
+}
+
+// DLM: the parity this trial runs under, for its speculative camera pass
+// (which may run after the decision has flipped par); block `b0` writes it
+__device__ __forceinline__ bool pose_enter(DevProblem &d, int b0) {
   if (d.ctl) {
-    if (d.ctl->done) return;
-    // the parity this trial runs under, for its speculative camera pass (which
-    // may run after the decision has flipped par)
-    if (blockIdx.x == 0 && threadIdx.x == 0) d.ctl->par_trial = d.ctl->par;
+    if (d.ctl->done) return false;
+    if (b0 == 0 && threadIdx.x == 0) d.ctl->par_trial = d.ctl->par;
   }
   lm_enter(d);
+  return true;
+}
+
+template <bool CR>
+__global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda) {
+  if (!pose_enter(d, blockIdx.x)) return;
   lambda = lm_lam(d, lambda);
   __shared__ double red[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double sc = 0.0;
-  if (p < d.n_pose) {
-    const double *qt = d.pose_qt[0] + 8 * p;
-    double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t[3] = {qt[4], qt[5], qt[6]};
-    const int h = d.pose_hidx[p];
-    if (h >= 0) {
-      double dd[6];
-      if (CR) {
-        const int pi = d.cam_pos ? d.cam_pos[h] : h;
-        const double *x = pi >= 0 ? d.cr_x + (size_t)(pi / d.cr_B) * d.cr_n + 6 * (pi % d.cr_B)
-                                  : d.bd_x + 6 * (-1 - pi);
-        const bool ok = d.flags[0] != 0;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dd[k] = ok ? x[k] : 0.0;
-        double *dx = d.dx + 6 * h;
-        store2(dx, dd[0], dd[1]); store2(dx + 2, dd[2], dd[3]); store2(dx + 4, dd[4], dd[5]);
-      } else {
-        const double *dx = d.dx + 6 * h;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) dd[k] = dx[k];
-      }
-      se3_oplus(q, t, dd);
-      // computeScale dx^T (lambda dx + b): sharded, b_p is summed over ranks and lambda counted once
-      const double lam = (!d.sharded || d.rank == 0) ? lambda : 0.0;
-      for (int k = 0; k < 6; ++k) sc += dd[k] * (lam * dd[k] + d.bp[8 * h + k]);
-    }
-    double *o = d.pose_qt[1] + 8 * p;
-    store2(o, q[0], q[1]); store2(o + 2, q[2], q[3]); store2(o + 4, t[0], t[1]); store2(o + 6, t[2], 0.0);
-    double R[9];
-    q_to_mat(q, R);
-    double *rt = d.pose_rt[1] + 16 * p;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) rt[k] = R[k];
-    rt[9] = t[0]; rt[10] = t[1]; rt[11] = t[2];
-    rt[12] = d.intr[4 * p]; rt[13] = d.intr[4 * p + 1]; rt[14] = d.intr[4 * p + 2]; rt[15] = d.intr[4 * p + 3];
-  }
+  if (p < d.n_pose) sc = pose_update_item<CR>(d, lambda, p);
   const double s = block_sum(sc, red);
   if (threadIdx.x == 0) d.partials[kPartScaleCam + blockIdx.x] = s;
 }
@@ -1612,17 +1637,32 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool
 // the window's poses at both states and its dx are staged in LDS once per
 // tile, and the per-observation gathers read LDS instead of L2. Tiles whose
 // window is wider (loop-closure landmarks) read the global arrays.
-constexpr int kUpdWin = 64;
 #ifndef SQLM_UPD_OCC
 #define SQLM_UPD_OCC 1
 #endif
-template <int W, bool ST, bool SPEC>
+// fuse_pose (first bucket of a band solve, no window wider than kUpdWin): the
+// blocks past nlm_blocks do k_pose_update<true>'s work, and every block tile
+// forms its window's trial poses and dx itself (the same trial_pose code, so
+// the same bits) instead of reading them -- one launch less per trial.
+template <int W, bool ST, bool SPEC, bool FUSE = false>
 __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : 4) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
-                                                         double lambda, int part_off, const int2 *rng) {
-  if (!lm_enter(d)) return;
-  lambda = lm_lam(d, lambda);
+                                                         double lambda, int part_off, const int2 *rng, int nlm_blocks) {
+  constexpr bool fuse_pose = FUSE;
   __shared__ double red[4];
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
+  if (fuse_pose && (int)blockIdx.x >= nlm_blocks) {  // k_pose_update<true>
+    const int pb = blockIdx.x - nlm_blocks;
+    if (!pose_enter(d, pb)) return;
+    lambda = lm_lam(d, lambda);
+    const int p = pb * blockDim.x + threadIdx.x;
+    double sc = 0.0;
+    if (p < d.n_pose) sc = pose_update_item<true>(d, lambda, p);
+    const double s = block_sum(sc, red);
+    if (threadIdx.x == 0) d.partials[kPartScaleCam + pb] = s;
+    return;
+  }
+  if (!lm_enter(d)) return;
+  lambda = lm_lam(d, lambda);
   constexpr int SPB = kBlock / W;
   const int lane = threadIdx.x & (W - 1);
   const int nseg = slot_end - slot_begin;
@@ -1733,18 +1773,37 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : 4) void k_landmark_update(
     }
     if (valid && lane == 0) chi_acc += chi;
   };
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  for (int tile = blockIdx.x; tile < ntiles; tile += nlm_blocks) {
     const int2 rg = rng[tile];  // pose id range of the tile's observations (x > y: none)
     const int nw = rg.y - rg.x + 1;
     if (nw <= kUpdWin) {
       __syncthreads();  // the previous tile's readers are done with the window
-      for (int k = threadIdx.x; k < 16 * nw; k += blockDim.x) {
-        Wp0[k] = d.pose_rt[0][16 * rg.x + k];
-        Wp1[k] = d.pose_rt[1][16 * rg.x + k];
-      }
-      for (int k = threadIdx.x; k < 8 * nw; k += blockDim.x) {
-        const int c = k >> 3, r = k & 7, h = d.pose_hidx[rg.x + c];
-        Wdx[k] = (h >= 0 && r < 6) ? d.dx[6 * h + r] : 0.0;
+      if constexpr (FUSE) {
+        for (int k = threadIdx.x; k < 16 * nw; k += blockDim.x) Wp0[k] = d.pose_rt[0][16 * rg.x + k];
+        for (int c = threadIdx.x; c < nw; c += blockDim.x) {
+          const int p = rg.x + c;
+          double q[4], t3[3], dd[6], R[9];
+          int h;
+          trial_pose<true>(d, p, q, t3, dd, h);
+          q_to_mat(q, R);
+          double *w1 = Wp1 + 16 * c, *wd = Wdx + 8 * c;
+#pragma unroll
+          for (int k = 0; k < 9; ++k) w1[k] = R[k];
+          w1[9] = t3[0]; w1[10] = t3[1]; w1[11] = t3[2];
+          w1[12] = d.intr[4 * p]; w1[13] = d.intr[4 * p + 1]; w1[14] = d.intr[4 * p + 2]; w1[15] = d.intr[4 * p + 3];
+#pragma unroll
+          for (int k = 0; k < 6; ++k) wd[k] = dd[k];
+          wd[6] = wd[7] = 0.0;
+        }
+      } else {
+        for (int k = threadIdx.x; k < 16 * nw; k += blockDim.x) {
+          Wp0[k] = d.pose_rt[0][16 * rg.x + k];
+          Wp1[k] = d.pose_rt[1][16 * rg.x + k];
+        }
+        for (int k = threadIdx.x; k < 8 * nw; k += blockDim.x) {
+          const int c = k >> 3, r = k & 7, h = d.pose_hidx[rg.x + c];
+          Wdx[k] = (h >= 0 && r < 6) ? d.dx[6 * h + r] : 0.0;
+        }
       }
       __syncthreads();
       tile_body(tile, Wp0 - 16 * rg.x, Wp1 - 16 * rg.x, Wdx - 8 * rg.x, std::true_type{});
@@ -1762,21 +1821,25 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : 4) void k_landmark_update(
 }
 
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st,
-                            bool spec) {
+                            bool spec, bool fuse_pose) {
   const int nb = linearize_blocks(b);
   if (nb <= 0) return;
-#define SQLM_LAUNCH(WW, STT, SP) \
-  hipLaunchKernelGGL((k_landmark_update<WW, STT, SP>), dim3(nb), dim3(kBlock), 0, st, d, b.slot_begin, b.slot_end, \
-                     lambda, part_off, d.upd_rng + b.rng_off)
-#define SQLM_CASE(WW)                                   \
-  case WW:                                              \
-    if (d.has_stereo) {                                 \
-      if (spec) SQLM_LAUNCH(WW, true, true);            \
-      else SQLM_LAUNCH(WW, true, false);                \
-    } else {                                            \
-      if (spec) SQLM_LAUNCH(WW, false, true);           \
-      else SQLM_LAUNCH(WW, false, false);               \
-    }                                                   \
+  fuse_pose = fuse_pose && spec;  // instantiated for the speculative schedule only
+  const int grid = nb + (fuse_pose ? (d.n_pose + kBlock - 1) / kBlock : 0);
+#define SQLM_LAUNCH(WW, STT, SP, FU) \
+  hipLaunchKernelGGL((k_landmark_update<WW, STT, SP, FU>), dim3(grid), dim3(kBlock), 0, st, d, b.slot_begin, \
+                     b.slot_end, lambda, part_off, d.upd_rng + b.rng_off, nb)
+#define SQLM_CASE(WW)                                            \
+  case WW:                                                       \
+    if (d.has_stereo) {                                          \
+      if (fuse_pose) SQLM_LAUNCH(WW, true, true, true);          \
+      else if (spec) SQLM_LAUNCH(WW, true, true, false);         \
+      else SQLM_LAUNCH(WW, true, false, false);                  \
+    } else {                                                     \
+      if (fuse_pose) SQLM_LAUNCH(WW, false, true, true);         \
+      else if (spec) SQLM_LAUNCH(WW, false, true, false);        \
+      else SQLM_LAUNCH(WW, false, false, false);                 \
+    }                                                            \
     break;
   switch (b.W) {
     SQLM_CASE(2) SQLM_CASE(4) SQLM_CASE(8) SQLM_CASE(16) SQLM_CASE(32) SQLM_CASE(64)

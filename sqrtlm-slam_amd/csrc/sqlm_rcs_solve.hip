@@ -1893,9 +1893,9 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CR
   }
 }
 
-bool cr_persist_enabled() {
-  static const bool on = std::getenv("SQLM_CR_PERSIST") && std::atoi(std::getenv("SQLM_CR_PERSIST")) != 0;
-  return on && !cr_legacy();
+bool cr_persist_enabled() {  // read per call (prepare, trial): tests switch it
+  const char *e = std::getenv("SQLM_CR_PERSIST");
+  return e && std::atoi(e) != 0 && !cr_legacy();
 }
 
 void cr_persist_free(CRPersist &ps) {

@@ -34,13 +34,16 @@ def _gpu_rank(rank, world, gen, scale, iters):
 
 
 @pytest.mark.parametrize("world,gen,scale", [(2, "band", 0.01), (3, "band", 0.05), (2, "loop", 0.02),
-                                             (3, "loop", 0.05), (2, "band", 1.0), (2, "loop", 1.0)])
+                                             (3, "loop", 0.05), (8, "band", 0.02), (8, "loop", 0.02),
+                                             (2, "band", 1.0), (2, "loop", 1.0)])
 def test_sharded_global_ba_matches_oracle(oracle, world, gen, scale):
     """Loop-closed maps ("loop"): the ranks holding the revisited keyframes'
     landmarks see S blocks far off the band; the shared S pattern is the union
     of the shards' patterns, so every rank plans the same band + border solve.
     scale 1.0: BASELINE config 4 itself (5k poses, 500k landmarks) on two
-    ranks; the oracle runs with its OpenMP loops (bit-identical results)."""
+    ranks; the oracle runs with its OpenMP loops (bit-identical results).
+    world 8: the driver's 8-GPU protocol (seven concurrent receives into rank
+    0, eight-way shard balance) at 2 % scale, eight processes on one GPU."""
     prob = _problem(gen, scale)
     ref = oracle.OracleGraph(prob, omp=scale >= 0.5)
     nr, sr = ref.global_ba(10)

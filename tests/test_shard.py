@@ -46,9 +46,13 @@ def test_ranges_cover_and_balance():
         assert max(obs) - min(obs) <= 2 * 18 + 1  # one landmark's track of slack per cut
 
 
-def test_two_rank_exchanges_match_single_process():
+@pytest.mark.parametrize("world", [2, 8])
+def test_rank_exchanges_match_single_process(world):
+    """The setup exchanges of prepare() at world size 2 and 8 (the driver's
+    8-GPU node): camera set, counts, chi2 and the longest track agree with
+    the single process; the shards cover the trajectory end to end."""
     prob = synth.config4(seed=4, scale=0.01)
-    res = run_ranks(_rank_work, 2, 0.01)
+    res = run_ranks(_rank_work, world, 0.01)
     full_act = np.zeros(prob.n_pose, np.uint8)
     full_act[np.unique(prob.obs_pose)] = 1
     for r in res:
@@ -56,9 +60,11 @@ def test_two_rank_exchanges_match_single_process():
         assert r["cnt"][0] == prob.n_obs and r["cnt"][1] == prob.n_pt
         assert r["chi"] == pytest.approx(_sse(prob), rel=1e-12)   # chi2 sums across shards
         assert r["bw"] == int(np.max(np.bincount(prob.obs_pt)))
-    assert res[0]["n_obs"] + res[1]["n_obs"] == prob.n_obs
+    assert sum(r["n_obs"] for r in res) == prob.n_obs
     # contiguous landmark ranges in trajectory order touch overlapping camera bands
-    assert res[0]["first_pose"] == 0 and res[1]["last_pose"] == prob.n_pose - 1
+    assert res[0]["first_pose"] == 0 and res[-1]["last_pose"] == prob.n_pose - 1
+    for a, b in zip(res, res[1:]):
+        assert a["first_pose"] <= b["first_pose"] <= a["last_pose"] + 1
 
 
 def test_lidar_edges_only_on_rank0():
@@ -97,9 +103,26 @@ def _gather_work(rank, world, n_rows, seed):
     return dict(x=x, ref=full.sum(axis=1))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gather_to_root_and_broadcast(world):
     res = run_ranks(_gather_work, world, 50, 7)
     for r in res:
         np.testing.assert_allclose(r["x"], r["ref"], rtol=1e-12, atol=1e-12)
         np.testing.assert_array_equal(r["x"], res[0]["x"])
+
+
+def test_balance_at_eight_ranks_full_size():
+    """shard.py at the driver's N = 8 on config 4's full-size landmark layout:
+    observation counts within one track of each other, every rank's camera
+    window a contiguous 1/8 of the trajectory plus the overlap of the tracks
+    cut at its ends (<= 17 cameras on each side)."""
+    prob = synth.config4(seed=4, scale=0.2)
+    rng = landmark_ranges(prob, 8)
+    obs = []
+    for lo, hi in rng:
+        sel = (prob.obs_pt >= lo) & (prob.obs_pt < hi)
+        obs.append(int(sel.sum()))
+        cams = np.unique(prob.obs_pose[sel])
+        assert cams[-1] - cams[0] + 1 == cams.size  # contiguous window
+        assert cams.size <= prob.n_pose / 8 + 2 * 18
+    assert max(obs) - min(obs) <= 2 * 18 + 1
