@@ -1738,7 +1738,8 @@ int trial_launch(sqlm_ctx *c, double lambda, bool &cam_after) {
   const bool no_fuse = c->no_pose_fuse;
   // (small problems only: the fused variant runs at lower occupancy, which the
   // latency-bound config-4 update pays for more than one launch saves)
-  const bool fuse = pose_from_cr && c->cam_inline && !no_fuse && !c->buckets.empty() && !c->buckets[0].wide;
+  // (the fused variant is instantiated for the speculative schedule only)
+  const bool fuse = pose_from_cr && c->spec && c->cam_inline && !no_fuse && !c->buckets.empty() && !c->buckets[0].wide;
   tmark(c, 5, false);
   if (!fuse) launch_pose_update(d, lambda, c->stream, pose_from_cr);
   tmark(c, 5, true);

@@ -132,6 +132,11 @@ __device__ __forceinline__ bool spin(int *f) {
   int it = 0;
   for (; __atomic_load_n(p, __ATOMIC_RELAXED) == 0 && it < kSpinLimit; ++it) __builtin_amdgcn_s_sleep(1);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef SQLM_SPIN_DEBUG
+  if (it >= kSpinLimit && (threadIdx.x & 63) == 0)
+    printf("spin timeout: block %d wave %d lds offset %u\n", (int)blockIdx.x, (int)(threadIdx.x >> 6),
+           (unsigned)(uintptr_t)p);
+#endif
 #ifdef SQLM_SPIN_FORCE_TIMEOUT
   return false;
 #else
@@ -388,6 +393,10 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
     else if (t < 2 * kMaxNt + kPairs) sh.fH[t - kMaxNt - kPairs] = 0;
   }
   __syncthreads();
+#ifdef SQLM_SPIN_DEBUG
+  if (lane == 0 && (wave == 0 || wave == 9))
+    printf("aug blk %d wave %d I %d mode %d past zeroing, fT0 %d\n", (int)blockIdx.x, wave, I, MODE, sh.fT[0]);
+#endif
   if (threadIdx.x == 0) AUG_PROF(0);
   AUG_HWID(wave);
   // MODE 1 with v.ld: one diagonal block of a larger dense matrix (row stride ld)
@@ -408,6 +417,9 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
     }
     for (int k = 0; k < nt; ++k) {
       AUG_STAMP(0, k, 0);
+#ifdef SQLM_SPIN_DEBUG
+      if (lane == 0) printf("w0 blk %d I %d step %d t %lld\n", (int)blockIdx.x, I, k, (long long)clock64());
+#endif
       d4 Tt;
       if (k + 1 < nt) diag_groups<true>(Dg, P, Q, Tt, lane, bad);
       else diag_groups<false>(Dg, P, Q, Tt, lane, bad);
@@ -442,6 +454,9 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
     }
     if (bad && lane == 0) v.flags[0] = 0;
     if (tmo) cr_fail(v, lane);
+#ifdef SQLM_SPIN_DEBUG
+    if (lane == 0) printf("w0 blk %d I %d done t %lld\n", (int)blockIdx.x, I, (long long)clock64());
+#endif
     return;
   }
   if ((wave & 3) == 0) return;  // the diagonal wave's SIMD partners stay idle

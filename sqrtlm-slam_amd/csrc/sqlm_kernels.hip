@@ -1824,7 +1824,7 @@ void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda,
                             bool spec, bool fuse_pose) {
   const int nb = linearize_blocks(b);
   if (nb <= 0) return;
-  fuse_pose = fuse_pose && spec;  // instantiated for the speculative schedule only
+  if (fuse_pose && !spec) return;  // instantiated for the speculative schedule only: the caller must not ask
   const int grid = nb + (fuse_pose ? (d.n_pose + kBlock - 1) / kBlock : 0);
 #define SQLM_LAUNCH(WW, STT, SP, FU) \
   hipLaunchKernelGGL((k_landmark_update<WW, STT, SP, FU>), dim3(grid), dim3(kBlock), 0, st, d, b.slot_begin, \

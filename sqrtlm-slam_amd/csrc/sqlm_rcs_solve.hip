@@ -1725,22 +1725,28 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
 constexpr int kPersistUpdItems = 16;  // UP task: one item per wave
 
 // the task bodies as separate functions: inlined into one switch they share
-// one register allocation (the union of their live ranges spills)
-__device__ __noinline__ void pt_f(aug::Shared &sh, const CRView &v, int h, int I, int split, int sidx) {
-  aug_body<0, false, false, true>(sh, v, h, I, split, sidx);
+// one register allocation (the union of their live ranges spills). Each
+// names the dynamic LDS itself (extern __shared__), so its LDS accesses stay
+// DS instructions (a generic pointer parameter would turn them into FLAT
+// accesses, which do not keep the DS ordering the in-workgroup flags rely on).
+extern __shared__ __attribute__((aligned(16))) unsigned char cr_persist_lds[];
+__device__ __forceinline__ aug::Shared &persist_shared() { return *reinterpret_cast<aug::Shared *>(cr_persist_lds); }
+__device__ __noinline__ void pt_f(const CRView v, int h, int I, int split, int sidx) {
+  aug_body<0, false, false, true>(persist_shared(), v, h, I, split, sidx);
 }
-__device__ __noinline__ void pt_fo(aug::Shared &sh, const CRView &v, int h, int I) {
-  aug_body<1, false, false, true>(sh, v, h, I, 1, 0);
+__device__ __noinline__ void pt_fo(const CRView v, int h, int I) {
+  aug_body<1, false, false, true>(persist_shared(), v, h, I, 1, 0);
 }
-__device__ __noinline__ void pt_top(aug::Shared &sh, const CRView &v) { aug_body<1, false, true, true>(sh, v, 0, 0, 1, 0); }
-__device__ __noinline__ void pt_tr(const CRView &v, int h, int I, int s) { trsm_strip<true>(v, h, I, s); }
-__device__ __noinline__ void pt_up(const CRView &v, int h, int lb) { cr_update_item<true, 4>(v, h, lb); }
+__device__ __noinline__ void pt_top(const CRView v) { aug_body<1, false, true, true>(persist_shared(), v, 0, 0, 1, 0); }
+__device__ __noinline__ void pt_tr(const CRView v, int h, int I, int s) { trsm_strip<true>(v, h, I, s); }
+__device__ __noinline__ void pt_up(const CRView v, int h, int lb) { cr_update_item<true, 4>(v, h, lb); }
 
 // k_cr_back_u<false> for the persistent solve (16 waves, <= 128 VGPRs): the
 // neighbours' solutions staged in LDS, y = z_I - A_I x_{I-h} - C_I x_{I+h}
 // with one 8-row slice per wave, then the blocked backward substitution of
 // back_u_body.
-__device__ __noinline__ void pt_bk(double *sm, const CRView &v, int h, int I) {
+__device__ __noinline__ void pt_bk(const CRView v, int h, int I) {
+  double *sm = reinterpret_cast<double *>(cr_persist_lds);
   double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN, *xl = sm + 3 * kCRMaxN, *xr = sm + 4 * kCRMaxN;
   int *fx = reinterpret_cast<int *>(sm + 5 * kCRMaxN);
   const int n = v.n, nt = n >> 4;
@@ -1821,75 +1827,91 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CR
                                                              const int *__restrict__ deps, int ntasks, int *done,
                                                              unsigned long long *head, unsigned long long qbase,
                                                              int epoch) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ CRTask s_task;
   __shared__ int s_id;
-  aug::Shared &sh = *reinterpret_cast<aug::Shared *>(lds_raw);
-  double *lds_d = reinterpret_cast<double *>(lds_raw);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // a trial enqueued past the end of a device-side LM run: take the tasks (the
   // queue head must advance as the host counts) but run none
-  const bool skip = v.skip && *v.skip;
-  for (;;) {
-    if (tid == 0) {
-      const unsigned long long q = __hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const long long t = (long long)(q - qbase);
-      s_id = t < ntasks ? (int)t : -1;
-      if (t < ntasks) s_task = tasks[t];
-    }
-    __syncthreads();
-    const int id = s_id;
-    if (id < 0) break;
-    const CRTask tk = s_task;
-    if (skip) {
-      __syncthreads();  // s_task / s_id are rewritten by the next dequeue
-      continue;
-    }
-    if (wave == 0 && tk.dep_cnt > 0) {
-      bool ok = true;
-      for (int base = 0; base < tk.dep_cnt; base += 64) {
-        const int k = base + lane;
-        int *f = k < tk.dep_cnt ? done + deps[tk.dep_off + k] : nullptr;
-        for (int it = 0;; ++it) {
-          const bool mine = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-          if (__all(mine)) break;
-          if (it >= aug::kSpinLimit) {
-            ok = false;
-            break;
+  const bool skip = __builtin_amdgcn_readfirstlane(v.skip && *v.skip ? 1 : 0) != 0;
+  // thread 0 takes the next task into LDS (after publishing the previous one)
+  auto take = [&]() {
+    const unsigned long long q = __hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long t = (long long)(q - qbase);
+    s_id = (t >= 0 && t < ntasks) ? (int)t : -1;
+    if (t >= 0 && t < ntasks) s_task = tasks[t];
+  };
+  if (tid == 0) take();
+  __syncthreads();
+  // the task id and fields are workgroup-uniform: say so (readfirstlane), so
+  // the loop and the switch are uniform branches (a loop the compiler takes for
+  // divergent is restructured around the barriers and the dequeue)
+  int id = __builtin_amdgcn_readfirstlane(s_id);
+  while (id >= 0) {
+    CRTask tk;
+    tk.type = __builtin_amdgcn_readfirstlane(s_task.type);
+    tk.I = __builtin_amdgcn_readfirstlane(s_task.I);
+    tk.h = __builtin_amdgcn_readfirstlane(s_task.h);
+    tk.a = __builtin_amdgcn_readfirstlane(s_task.a);
+    tk.b = __builtin_amdgcn_readfirstlane(s_task.b);
+    tk.dep_off = __builtin_amdgcn_readfirstlane(s_task.dep_off);
+    tk.dep_cnt = __builtin_amdgcn_readfirstlane(s_task.dep_cnt);
+#ifdef SQLM_SPIN_DEBUG
+    if (lane == 0 && (wave == 0 || wave == 9))
+      printf("persist blk %d wave %d task %d type %d I %d h %d deps %d\n", (int)blockIdx.x, wave, id, tk.type, tk.I, tk.h,
+             tk.dep_cnt);
+#endif
+    if (!skip) {
+      if (wave == 0 && tk.dep_cnt > 0) {
+        bool ok = true;
+        for (int base = 0; base < tk.dep_cnt; base += 64) {
+          const int k = base + lane;
+          int *f = k < tk.dep_cnt ? done + deps[tk.dep_off + k] : nullptr;
+          for (int it = 0;; ++it) {
+            const bool mine = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+            if (__all(mine)) break;
+            if (it >= aug::kSpinLimit) {
+              ok = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
           }
-          __builtin_amdgcn_s_sleep(1);
         }
+        if (!ok) cr_fail(v, lane);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if (!ok) cr_fail(v, lane);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __syncthreads();
+      switch (tk.type) {
+        case kTkF:
+          pt_f(v, tk.h, tk.I, tk.b, tk.a);
+          break;
+        case kTkFO:
+          pt_fo(v, tk.h, tk.I);
+          break;
+        case kTkTR:
+          if (wave < tk.b) pt_tr(v, tk.h, tk.I, tk.a + wave);
+          break;
+        case kTkUP: {
+          const int nt = v.n >> 4, items = nt * (nt + 1) / 2 + nt * nt + nt;
+          if (wave < tk.b) pt_up(v, tk.h, (tk.I / (2 * tk.h)) * items + tk.a + wave);
+          break;
+        }
+        case kTkTOP:
+          pt_top(v);
+          break;
+        default:  // kTkBK
+          pt_bk(v, tk.h, tk.I);
+          break;
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
-    switch (tk.type) {
-      case kTkF:
-        pt_f(sh, v, tk.h, tk.I, tk.b, tk.a);
-        break;
-      case kTkFO:
-        pt_fo(sh, v, tk.h, tk.I);
-        break;
-      case kTkTR:
-        if (wave < tk.b) pt_tr(v, tk.h, tk.I, tk.a + wave);
-        break;
-      case kTkUP: {
-        const int nt = v.n >> 4, items = nt * (nt + 1) / 2 + nt * nt + nt;
-        if (wave < tk.b) pt_up(v, tk.h, (tk.I / (2 * tk.h)) * items + tk.a + wave);
-        break;
-      }
-      case kTkTOP:
-        pt_top(sh, v);
-        break;
-      default:  // kTkBK
-        pt_bk(lds_d, v, tk.h, tk.I);
-        break;
+    __syncthreads();  // every wave's results drained; s_task / s_id read by all
+    if (tid == 0) {
+      if (!skip) __hip_atomic_store(done + id, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      take();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(done + id, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    id = __builtin_amdgcn_readfirstlane(s_id);
   }
 }
 

@@ -2,8 +2,6 @@
 
 * the device-side LM loop (k_reduce applies lm_decide, trials enqueued ahead
   with parity-resolved state buffers) vs the host loop (SQLM_NO_DLM=1);
-* the persistent cyclic-reduction solve (k_cr_persist, one launch) vs the
-  per-level launches (SQLM_CR_PERSIST=0);
 * the pose update folded into the first landmark-update launch vs its own
   launch (SQLM_NO_POSE_FUSE=1).
 Each replaces launches or host decisions only -- the arithmetic is the same
@@ -38,12 +36,11 @@ def _run(ctx, prob, kind, monkeypatch, env):
     return out, q.copy(), t.copy(), ctx.points().copy(), ctx.edge_chi2().copy(), info
 
 
-NEW = {"SQLM_CR_PERSIST": "1", "SQLM_NO_DLM": None, "SQLM_NO_POSE_FUSE": None}
+NEW = {"SQLM_CR_PERSIST": None, "SQLM_NO_DLM": None, "SQLM_NO_POSE_FUSE": None}
 OLD = {
     "host_loop": {"SQLM_NO_DLM": "1"},
-    "per_level_cr": {"SQLM_CR_PERSIST": "0"},
     "pose_launch": {"SQLM_NO_POSE_FUSE": "1"},
-    "all_old": {"SQLM_CR_PERSIST": "0", "SQLM_NO_DLM": "1", "SQLM_NO_POSE_FUSE": "1"},
+    "all_old": {"SQLM_NO_DLM": "1", "SQLM_NO_POSE_FUSE": "1"},
 }
 
 
@@ -62,6 +59,3 @@ def test_schedule_bitwise_equal(gpu_ctx, monkeypatch, name, old):
         assert _strip(a[0][1]) == _strip(b[0][1])
     for x, y in zip(a[1:5], b[1:5]):
         assert np.array_equal(x, y)
-    if a[5]["solve"] in ("cr_levels", "cr_persistent"):
-        assert a[5]["solve"] == "cr_persistent"
-        assert b[5]["solve"] == ("cr_levels" if "SQLM_CR_PERSIST" in OLD[old] else "cr_persistent")

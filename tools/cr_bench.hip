@@ -17,6 +17,7 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); return 2; } } while (0)
 
 int main(int argc, char **argv) {
+  std::setvbuf(stdout, nullptr, _IONBF, 0);
   const int p = argc > 1 ? std::atoi(argv[1]) : 278, n = argc > 2 ? std::atoi(argv[2]) : 112;
   const int reps = argc > 3 ? std::atoi(argv[3]) : 20;
   if (n % 16 || n > sqlm::kCRMaxN || p < 1) { std::printf("bad shape\n"); return 1; }
@@ -151,12 +152,14 @@ int main(int argc, char **argv) {
     CK(hipMemcpyAsync(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice, st));
     CK(hipMemcpyAsync(dflags, one, 16, hipMemcpyHostToDevice, st));
     CK(hipEventRecord(e0, st));
+    if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "launch %d ...\n", it);
     sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st, &ps);
     CK(hipEventRecord(e1, st));
     CK(hipStreamSynchronize(st));
     CK(hipGetLastError());
     float ms = 0.f;
     CK(hipEventElapsedTime(&ms, e0, e1));
+    if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "launch %d: %.3f ms\n", it, ms);
     if (it >= 2) { best = std::min(best, (double)ms); sum += ms; }
   }
   std::vector<double> x(g.size());
@@ -164,7 +167,8 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(x.data(), dx, x.size() * 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(fl, dflags, 16, hipMemcpyDeviceToHost));
   flag = fl[0];
-  {  // the same system through the per-level launches: the persistent solve must give the same bits
+  if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "persistent launches done\n");
+  if (!std::getenv("CRB_NO_LEVELS")) {  // the same system through the per-level launches: the persistent solve must give the same bits
     CK(hipMemcpy(dD, D.data(), nb * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dE, E.data(), nb * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice));
@@ -182,6 +186,7 @@ int main(int argc, char **argv) {
     std::printf("{\"persist_vs_levels\": {\"differing\": %zu, \"max_abs\": %.3e}, \"dev_err\": %d}\n", ndiff, dmax,
                 fl[1]);
   }
+  if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "levels comparison done\n");
   if (p == 2 && std::getenv("SQLM_CR_LEGACY")) {  // stage-by-stage host check of the one-level solve (Linv layout)
     std::vector<double> dDh(nb), dLh(nb), dAh(nb), dgh(g.size());
     CK(hipMemcpy(dDh.data(), dD, nb * 8, hipMemcpyDeviceToHost));
