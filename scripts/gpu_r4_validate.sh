@@ -1,15 +1,42 @@
 #!/bin/bash
-# Round-4 validation on MI355X: forced-timeout build, focused GPU tests
+# Round-4 validation on MI355X: the factor with its pipe wave against the
+# one-wave chain (same bits, cycles), forced-timeout build, focused GPU tests
 # (schedules bit for bit, parity, spec, concurrent, EG vs glibc), and short
 # A/B benches of the device-side LM loop + pose fusion.
 set -o pipefail
 mkdir -p gpurun_out
 out=gpurun_out/r4_validate.log
 : > $out
+echo "== factor: pipe wave vs solo (x_hash must match)" >> $out
+for shape in "278 112" "4 64" "9 112" "2 112"; do
+  for b in cr_bench cr_bench_solo; do
+    echo "-- $b $shape" >> $out
+    CRB_NO_LEVELS=1 timeout -k 10 60 ./tools/$b $shape 20 > gpurun_out/crb_tmp.log 2>&1
+    rc=$?
+    grep -v "aug_wave\|aug_phase\|top_phase" gpurun_out/crb_tmp.log >> $out
+    echo "rc=$rc" >> $out
+    [ $rc -eq 0 ] || exit 1
+  done
+done
+echo "== small bands: sequential one-launch solve vs cyclic reduction" >> $out
+for shape in "4 64" "5 80" "3 48"; do
+  for seqoff in 0 1; do
+    echo "-- cr_bench $shape no_seq=$seqoff" >> $out
+    if [ $seqoff = 1 ]; then export SQLM_NO_CR_SEQ=1; else unset SQLM_NO_CR_SEQ; fi
+    CRB_NO_LEVELS=1 timeout -k 10 60 ./tools/cr_bench $shape 50 > gpurun_out/crb_tmp.log 2>&1
+    rc=$?
+    grep -v "aug_wave\|aug_phase\|top_phase" gpurun_out/crb_tmp.log >> $out
+    echo "rc=$rc" >> $out
+    [ $rc -eq 0 ] || exit 1
+  done
+done
+unset SQLM_NO_CR_SEQ
+timeout -k 10 60 ./tools/group_probe >> $out 2>&1 || exit 1
 echo "== forced timeout (expect flag 0, dev_err 1, rc 3)" >> $out
 timeout -k 10 60 ./tools/cr_bench_tmo 9 112 2 2>&1 | grep -v "aug_wave\|aug_phase\|top_phase" >> $out; echo "tmo rc=$?" >> $out
 timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
-  tests/test_gpu_schedules.py tests/test_gpu_spec.py tests/test_gpu_parity.py tests/test_gpu_concurrent.py tests/test_gpu_sharded.py \
+  tests/test_gpu_cr_fuse.py "tests/test_gpu_parity.py::test_small_rcs_superblock_counts" tests/test_gpu_schedules.py tests/test_gpu_spec.py tests/test_gpu_parity.py \
+  tests/test_gpu_concurrent.py tests/test_gpu_sharded.py \
   "tests/test_eg_gpu.py::test_eg_bench_size_first_iteration" > gpurun_out/pytest_r4.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> $out
@@ -20,4 +47,6 @@ for v in new base; do
   timeout -k 10 200 python -u bench.py --config lba --steps 200 --warmup 20 --no-cpu-baseline --no-extras > gpurun_out/bench_lba_$v.json 2> gpurun_out/bench_lba_$v.err || exit 1
   timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/bench_gba_$v.json 2> gpurun_out/bench_gba_$v.err || exit 1
 done
+unset SQLM_NO_DLM SQLM_NO_POSE_FUSE
 echo "all ok" >> $out
+SQLM_PREP_TIMING=1 timeout -k 10 120 python -u bench.py --config lba --steps 50 --warmup 5 --no-cpu-baseline --no-extras > gpurun_out/bench_lba_prep.json 2> gpurun_out/bench_lba_prep.err || exit 1

@@ -2373,7 +2373,8 @@ int sqlm_get_exec_info(sqlm_ctx *c, int out[8]) {
   const bool persist = pl.enabled && !pl.R && cr_persist_enabled() && c->crp.p == pl.p && c->crp.n == pl.n;
   for (int k = 0; k < 8; ++k) out[k] = 0;
   out[0] = c->d.obs_f32 ? 1 : 0;
-  out[1] = c->d.nP == 0 ? 0 : !pl.enabled ? 4 : pl.R ? 3 : persist ? 2 : 1;
+  const bool seq = pl.enabled && !pl.R && !persist && cr_seq_enabled() && cr_seq_fits(pl.p, pl.n);
+  out[1] = c->d.nP == 0 ? 0 : !pl.enabled ? 4 : pl.R ? 3 : persist ? 2 : seq ? 5 : 1;
   out[2] = persist ? c->crp.ntasks : 0;
   out[3] = persist ? c->crp.G : 0;
   return SQLM_OK;

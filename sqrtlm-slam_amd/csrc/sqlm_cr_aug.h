@@ -47,7 +47,15 @@
 namespace sqlm {
 namespace aug {
 
-constexpr int kWaves = 16, kThreads = 64 * kWaves, kMaxNt = kCRMaxN / 16, kWorkers = 12;
+// wave 0: the diagonal chain; wave 1: its pipe wave (the chain's off-chain
+// MFMAs, on another SIMD); waves 4, 8, 12 (wave 0's SIMD) idle; the other 11
+// are column workers. SQLM_AUG_SOLO (A/B builds): wave 0 alone, 12 workers.
+#ifdef SQLM_AUG_SOLO
+constexpr bool kPipe = false;
+#else
+constexpr bool kPipe = true;
+#endif
+constexpr int kWaves = 16, kThreads = 64 * kWaves, kMaxNt = kCRMaxN / 16, kWorkers = kPipe ? 11 : 12;
 constexpr int kPairs = kMaxNt * (kMaxNt - 1) / 2;
 enum : int { kNone = 0, kColD = 1, kColI0 = 3, kColEt = 4, kColE = 5, kColG = 6 };
 
@@ -62,6 +70,11 @@ struct Shared {
   double Hp[kMaxNt][256];   // column J's tiles (J-1, J) and (J, J) through step J-3, handed to wave 0
   double Hq[kMaxNt][256];
   int fT[kMaxNt], fU[kPairs], fH[kMaxNt];
+  // diagonal wave -> pipe wave: group a's A operand (W) and rank-4 rows (op),
+  // one slot per group reused every step (flag value = step + 1); pipe wave ->
+  // diagonal wave: the next diagonal tile (flag value = its step)
+  double Ga[4][64], Go[4][64], Dn[256];
+  int fA[4], fO[4], fD;
   double by[kCRMaxN], bx[kCRMaxN], br[16];  // BACK: y, x and one block row's right-hand side
 };
 
@@ -75,13 +88,18 @@ __device__ __forceinline__ double rl(double v, int l) {
 }
 
 // 1/sqrt(x) by v_rsq_f64 and one Newton step; a non-positive pivot is flagged
+// (off the chain: the value is not guarded -- a flagged factor is discarded
+// whole, and a NaN or inf in it changes no control flow)
 __device__ __forceinline__ double rsqn(double x, bool &bad) {
   bad |= !(x > 0.0);
-  const double v = x > 0.0 ? x : 1.0;
-  double y = __builtin_amdgcn_rsq(v);
-  const double hh = 0.5 * v * y;
+  double y = __builtin_amdgcn_rsq(x);
+  const double hh = 0.5 * x * y;
   return fma(y, fma(-hh, y, 0.5), y);
 }
+
+// per-lane select of two values (a v_cndmask pair: the operands are plain
+// values, so the front end emits a select, never a branch on the lane)
+__device__ __forceinline__ double sel(bool c, double x, double y) { return c ? x : y; }
 
 __device__ __forceinline__ d4 mfma(double a, double b, const d4 &c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -146,9 +164,24 @@ __device__ __forceinline__ bool spin(int *f) {
 // Producer side: the DS instructions of one wave execute in order, so the flag
 // store lands after the data stores issued before it; only the compiler must
 // not move them (no s_waitcnt: the wave goes on while the stores drain).
-__device__ __forceinline__ void raise_flag(int *f, int lane) {
+__device__ __forceinline__ void raise_flag(int *f, int lane, int val = 1) {
   __asm__ volatile("" ::: "memory");
-  if (lane == 0) __atomic_store_n((lds_int *)f, 1, __ATOMIC_RELAXED);
+  if (lane == 0) __atomic_store_n((lds_int *)f, val, __ATOMIC_RELAXED);
+}
+// Wait until a step-numbered flag reaches val; no sleep between polls (the
+// hand-offs between the diagonal wave and its pipe wave are the chain itself).
+// Bounded and fail-loud like spin().
+__device__ __forceinline__ bool spin_to(int *f, int val) {
+  lds_int *p = (lds_int *)f;
+  int it = 0;
+  for (; __atomic_load_n(p, __ATOMIC_RELAXED) < val && it < 16 * kSpinLimit; ++it) {
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#ifdef SQLM_SPIN_FORCE_TIMEOUT
+  return false;
+#else
+  return it < 16 * kSpinLimit;
+#endif
 }
 
 __device__ __forceinline__ void put_tile(double *dst, const d4 &t, int lane) {
@@ -162,47 +195,70 @@ __device__ __forceinline__ d4 get_tile(const double *src, int lane) {
   return t;
 }
 
-// Step k on the diagonal tile Dg, in four rank-4 groups; T_k = L_kk^-1 in Tt.
-// With PQ the same groups also finish P = tile (k, k+1) -> U_k,k+1 and take
-// the step-k piece of the next diagonal tile Q = (k+1, k+1) -= U_k,k+1^T
-// U_k,k+1: the critical path of the next step stays on this wave's SIMD.
+// Group a of a diagonal step: the 4x4 pivot block of Dg (rows / columns
+// 4a .. 4a+3, element a of lanes 16 r + 4a + c), its Cholesky on uniform values
+// from readlane, and W = (U44^T)^-1 as the A operand of the group's MFMAs:
+// lane (b, i) holds W[i][b] (column b; zero for i >= 4).
+__device__ __forceinline__ double group_pivot(const d4 &Dg, int a, int lane, bool &bad) {
+  const int b = lane >> 4, i = lane & 15;
+  const bool b0 = b == 0, b1 = b == 1, b2 = b == 2, b3 = b == 3, i3 = i == 3;
+  const double m00 = rl(Dg[a], 4 * a), m01 = rl(Dg[a], 4 * a + 1), m02 = rl(Dg[a], 4 * a + 2),
+               m03 = rl(Dg[a], 4 * a + 3);
+  const double m11 = rl(Dg[a], 16 + 4 * a + 1), m12 = rl(Dg[a], 16 + 4 * a + 2), m13 = rl(Dg[a], 16 + 4 * a + 3);
+  const double m22 = rl(Dg[a], 32 + 4 * a + 2), m23 = rl(Dg[a], 32 + 4 * a + 3);
+  const double m33 = rl(Dg[a], 48 + 4 * a + 3);
+  // U44 (upper, U44^T U44 = M44) with d_r = 1 / U44[r][r]
+  const double d0 = rsqn(m00, bad);
+  const double u01 = m01 * d0, u02 = m02 * d0, u03 = m03 * d0;
+  const double d1 = rsqn(fma(-u01, u01, m11), bad);
+  const double u12 = fma(-u01, u02, m12) * d1, u13 = fma(-u01, u03, m13) * d1;
+  const double d2 = rsqn(fma(-u12, u12, fma(-u02, u02, m22)), bad);
+  const double u23 = fma(-u12, u13, fma(-u02, u03, m23)) * d2;
+  const double d3 = rsqn(fma(-u23, u23, fma(-u13, u13, fma(-u03, u03, m33))), bad);
+  // Every entry of W is a uniform value (column cb below, cb a constant); the
+  // lane picks its own by selects, so the wave never branches on its lane.
+  double W[4][4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const double w0 = cb == 0 ? d0 : 0.0;
+    const double w1 = cb == 1 ? d1 : (cb < 1 ? -d1 * (u01 * w0) : 0.0);
+    const double w2 = cb == 2 ? d2 : (cb < 2 ? -d2 * fma(u12, w1, u02 * w0) : 0.0);
+    W[0][cb] = w0;
+    W[1][cb] = w1;
+    W[2][cb] = w2;
+    W[3][cb] = cb == 3 ? d3 : -d3 * fma(u23, w2, fma(u13, w1, u03 * w0));
+  }
+  // rows 0..2 first (ready before d3), row 3 -- the chain's last -- selected last
+  double r012 = 0.0;
+#pragma unroll
+  for (int r = 2; r >= 0; --r) {
+    const double wr = sel(b0, W[r][0], sel(b1, W[r][1], sel(b2, W[r][2], W[r][3])));
+    r012 = sel(i == r, wr, r012);
+  }
+  const double w3b = sel(b3, W[3][3], sel(b2, W[3][2], sel(b1, W[3][1], W[3][0])));
+  return sel(i3, w3b, r012);
+}
+
+// Step k on the diagonal tile Dg, in four rank-4 groups, all on one wave
+// (SQLM_AUG_SOLO builds, A/B only); T_k = L_kk^-1 in Tt. With PQ the same
+// groups also finish P = tile (k, k+1) -> U_k,k+1 and take the step-k piece of
+// the next diagonal tile Q = (k+1, k+1) -= U_k,k+1^T U_k,k+1.
 template <bool PQ>
 __device__ __forceinline__ void diag_groups(d4 Dg, d4 &P, d4 &Q, d4 &Tt, int lane, bool &bad) {
-  const int b = lane >> 4, i = lane & 15, c = lane & 15;
+  const int c = lane & 15;
   const d4 zero = {0.0, 0.0, 0.0, 0.0};
   Tt = identity_tile(lane);
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
-    // the group's 4x4 pivot block: rows / columns 4a .. 4a+3 sit in element a
-    // of lanes 16 r + 4a + c (r = row - 4a, c = column - 4a)
-    const double m00 = rl(Dg[a], 4 * a), m01 = rl(Dg[a], 4 * a + 1), m02 = rl(Dg[a], 4 * a + 2),
-                 m03 = rl(Dg[a], 4 * a + 3);
-    const double m11 = rl(Dg[a], 16 + 4 * a + 1), m12 = rl(Dg[a], 16 + 4 * a + 2), m13 = rl(Dg[a], 16 + 4 * a + 3);
-    const double m22 = rl(Dg[a], 32 + 4 * a + 2), m23 = rl(Dg[a], 32 + 4 * a + 3);
-    const double m33 = rl(Dg[a], 48 + 4 * a + 3);
-    // U44 (upper, U44^T U44 = M44) with d_r = 1 / U44[r][r]
-    const double d0 = rsqn(m00, bad);
-    const double u01 = m01 * d0, u02 = m02 * d0, u03 = m03 * d0;
-    const double d1 = rsqn(fma(-u01, u01, m11), bad);
-    const double u12 = fma(-u01, u02, m12) * d1, u13 = fma(-u01, u03, m13) * d1;
-    const double d2 = rsqn(fma(-u12, u12, fma(-u02, u02, m22)), bad);
-    const double u23 = fma(-u12, u13, fma(-u02, u03, m23)) * d2;
-    const double d3 = rsqn(fma(-u23, u23, fma(-u13, u13, fma(-u03, u03, m33))), bad);
-    // W = (U44^T)^-1, lower; lane (b, i) of the A operand holds W[i][b] (column b)
-    const double w0 = b == 0 ? d0 : 0.0;
-    const double w1 = b == 1 ? d1 : (b < 1 ? -d1 * (u01 * w0) : 0.0);
-    const double w2 = b == 2 ? d2 : (b < 2 ? -d2 * fma(u12, w1, u02 * w0) : 0.0);
-    const double w3 = b == 3 ? d3 : -d3 * fma(u23, w2, fma(u13, w1, u03 * w0));
-    const double aop = i == 0 ? w0 : i == 1 ? w1 : i == 2 ? w2 : i == 3 ? w3 : 0.0;
+    const double aop = group_pivot(Dg, a, lane, bad);
     // finished rows 4a .. 4a+3 = W M4 (rows 0..3 of the product, element 0);
     // the rank-4 update of the rows and columns past the group
     const d4 Xd = mfma(aop, Dg[a], zero);
     const double op = c >= 4 * a + 4 ? Xd[0] : 0.0;
     Dg = mfma(-op, op, Dg);
     __builtin_amdgcn_sched_barrier(0);  // the chain's update is issued first
-    // off the chain (in the pipe while the next group's scalar work runs):
-    // T_k = the same groups on the identity; with PQ, P = (k, k+1) -> U_k,k+1
-    // and the step-k piece of the next diagonal Q = (k+1, k+1) -= U^T U
+    // off the chain: T_k = the same groups on the identity; with PQ, P = (k, k+1)
+    // -> U_k,k+1 and the step-k piece of the next diagonal Q = (k+1, k+1) -= U^T U
     const d4 Xt = mfma(aop, Tt[a], zero);
     Tt[a] = Xt[0];
     Tt = mfma(-op, Xt[0], Tt);
@@ -265,9 +321,10 @@ __device__ __forceinline__ void store_tile(double *P, int n, int r0, int c0, con
 // D columns carried by workers: J = 1 .. nt-1 (LINV: 0 .. nt-1, column 0 then
 // carries identity column 1)
 __host__ __device__ __forceinline__ int d_columns(int nt, bool linv) { return linv ? nt : nt - 1; }
-// E / g columns of a superblock
-__host__ __device__ __forceinline__ int extra_columns(int nt, bool level, bool right) {
-  return (level ? nt : 0) + (level && right ? nt : 0) + 1;
+// E / g columns of a superblock: E_{I-h}^T (left, a level step), E_I (right)
+// and g
+__host__ __device__ __forceinline__ int extra_columns(int nt, bool left, bool right) {
+  return (left ? nt : 0) + (right ? nt : 0) + 1;
 }
 // workers left for the E / g columns (LINV also carries identity column 0)
 __host__ __device__ __forceinline__ int fixed_columns(int nt, bool linv) { return d_columns(nt, linv) + (linv ? 1 : 0); }
@@ -277,7 +334,7 @@ inline int min_split(int nt, bool linv, int ne) {
 }
 
 // role of a worker (q = 0 .. kWorkers-1) of a workgroup serving one superblock
-__device__ __forceinline__ void column_of(int q, int nt, bool linv, bool level, bool right, int split, int sidx,
+__device__ __forceinline__ void column_of(int q, int nt, bool linv, bool left, bool right, int split, int sidx,
                                           int &type, int &J) {
   J = 0;
   const int nd = d_columns(nt, linv);
@@ -291,7 +348,7 @@ __device__ __forceinline__ void column_of(int q, int nt, bool linv, bool level, 
     return;
   }
   const int e = (q - fixed_columns(nt, linv)) * split + sidx;
-  const int net = level ? nt : 0, nee = (level && right) ? nt : 0;
+  const int net = left ? nt : 0, nee = right ? nt : 0;
   if (e < net) {
     type = kColEt;
     J = e;
@@ -374,7 +431,9 @@ __device__ __forceinline__ void cr_fail(const CRView &v, int lane) {
 }
 
 // MODE 0: level step (A_I, C_I, z_I and the back-substitution factor).
-// MODE 1: factor only (z_I and the factor). LINV: the factor is Linv_I
+// MODE 1: factor only (z_I and the factor).
+// MODE 2: step I of the sequential block-tridiagonal factorization (k_cr_seq):
+// C_I = L^-1 E_I (when I + h < p), z_I and the factor; no left column. LINV: the factor is Linv_I
 // (lower, dense tiles); otherwise the upper U tiles with T_k on the diagonal.
 // Superblock I, workgroup sidx of the split that serve it. Every thread of the
 // workgroup enters; waves return as their role ends (no barrier after the
@@ -385,12 +444,15 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
   using namespace aug;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n = v.n, nt = n >> 4;
-  const bool level = MODE == 0, right = level && I + h < v.p, first = sidx == 0;
+  const bool left = MODE == 0, right = MODE != 1 && I + h < v.p, first = sidx == 0;
   bool tmo = false;
-  for (int t = threadIdx.x; t < 2 * kMaxNt + kPairs; t += blockDim.x) {
+  for (int t = threadIdx.x; t < 2 * kMaxNt + kPairs + 9; t += blockDim.x) {
     if (t < kMaxNt) sh.fT[t] = 0;
     else if (t < kMaxNt + kPairs) sh.fU[t - kMaxNt] = 0;
     else if (t < 2 * kMaxNt + kPairs) sh.fH[t - kMaxNt - kPairs] = 0;
+    else if (t < 2 * kMaxNt + kPairs + 4) sh.fA[t - 2 * kMaxNt - kPairs] = 0;
+    else if (t < 2 * kMaxNt + kPairs + 8) sh.fO[t - 2 * kMaxNt - kPairs - 4] = 0;
+    else sh.fD = 0;
   }
   __syncthreads();
 #ifdef SQLM_SPIN_DEBUG
@@ -406,7 +468,105 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
   const int ldd = dense ? v.ld : n;
   const double *Dblk = dense ? v.D : blk(v.D, I, n);
   bool bad = false;
-  if (wave == 0) {  // ---- the diagonal wave
+  if (kPipe && wave == 0) {  // ---- the diagonal wave: the chain only
+    __builtin_amdgcn_s_setprio(3);
+    AUG_PROF(1);
+    const int c = lane & 15;
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    d4 Dg = dense ? load_tile_sym(Dblk, ldd, 0, lane) : load_tile(Dblk, n, 0, 0, lane);
+    for (int k = 0; k < nt; ++k) {
+      AUG_STAMP(0, k, 0);
+      if (k > 0) {  // diagonal tile k, updated through step k-1 by the pipe wave
+        tmo |= !spin_to(&sh.fD, k);
+        Dg = get_tile(sh.Dn, lane);
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const double aop = group_pivot(Dg, a, lane, bad);
+        sh.Ga[a][lane] = aop;
+        raise_flag(&sh.fA[a], lane, k + 1);
+        if (a == 3) break;  // the last group updates nothing past the tile
+        // finished rows 4a .. 4a+3 = W M4 (element 0); the rank-4 update of the
+        // rows and columns past the group
+        const d4 Xd = mfma(aop, Dg[a], zero);
+        const double op = c >= 4 * a + 4 ? Xd[0] : 0.0;
+        Dg = mfma(-op, op, Dg);
+        sh.Go[a][lane] = op;
+        raise_flag(&sh.fO[a], lane, k + 1);
+      }
+    }
+    if (bad && lane == 0) v.flags[0] = 0;
+    if (tmo) cr_fail(v, lane);
+    return;
+  }
+  if (kPipe && wave == 1) {  // ---- the pipe wave: T_k, U_k,k+1 and the next diagonal
+    __builtin_amdgcn_s_setprio(3);
+    double *Lb = blk(v.L, I, n);
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    d4 P = zero, Q = zero;
+    if (nt > 1) {
+      P = load_tile_t(Dblk, ldd, 0, 16, lane);  // U tile (0, 1) from the lower block (1, 0)
+      Q = dense ? load_tile_sym(Dblk, ldd, 16, lane) : load_tile(Dblk, n, 16, 16, lane);
+    }
+    for (int k = 0; k < nt; ++k) {
+      d4 Tt = identity_tile(lane);
+      const bool pq = k + 1 < nt;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        tmo |= !spin_to(&sh.fA[a], k + 1);
+        const double aop = sh.Ga[a][lane];
+        const d4 Xt = mfma(aop, Tt[a], zero);
+        d4 Xp = zero;
+        if (pq) {
+          Xp = mfma(aop, P[a], zero);
+          Q = mfma(-Xp[0], Xp[0], Q);
+        }
+        double op = 0.0;  // the last group's rows update nothing (the diagonal wave's op is 0 there)
+        if (a < 3) {
+          tmo |= !spin_to(&sh.fO[a], k + 1);
+          op = sh.Go[a][lane];
+        }
+        Tt[a] = Xt[0];
+        Tt = mfma(-op, Xt[0], Tt);
+        if (pq) {
+          P[a] = Xp[0];
+          P = mfma(-op, Xp[0], P);
+        }
+      }
+      if (pq) {  // the next diagonal first: it is the chain
+        put_tile(sh.Dn, Q, lane);
+        raise_flag(&sh.fD, lane, k + 1);
+      }
+      {  // T_k for the workers (row-major) and, U/T layout, for the back substitution
+        const int k4 = lane >> 4, c = lane & 15;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sh.T[k][(k4 + 4 * j) * kTp + c] = Tt[j];
+        raise_flag(&sh.fT[k], lane);
+        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * k, Tt, lane);
+      }
+      AUG_PROF(2 + k);
+      if (pq) {  // U_k,k+1 feeds the trailing updates of row k+1
+        put_tile(sh.U[pair_id(k, k + 1)], P, lane);
+        raise_flag(&sh.fU[pair_id(k, k + 1)], lane);
+        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * (k + 1), P, lane);
+      }
+      if (k + 2 < nt) {  // the next step's P = (k+1, k+2) and Q = (k+2, k+2) through step k
+        tmo |= !spin(&sh.fH[k + 2]);
+        d4 P2 = get_tile(sh.Hp[k + 2], lane), Q2 = get_tile(sh.Hq[k + 2], lane);
+        tmo |= !spin(&sh.fU[pair_id(k, k + 2)]);
+        const d4 X = get_tile(sh.U[pair_id(k, k + 2)], lane);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) Q2 = mfma(-X[s4], X[s4], Q2);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) P2 = mfma(-P[s4], X[s4], P2);
+        P = P2;
+        Q = Q2;
+      }
+    }
+    if (tmo) cr_fail(v, lane);
+    return;
+  }
+  if (!kPipe && wave == 0) {  // ---- the diagonal wave alone (SQLM_AUG_SOLO)
     __builtin_amdgcn_s_setprio(3);
     AUG_PROF(1);
     double *Lb = blk(v.L, I, n);
@@ -460,9 +620,9 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
     return;
   }
   if ((wave & 3) == 0) return;  // the diagonal wave's SIMD partners stay idle
-  const int q = wave - (wave >> 2) - 1;
+  const int q = wave - (wave >> 2) - (kPipe ? 2 : 1);
   int type, J;
-  column_of(q, nt, LINV, level, right, split, sidx, type, J);
+  column_of(q, nt, LINV, left, right, split, sidx, type, J);
   if (type == kNone) return;
   // ---- load this wave's column
   d4 t[kMaxNt];

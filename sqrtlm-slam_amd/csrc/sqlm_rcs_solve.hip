@@ -1744,8 +1744,10 @@ __device__ __noinline__ void pt_up(const CRView v, int h, int lb) { cr_update_it
 // k_cr_back_u<false> for the persistent solve (16 waves, <= 128 VGPRs): the
 // neighbours' solutions staged in LDS, y = z_I - A_I x_{I-h} - C_I x_{I+h}
 // with one 8-row slice per wave, then the blocked backward substitution of
-// back_u_body.
-__device__ __noinline__ void pt_bk(const CRView v, int h, int I) {
+// back_u_body. LEFT = false (k_cr_seq): no A_I term, y = z_I - C_I x_{I+h}.
+// WT: x stored write-through (read by other workgroups of the launch).
+template <bool LEFT, bool WT>
+__device__ __forceinline__ void back_lean_body(const CRView &v, int h, int I) {
   double *sm = reinterpret_cast<double *>(cr_persist_lds);
   double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN, *xl = sm + 3 * kCRMaxN, *xr = sm + 4 * kCRMaxN;
   int *fx = reinterpret_cast<int *>(sm + 5 * kCRMaxN);
@@ -1754,7 +1756,7 @@ __device__ __noinline__ void pt_bk(const CRView v, int h, int I) {
   const bool right = I + h < v.p;
   if (threadIdx.x < aug::kMaxNt) fx[threadIdx.x] = 0;
   for (int k = threadIdx.x; k < 2 * n; k += blockDim.x) {
-    if (k < n) xl[k] = v.x[(size_t)(I - h) * n + k];
+    if (k < n) xl[k] = LEFT ? v.x[(size_t)(I - h) * n + k] : 0.0;
     else xr[k - n] = right ? v.x[(size_t)(I + h) * n + k - n] : 0.0;
   }
   // this wave's U row and T_i (waves < nt): in flight during the right-hand side
@@ -1778,7 +1780,7 @@ __device__ __noinline__ void pt_bk(const CRView v, int h, int I) {
 #pragma unroll
     for (int uu = 0; uu < kCRMaxN / 16; ++uu) {
       const int cc = kclamp(16 * uu + 2 * lo, n) >> 1;
-      a[uu] = A[row * hn + cc];
+      a[uu] = LEFT ? A[row * hn + cc] : d2{0.0, 0.0};
       c[uu] = right ? C[row * hn + cc] : d2{0.0, 0.0};
     }
     double s = 0.0;
@@ -1786,7 +1788,7 @@ __device__ __noinline__ void pt_bk(const CRView v, int h, int I) {
     for (int uu = 0; uu < kCRMaxN / 16; ++uu)
       if (16 * uu < n) {
         const int cc = 16 * uu + 2 * lo;
-        s += a[uu].x * xl[cc] + a[uu].y * xl[cc + 1];
+        if (LEFT) s += a[uu].x * xl[cc] + a[uu].y * xl[cc + 1];
         if (right) s += c[uu].x * xr[cc] + c[uu].y * xr[cc + 1];
       }
 #pragma unroll
@@ -1817,10 +1819,72 @@ __device__ __noinline__ void pt_bk(const CRView v, int h, int I) {
   x += __shfl_xor(x, 32, 64);
   if (q == 0) {
     xs[16 * i + r] = x;
-    st_d<true>(v.x + (size_t)I * n + 16 * i + r, x);
+    st_d<WT>(v.x + (size_t)I * n + 16 * i + r, x);
   }
   aug::raise_flag(&fx[i], lane);
   if (tmo) cr_fail(v, lane);
+}
+__device__ __noinline__ void pt_bk(const CRView v, int h, int I) { back_lean_body<true, true>(v, h, I); }
+
+// ---- sequential block-tridiagonal solve (small systems, one launch) ----------
+// For a band of a few superblocks every cyclic-reduction level is a chain of
+// dependent launches (factor, update, back substitution: >= 4.5 us each). One
+// workgroup instead runs the block Thomas factorization of the same system
+// (linear_solver_eigen.h:94-124's Cholesky of S, block-tridiagonal):
+//   D'_I = D_I - C_{I-1}^T C_{I-1},  g'_I = g_I - C_{I-1}^T z_{I-1},
+//   D'_I = L_I L_I^T,  C_I = L_I^-1 E_I,  z_I = L_I^-1 g'_I   (k_cr_aug MODE 2)
+//   x_{p-1} = L^-T z_{p-1},  x_I = L_I^-T (z_I - C_I x_{I+1})  (back_lean_body)
+// with a barrier between the steps: the whole solve is one launch. Needs the
+// factor's columns in one workgroup: (nt - 1) D + nt E + g <= kWorkers.
+constexpr int kSeqMaxP = 5;
+bool cr_seq_fits(int p, int n) {
+  const int nt = n / 16;
+  return p >= 2 && p <= kSeqMaxP && aug::fixed_columns(nt, false) + aug::extra_columns(nt, false, true) <= aug::kWorkers;
+}
+
+// D'_I's lower tiles (R >= c) -= C_{I-1}^T C_{I-1} (MFMA over the 16-row slices
+// of C, in slice order), g'_I -= C_{I-1}^T z_{I-1}; every thread of the workgroup
+__device__ __noinline__ void seq_update(const CRView v, int I) {
+  const int n = v.n, nt = n >> 4, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const double *Cp = blk(v.C, I - 1, n);
+  double *D = blk(v.D, I, n);
+  int idx = 0;
+  for (int R = 0; R < nt; ++R)
+    for (int c = 0; c <= R; ++c, ++idx) {
+      if (idx % aug::kWaves != wave) continue;
+      d4 acc = aug::load_tile(D, n, 16 * R, 16 * c, lane);
+      for (int K = 0; K < nt; ++K) {
+        const d4 a = aug::load_tile(Cp, n, 16 * K, 16 * R, lane), b = aug::load_tile(Cp, n, 16 * K, 16 * c, lane);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc = aug::mfma(-a[s4], b[s4], acc);
+      }
+      aug::store_tile<false>(D, n, 16 * R, 16 * c, acc, lane);
+    }
+  for (int r = threadIdx.x; r < n; r += blockDim.x) {
+    double s = 0.0;
+    for (int k = 0; k < n; ++k) s = fma(Cp[(size_t)k * n + r], v.g[(size_t)(I - 1) * n + k], s);
+    v.g[(size_t)I * n + r] -= s;
+  }
+}
+
+// the steps as separate functions (one register allocation each, as k_cr_persist)
+__device__ __noinline__ void seq_factor(const CRView v, int I) { aug_body<2, false, false, false>(persist_shared(), v, 1, I, 1, 0); }
+__device__ __noinline__ void seq_back(const CRView v, int I) { back_lean_body<false, false>(v, 1, I); }
+
+__global__ __launch_bounds__(aug::kThreads) void k_cr_seq(CRView v) {
+  const int p = v.p;
+  for (int I = 0; I < p; ++I) {
+    if (I > 0) {
+      seq_update(v, I);
+      __syncthreads();
+    }
+    seq_factor(v, I);
+    __syncthreads();
+  }
+  for (int I = p - 1; I >= 0; --I) {
+    seq_back(v, I);
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CRTask *__restrict__ tasks,
@@ -1914,6 +1978,9 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CR
     id = __builtin_amdgcn_readfirstlane(s_id);
   }
 }
+
+// SQLM_NO_CR_SEQ=1: small systems take the cyclic reduction too (A/B, tests); read per call
+bool cr_seq_enabled() { return std::getenv("SQLM_NO_CR_SEQ") == nullptr; }
 
 bool cr_persist_enabled() {  // read per call (prepare, trial): tests switch it
   const char *e = std::getenv("SQLM_CR_PERSIST");
@@ -2043,6 +2110,10 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
   v.skip = skip;
   if (ps && ps->p == p && ps->n == n && ps->tasks && cr_persist_enabled()) {
     launch_cr_persist(v, *ps, st);
+    return;
+  }
+  if (cr_seq_enabled() && cr_seq_fits(p, n) && !cr_legacy()) {  // a few superblocks: one launch
+    hipLaunchKernelGGL(k_cr_seq, dim3(1), dim3(aug::kThreads), sizeof(aug::Shared), st, v);
     return;
   }
   const size_t lds = cr_factor_lds(n);

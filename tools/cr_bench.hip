@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <random>
 #include <vector>
@@ -265,7 +266,15 @@ int main(int argc, char **argv) {
       rmax = std::max(rmax, std::fabs(s - g[(size_t)I * n + r]));
       gmax = std::max(gmax, std::fabs(g[(size_t)I * n + r]));
     }
-  std::printf("{\"p\": %d, \"n\": %d, \"ms_best\": %.4f, \"ms_avg\": %.4f, \"flag\": %d, \"rel_residual\": %.3e}\n", p, n,
-              best, sum / reps, flag, rmax / gmax);
+  // FNV-1a over the solution's bits: builds that must agree bit for bit (e.g.
+  // the SQLM_AUG_SOLO factor layout) print the same hash
+  unsigned long long hx = 1469598103934665603ull;
+  for (double xv : x) {
+    unsigned long long b;
+    std::memcpy(&b, &xv, 8);
+    for (int k = 0; k < 8; ++k) { hx ^= (b >> (8 * k)) & 0xff; hx *= 1099511628211ull; }
+  }
+  std::printf("{\"p\": %d, \"n\": %d, \"ms_best\": %.4f, \"ms_avg\": %.4f, \"flag\": %d, \"rel_residual\": %.3e, "
+              "\"x_hash\": \"%016llx\"}\n", p, n, best, sum / reps, flag, rmax / gmax, hx);
   return (flag == 1 && rmax / gmax < 1e-10) ? 0 : 3;
 }
