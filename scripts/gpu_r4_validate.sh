@@ -8,10 +8,12 @@ mkdir -p gpurun_out
 out=gpurun_out/r4_validate.log
 : > $out
 echo "== factor: pipe wave vs solo (x_hash must match)" >> $out
-for shape in "278 112" "4 64" "9 112" "2 112"; do
-  for b in cr_bench cr_bench_solo; do
+for shape in "278 112" "4 112" "9 112" "2 112" "17 96"; do
+  for b in cr_bench cr_bench_solo cr_bench_nodeep; do
     echo "-- $b $shape" >> $out
-    CRB_NO_LEVELS=1 timeout -k 10 60 ./tools/$b $shape 20 > gpurun_out/crb_tmp.log 2>&1
+    exe=$b; extra=""
+    if [ $b = cr_bench_nodeep ]; then exe=cr_bench; extra="SQLM_NO_DEEP_BACK=1"; fi
+    env $extra CRB_NO_LEVELS=1 timeout -k 10 60 ./tools/$exe $shape 20 > gpurun_out/crb_tmp.log 2>&1
     rc=$?
     grep -v "aug_wave\|aug_phase\|top_phase" gpurun_out/crb_tmp.log >> $out
     echo "rc=$rc" >> $out
@@ -32,6 +34,11 @@ for shape in "4 64" "5 80" "3 48"; do
 done
 unset SQLM_NO_CR_SEQ
 timeout -k 10 60 ./tools/group_probe >> $out 2>&1 || exit 1
+echo "== persistent all-levels CR (opt-in, SQLM_CR_PERSIST=1) on config 4's band" >> $out
+SQLM_CR_PERSIST=1 timeout -k 10 120 ./tools/cr_bench 278 112 20 > gpurun_out/crb_tmp.log 2>&1
+rc=$?
+grep -v "aug_wave\|aug_phase\|top_phase" gpurun_out/crb_tmp.log >> $out
+echo "rc=$rc" >> $out
 echo "== forced timeout (expect flag 0, dev_err 1, rc 3)" >> $out
 timeout -k 10 60 ./tools/cr_bench_tmo 9 112 2 2>&1 | grep -v "aug_wave\|aug_phase\|top_phase" >> $out; echo "tmo rc=$?" >> $out
 timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
