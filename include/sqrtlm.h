@@ -176,7 +176,7 @@ int sqlm_get_rcs_layout(sqlm_ctx *ctx, int out[8]);
  * 1 cyclic reduction as per-level launches, 2 cyclic reduction as one
  * persistent launch (k_cr_persist), 3 band + border, 4 dense Cholesky,
  * 5 sequential block-tridiagonal factorization in one launch (k_cr_seq, a
- * band of at most 5 superblocks);
+ * band of at most 5 superblocks; opt-in, SQLM_CR_SEQ=1);
  * out[2] = tasks of the persistent solve, out[3] = its workgroups;
  * out[4..7] = 0 (reserved). */
 int sqlm_get_exec_info(sqlm_ctx *ctx, int out[8]);

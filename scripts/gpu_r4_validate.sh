@@ -50,10 +50,12 @@ echo "pytest rc=$rc" >> $out
 tail -5 gpurun_out/pytest_r4.log >> $out
 [ $rc -eq 0 ] || exit 1
 for v in new base; do
-  if [ $v = base ]; then export SQLM_NO_DLM=1 SQLM_NO_POSE_FUSE=1; fi
+  if [ $v = base ]; then export SQLM_DLM=1 SQLM_NO_POSE_FUSE=1; fi
   timeout -k 10 200 python -u bench.py --config lba --steps 200 --warmup 20 --no-cpu-baseline --no-extras > gpurun_out/bench_lba_$v.json 2> gpurun_out/bench_lba_$v.err || exit 1
   timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/bench_gba_$v.json 2> gpurun_out/bench_gba_$v.err || exit 1
 done
-unset SQLM_NO_DLM SQLM_NO_POSE_FUSE
+unset SQLM_DLM SQLM_NO_POSE_FUSE
 echo "all ok" >> $out
 SQLM_PREP_TIMING=1 timeout -k 10 120 python -u bench.py --config lba --steps 50 --warmup 5 --no-cpu-baseline --no-extras > gpurun_out/bench_lba_prep.json 2> gpurun_out/bench_lba_prep.err || exit 1
+SQLM_LIB_PATH=$PWD/sqrtlm-slam_amd/sqrtlm/libsqrtlm_lm256.so timeout -k 10 200 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-extras > gpurun_out/bench_gba_lm256.json 2> gpurun_out/bench_gba_lm256.err || exit 1
+echo "lm256 done" >> $out

@@ -1815,8 +1815,11 @@ void flush_cam_timers(sqlm_ctx *c) {
 }
 
 // Host loop: every trial's scalars come back before the next trial is
-// enqueued, and the host applies lm_decide (the timing run, sharded runs, the
-// row-kernel RCS fallback, SQLM_NO_DLM=1).
+// enqueued, and the host applies lm_decide. The default: the device-side loop
+// (lm_device, SQLM_DLM=1) measured slower on MI355X -- every per-trial kernel
+// then starts with a dependent load of the control block, which costs more
+// than the host turnaround it hides (config 4 703 -> 649-675 it/s, config 2
+// 5.58-5.61k -> 5.40k it/s; profiles/r04/ab_dlm_fuse_r4.log).
 int lm_host(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
   while (!L.done) {
     if (L.qmax == 0 && L.its > 0) {  // the next iteration (sparse_optimizer.cpp:376-414)
@@ -1842,8 +1845,8 @@ int lm_host(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
 // from every kernel at once. The caller's stop flag is mirrored into a mapped
 // word the decision reads.
 bool dlm_ok(const sqlm_ctx *c) {
-  const bool off = std::getenv("SQLM_NO_DLM") != nullptr;  // read per run: tests switch it
-  return !off && c->ctl_dev && c->ctl_host && c->mbox && c->stop_map_dev && c->spec && c->use_tiles && !c->timing && !c->htrace &&
+  const bool on = std::getenv("SQLM_DLM") != nullptr;  // read per run: tests switch it
+  return on && c->ctl_dev && c->ctl_host && c->mbox && c->stop_map_dev && c->spec && c->use_tiles && !c->timing && !c->htrace &&
          !c->comm.enabled();
 }
 

@@ -383,8 +383,8 @@ struct CRPersist {
 };
 // SQLM_CR_PERSIST=1 selects it (until validated on MI355X: per-level launches by default)
 bool cr_persist_enabled();
-// one-launch sequential solve of a small band (k_cr_seq): SQLM_NO_CR_SEQ unset
-// and at most kSeqMaxP superblocks whose factor columns fit one workgroup
+// one-launch sequential solve of a small band (k_cr_seq, opt-in: SQLM_CR_SEQ=1)
+// for at most kSeqMaxP superblocks whose factor columns fit one workgroup
 bool cr_seq_enabled();
 bool cr_seq_fits(int p, int n);
 int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu);  // 0 ok, -2 HIP error

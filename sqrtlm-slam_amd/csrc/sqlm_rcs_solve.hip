@@ -2000,14 +2000,19 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CR
   }
 }
 
-// SQLM_NO_DEEP_BACK=1: every back-substitution level as its own launch (A/B)
+// SQLM_CR_DEEP_BACK=1: the deepest back-substitution levels inside the top
+// factor's launch (k_cr_top_back). Measured slower on MI355X (config-4 band
+// solve 0.485 -> 0.592 ms, tools/cr_bench; profiles/r04/cr_ab_r4.log): opt-in only.
 static bool deep_back_enabled() {
-  static const bool v = std::getenv("SQLM_NO_DEEP_BACK") == nullptr;
+  static const bool v = std::getenv("SQLM_CR_DEEP_BACK") != nullptr;
   return v;
 }
 
-// SQLM_NO_CR_SEQ=1: small systems take the cyclic reduction too (A/B, tests); read per call
-bool cr_seq_enabled() { return std::getenv("SQLM_NO_CR_SEQ") == nullptr; }
+// SQLM_CR_SEQ=1: bands of <= kSeqMaxP superblocks by the one-launch sequential
+// factorization (k_cr_seq). Measured slower than the cyclic reduction on
+// MI355X (4 x 64: 0.162 vs 0.096 ms; 5 x 80: 0.245 vs 0.142 ms): opt-in only
+// (tests cover it). Read per call.
+bool cr_seq_enabled() { return std::getenv("SQLM_CR_SEQ") != nullptr; }
 
 bool cr_persist_enabled() {  // read per call (prepare, trial): tests switch it
   const char *e = std::getenv("SQLM_CR_PERSIST");

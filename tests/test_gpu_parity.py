@@ -59,17 +59,17 @@ def test_small_rcs_superblock_counts(gpu_ctx, oracle, n_pose, b_min, seq, monkey
     bandwidth + 1 cameras (SQLM_CR_B_MIN, the level counts above); otherwise
     the width the planner's latency estimate picks (fewer, wider superblocks,
     down to a single one). seq: bands of 2..5 superblocks whose factor fits one
-    workgroup take the one-launch sequential factorization (k_cr_seq, asserted
-    through sqlm_get_exec_info); otherwise (SQLM_NO_CR_SEQ) the per-level
+    workgroup take the one-launch sequential factorization (SQLM_CR_SEQ=1,
+    k_cr_seq, asserted through sqlm_get_exec_info); otherwise the per-level
     cyclic reduction."""
     if b_min:
         monkeypatch.setenv("SQLM_CR_B_MIN", "1")
     else:
         monkeypatch.delenv("SQLM_CR_B_MIN", raising=False)
     if seq:
-        monkeypatch.delenv("SQLM_NO_CR_SEQ", raising=False)
+        monkeypatch.setenv("SQLM_CR_SEQ", "1")
     else:
-        monkeypatch.setenv("SQLM_NO_CR_SEQ", "1")
+        monkeypatch.delenv("SQLM_CR_SEQ", raising=False)
     prob = synth.make_problem(n_pose, 50 * n_pose, pair_window=4, n_fixed=3, seed=100 + n_pose, robust=True)
     ref = oracle.OracleGraph(prob)
     nr, sr = ref.optimize(0, 10)
