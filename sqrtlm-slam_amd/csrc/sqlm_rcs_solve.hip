@@ -1871,22 +1871,24 @@ __device__ __noinline__ void seq_update(const CRView v, int I) {
 __device__ __noinline__ void seq_factor(const CRView v, int I) { aug_body<2, false, false, false>(persist_shared(), v, 1, I, 1, 0); }
 __device__ __noinline__ void seq_back(const CRView v, int I) { back_lean_body<false, false>(v, 1, I); }
 
-// The top of the cyclic reduction and the back substitution of its deepest
-// levels in one workgroup: x_0 = U_0^-1 z_0 (k_cr_aug<1, BACK>), then, level
-// by level down to h_stop, every odd superblock's x_I in turn (the levels whose
-// few odd superblocks would each be a dependent launch of a few microseconds;
-// back_lean_body is k_cr_back_u's arithmetic, bit for bit).
-__device__ __noinline__ void top_factor_back(const CRView v) { aug_body<1, false, true, false>(persist_shared(), v, 0, 0, 1, 0); }
-__device__ __noinline__ void deep_back(const CRView v, int h, int I) { back_lean_body<true, false>(v, h, I); }
+// The back substitution of the deepest cyclic-reduction levels in one
+// workgroup launch, right after the top solve: level by level from h_top / 2
+// down to h_stop, every odd superblock's x_I in turn (levels whose few odd
+// superblocks would each be a dependent launch of a few microseconds), by
+// k_cr_back_u's own body: the same bits.
 constexpr int kDeepBackOdd = 4;  // fold a back-substitution level with at most this many odd superblocks
 
-__global__ __launch_bounds__(aug::kThreads) void k_cr_top_back(CRView v, int h_top, int h_stop) {
-  top_factor_back(v);
-  __syncthreads();
+// (k_cr_back_u's geometry: one wave per 16-row slice, blockDim = 64 nt)
+// (a call per superblock: one register allocation for the body, as in the
+// single-level kernel, instead of one stretched over the loop)
+__device__ __noinline__ void deep_back_pass(const CRView v, int h, int I) {
+  back_u_body<false, false>(reinterpret_cast<double *>(cr_persist_lds), v, h, I);
+}
+__global__ __launch_bounds__(512) void k_cr_deep_back(CRView v, int h_top, int h_stop) {
   for (int h = h_top / 2; h >= h_stop && h >= 1; h /= 2) {
     const int n_odd = (v.p - h + 2 * h - 1) / (2 * h);
     for (int k = 0; k < n_odd; ++k) {
-      deep_back(v, h, h + 2 * h * k);
+      deep_back_pass(v, h, h + 2 * h * k);
       __syncthreads();
     }
   }
@@ -2000,9 +2002,10 @@ __global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CR
   }
 }
 
-// SQLM_CR_DEEP_BACK=1: the deepest back-substitution levels inside the top
-// factor's launch (k_cr_top_back). Measured slower on MI355X (config-4 band
-// solve 0.485 -> 0.592 ms, tools/cr_bench; profiles/r04/cr_ab_r4.log): opt-in only.
+// SQLM_CR_DEEP_BACK=1: the deepest back-substitution levels in one launch
+// after the top (k_cr_deep_back). Folded into the top factor's own launch it
+// measured slower on MI355X (config-4 band solve 0.485 -> 0.592 ms,
+// tools/cr_bench; profiles/r04/cr_ab_r4.log); opt-in until measured.
 static bool deep_back_enabled() {
   static const bool v = std::getenv("SQLM_CR_DEEP_BACK") != nullptr;
   return v;
@@ -2167,13 +2170,17 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
   } else if (top_split()) {  // x_0 = U_0^-1 z_0 (A/B: factor and back substitution as two launches)
     launch_cr_factor(v, 0, 0, 0, 1, false, st);
     hipLaunchKernelGGL(k_cr_back_u<true>, dim3(1), dim3(64 * nt), back_lds, st, v, 0);
-  } else if (!deep_back_enabled()) {  // x_0 = U_0^-1 z_0 by the top factor's workgroup
+  } else {  // x_0 = U_0^-1 z_0 by the top factor's workgroup
     hipLaunchKernelGGL((k_cr_aug<1, false, true>), dim3(1), dim3(aug::kThreads), sizeof(aug::Shared), st, v, 0, 0, 0, 1);
-  } else {  // ... and the deepest back-substitution levels after it
-    int h_stop = h;
-    while (h_stop > 1 && (p - h_stop / 2 + h_stop - 1) / h_stop <= kDeepBackOdd) h_stop /= 2;
-    hipLaunchKernelGGL(k_cr_top_back, dim3(1), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, h_stop);
-    h = h_stop;
+    if (deep_back_enabled()) {  // ... and the deepest back-substitution levels in one more launch
+      int h_stop = h;
+      while (h_stop > 1 && (p - h_stop / 2 + h_stop - 1) / h_stop <= kDeepBackOdd) h_stop /= 2;
+      if (h_stop < h) {
+        const size_t lds = 3 * kCRMaxN * sizeof(double) + aug::kMaxNt * sizeof(int);
+        hipLaunchKernelGGL(k_cr_deep_back, dim3(1), dim3(64 * nt), lds, st, v, h, h_stop);
+      }
+      h = h_stop;
+    }
   }
   for (h /= 2; h >= 1; h /= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
