@@ -1330,6 +1330,21 @@ __device__ __forceinline__ void rcs_put_g(const DevProblem &d, int i, int r, dou
 // sum of src[off[k] + e] over k = k0, k0 + step, ... < k1 in that order, eight loads in flight
 __device__ __forceinline__ double red_sum(const double *src, const int64_t *off, int k0, int k1, int step, int e) {
   double v = 0.0;
+  if (step == 1 && k1 - k0 <= kRedLong) {  // short list: offsets first (see red_sumv)
+    int64_t o[kRedLong];
+#pragma unroll
+    for (int u = 0; u < kRedLong; ++u) o[u] = k0 + u < k1 ? off[k0 + u] : -1;
+#pragma unroll
+    for (int g = 0; g < kRedLong; g += 8) {
+      if (k0 + g >= k1) break;
+      double p8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p8[u] = o[g + u] >= 0 ? src[o[g + u] + e] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += p8[u];
+    }
+    return v;
+  }
   for (int k = k0; k < k1; k += 8 * step) {
     double p8[8];
 #pragma unroll
@@ -1342,10 +1357,36 @@ __device__ __forceinline__ double red_sum(const double *src, const int64_t *off,
 
 // the same sum for the entries e .. e + V - 1 (V = 2 or 4, e a multiple of V):
 // 16-byte loads per contribution (every contribution starts at a multiple of 36 doubles)
+// A short list (<= kRedLong contributions): every offset is loaded first, in
+// one round trip, then the values in groups of eight -- two dependent memory
+// round trips in all instead of two per group (the sum keeps list order).
 template <int V>
 __device__ __forceinline__ void red_sumv(const double *src, const int64_t *off, int k0, int k1, int e, double *v) {
 #pragma unroll
   for (int j = 0; j < V; ++j) v[j] = 0.0;
+  if (k1 - k0 <= kRedLong) {
+    int64_t o[kRedLong];
+#pragma unroll
+    for (int u = 0; u < kRedLong; ++u) o[u] = k0 + u < k1 ? off[k0 + u] : -1;
+#pragma unroll
+    for (int g = 0; g < kRedLong; g += 8) {
+      if (k0 + g >= k1) break;
+      double2 p8[8][V / 2];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < V / 2; ++j)
+          p8[u][j] = o[g + u] >= 0 ? *reinterpret_cast<const double2 *>(src + o[g + u] + e + 2 * j) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int j = 0; j < V / 2; ++j) {
+          v[2 * j] += p8[u][j].x;
+          v[2 * j + 1] += p8[u][j].y;
+        }
+    }
+    return;
+  }
   for (int k = k0; k < k1; k += 8) {
     double2 p8[8][V / 2];
 #pragma unroll
