@@ -138,6 +138,7 @@ struct sqlm_ctx {
   TileBuild tb;
   std::vector<std::vector<int>> scat_base;  // per-thread counting-sort bases (slots)
   std::vector<int> h_kcount, h_span_lo, h_span_hi, h_pt_slot, h_key;
+  std::vector<int> h_efirst, h_elast;  // first / last active edge of every landmark (contiguity test)
   std::vector<uint8_t> h_pose_act, h_pt_act;
   // ---- device memory ----
   std::vector<DevBuf> bufs;
@@ -378,6 +379,14 @@ void par_assign(std::vector<T> &v, const T *src, size_t n) {
   });
 }
 
+// v <- n copies of x on host threads
+template <class T>
+void fill_par(std::vector<T> &v, size_t n, T x) {
+  v.resize(n);
+  const int nth = host_threads((int64_t)n);
+  run_threads(nth, [&](int t) { std::fill(v.begin() + n * t / nth, v.begin() + n * (t + 1) / nth, x); });
+}
+
 void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *obs_camh, int lm_cap, TilePlan &tp,
                  TileBuild &tb) {
   const int64_t nE = lm_begin[nL];
@@ -517,8 +526,9 @@ void pattern_from_tiles(int nP, const TileBuild &tb, std::vector<int> &s_row, st
         if (r.j != r.key) raw[cnt[th][r.key]++] = r.j;
   });
   std::vector<int> len(nP);
-  run_threads(host_threads((int64_t)ptr[nP]), [&](int th) {
-    const int n = host_threads((int64_t)ptr[nP]);
+  // (sorting is heavier per entry than a copy: more threads than a pass would take)
+  run_threads(host_threads(8 * (int64_t)ptr[nP]), [&](int th) {
+    const int n = host_threads(8 * (int64_t)ptr[nP]);
     for (int i = (int)((int64_t)nP * th / n); i < (int)((int64_t)nP * (th + 1) / n); ++i) {
       int *b = raw.data() + ptr[i] + 1, *e = raw.data() + ptr[i + 1];
       std::sort(b, e);
@@ -555,13 +565,28 @@ void build_tiles_finish(int nP, const std::vector<int> &s_row, const std::vector
       }
   });
   sub("keys");
-  // pass 3 (tile order): offsets, camera lists, the reduction lists
+  // pass 3 (tile order): offsets, camera lists, the reduction lists (the
+  // lists concatenated on host threads at per-tile offsets)
   std::vector<Red> red, gred;
+  {
+    std::vector<size_t> roff(nt + 1, 0), goff(nt + 1, 0);
+    for (int t = 0; t < nt; ++t) {
+      roff[t + 1] = roff[t] + out[t].red.size();
+      goff[t + 1] = goff[t] + out[t].cams.size();
+    }
+    red.resize(roff[nt]);
+    gred.resize(goff[nt]);
+    const int nr = host_threads((int64_t)roff[nt]);
+    run_threads(nr, [&](int th) {
+      for (int t = (int)((int64_t)nt * th / nr); t < (int)((int64_t)nt * (th + 1) / nr); ++t) {
+        std::copy(out[t].red.begin(), out[t].red.end(), red.begin() + roff[t]);
+        for (size_t u = 0; u < out[t].cams.size(); ++u) gred[goff[t] + u] = Red{out[t].cams[u], t, (int)u, 0};
+      }
+    });
+  }
   for (int t = 0; t < nt; ++t) {
     const std::vector<int> &cur = out[t].cams;
     const int cp = (int)cur.size();
-    red.insert(red.end(), out[t].red.begin(), out[t].red.end());
-    for (int u = 0; u < cp; ++u) gred.push_back({cur[u], t, u, 0});
     const int ld = (6 * cp + 15) / 16 * 16;
     tp.ld.push_back(ld);
     tp.part_ptr.push_back(tp.part_ptr.back() + 36 * (int64_t)(cp * (cp + 1) / 2));
@@ -609,7 +634,14 @@ void build_tiles_finish(int nP, const std::vector<int> &s_row, const std::vector
   std::vector<int2> red_idx;
   csr(red, s_row[nP], tp.red_ptr, red_idx);
   tp.red_off.resize(red_idx.size());
-  for (size_t k = 0; k < red_idx.size(); ++k) tp.red_off[k] = tp.part_ptr[red_idx[k].x] + 36 * (int64_t)red_idx[k].y;
+  {
+    const int64_t n = (int64_t)red_idx.size();
+    const int nc = host_threads(n);
+    run_threads(nc, [&](int t) {
+      for (int64_t k = n * t / nc; k < n * (t + 1) / nc; ++k)
+        tp.red_off[k] = tp.part_ptr[red_idx[k].x] + 36 * (int64_t)red_idx[k].y;
+    });
+  }
   csr(gred, nP, tp.gred_ptr, tp.gred_idx);
   tp.gred_off.resize(tp.gred_idx.size());
   for (size_t k = 0; k < tp.gred_idx.size(); ++k)
@@ -787,11 +819,14 @@ int prepare(sqlm_ctx *c, int level) {
   };
   std::vector<uint8_t> &pose_act = c->h_pose_act, &pt_act = c->h_pt_act;
   std::vector<int> &kcount = c->h_kcount, &span_lo = c->h_span_lo, &span_hi = c->h_span_hi;
+  std::vector<int> &efirst = c->h_efirst, &elast = c->h_elast;
   pose_act.assign(c->n_pose, 0);
-  pt_act.assign(c->n_pt, 0);
-  kcount.assign(c->n_pt, 0);
-  span_lo.assign(c->n_pt, std::numeric_limits<int>::max());
-  span_hi.assign(c->n_pt, -1);
+  fill_par(pt_act, (size_t)c->n_pt, (uint8_t)0);
+  fill_par(kcount, (size_t)c->n_pt, 0);
+  fill_par(span_lo, (size_t)c->n_pt, std::numeric_limits<int>::max());
+  fill_par(span_hi, (size_t)c->n_pt, -1);
+  fill_par(efirst, (size_t)c->n_pt, std::numeric_limits<int>::max());
+  fill_par(elast, (size_t)c->n_pt, -1);
   int64_t n_ae = 0;
   {  // active set, track lengths and camera spans in one pass on host threads (relaxed atomics)
     const int nth = host_threads(c->n_obs);
@@ -801,13 +836,15 @@ int prepare(sqlm_ctx *c, int level) {
       int64_t n = 0;
       // runs of one landmark (the reference adds a point's edges together,
       // g2oOptimizer.cc:213-281) are folded locally: one set of atomics per run
-      int rl = -1, rk = 0, rlo = 0, rhi = 0;
+      int rl = -1, rk = 0, rlo = 0, rhi = 0, rf = 0, rla = 0;
       auto flush = [&] {
         if (rl < 0) return;
         __atomic_store_n(&pt_act[rl], (uint8_t)1, __ATOMIC_RELAXED);
         __atomic_fetch_add(&kcount[rl], rk, __ATOMIC_RELAXED);
         __atomic_fetch_min(&span_lo[rl], rlo, __ATOMIC_RELAXED);
         __atomic_fetch_max(&span_hi[rl], rhi, __ATOMIC_RELAXED);
+        __atomic_fetch_min(&efirst[rl], rf, __ATOMIC_RELAXED);
+        __atomic_fetch_max(&elast[rl], rla, __ATOMIC_RELAXED);
       };
       for (int64_t e = e0; e < e1; ++e) {
         if (c->obs_level[e] != level) continue;
@@ -818,8 +855,10 @@ int prepare(sqlm_ctx *c, int level) {
           rl = l;
           rk = 0;
           rlo = rhi = pp;
+          rf = (int)e;
         }
         ++rk;
+        rla = (int)e;
         rlo = std::min(rlo, pp);
         rhi = std::max(rhi, pp);
         ++n;
@@ -858,14 +897,30 @@ int prepare(sqlm_ctx *c, int level) {
     const int64_t nb = 7 * (int64_t)c->n_pose + 1;
     std::vector<int> bcnt(nb + 1, 0);
     std::vector<int> &key = c->h_key;
-    key.assign(c->n_pt, -1);
-    for (int l = 0; l < c->n_pt; ++l)
-      if (pt_act[l]) { key[l] = (int)(wl(kcount[l]) * (int64_t)c->n_pose + span_lo[l]); ++bcnt[key[l] + 1]; }
-    for (int64_t b = 0; b < nb; ++b) bcnt[b + 1] += bcnt[b];
-    pts.assign(bcnt[nb], 0);
-    std::vector<int> f(bcnt.begin(), bcnt.end() - 1);
-    for (int l = 0; l < c->n_pt; ++l)
-      if (key[l] >= 0) pts[f[key[l]]++] = l;
+    key.resize(c->n_pt);
+    // the counting sort on host threads: chunk t (ids in order) histograms its
+    // keys, bucket-major / chunk-minor bases keep id order inside a bucket
+    const int nk = host_threads(c->n_pt);
+    std::vector<std::vector<int>> hist(nk);
+    run_threads(nk, [&](int t) {
+      std::vector<int> &h = hist[t];
+      h.assign(nb, 0);
+      for (int l = (int)((int64_t)c->n_pt * t / nk); l < (int)((int64_t)c->n_pt * (t + 1) / nk); ++l) {
+        key[l] = pt_act[l] ? (int)(wl(kcount[l]) * (int64_t)c->n_pose + span_lo[l]) : -1;
+        if (key[l] >= 0) ++h[key[l]];
+      }
+    });
+    for (int64_t b = 0, run = 0; b < nb; ++b) {
+      bcnt[b] = (int)run;
+      for (int t = 0; t < nk; ++t) { const int k = hist[t][b]; hist[t][b] = (int)run; run += k; }
+      bcnt[b + 1] = (int)run;
+    }
+    pts.resize(bcnt[nb]);
+    run_threads(nk, [&](int t) {
+      std::vector<int> &f = hist[t];
+      for (int l = (int)((int64_t)c->n_pt * t / nk); l < (int)((int64_t)c->n_pt * (t + 1) / nk); ++l)
+        if (key[l] >= 0) pts[f[key[l]]++] = l;
+    });
     // buckets hold a few dozen points: a stable insertion sort, buckets on host threads
     const int nth = host_threads(c->n_pt * 8);
     run_threads(nth, [&](int t) {
@@ -889,16 +944,21 @@ int prepare(sqlm_ctx *c, int level) {
   phase("active+sort");
   if (nP + nL == 0) return SQLM_ERR_STATE;  // "0 vertices to optimize"
   std::vector<int> &pt_slot = c->h_pt_slot;
-  pt_slot.assign(c->n_pt, -1);
-  for (int s = 0; s < nL; ++s) pt_slot[pts[s]] = s;
+  fill_par(pt_slot, (size_t)c->n_pt, -1);
+  const int nks = host_threads(nL);
+  run_threads(nks, [&](int t) {
+    for (int s = (int)((int64_t)nL * t / nks); s < (int)((int64_t)nL * (t + 1) / nks); ++s) pt_slot[pts[s]] = s;
+  });
   c->slot_pt = pts;
   c->buckets.clear();
   c->bucket_part_off.clear();
   c->n_lm_parts = 0;
+  // the slots ascend in segment width (the sort's major key): each bucket ends
+  // at the first slot of a wider segment
   for (int s = 0; s < nL;) {
     const int W = seg_width(kcount[pts[s]]);
-    int e = s;
-    while (e < nL && seg_width(kcount[pts[e]]) == W) ++e;
+    const int e = (int)(std::partition_point(pts.begin() + s, pts.end(), [&](int l) { return seg_width(kcount[l]) <= W; }) -
+                        pts.begin());
     Bucket b{W, s, e};
     c->buckets.push_back(b);
     c->bucket_part_off.push_back(c->n_lm_parts);
@@ -906,12 +966,29 @@ int prepare(sqlm_ctx *c, int level) {
     s = e;
   }
   if (c->n_lm_parts > 16384) return SQLM_ERR_UNSUPPORTED;
-  // observations in slot order (edge-id order inside a landmark)
+  // observations in slot order (edge-id order inside a landmark): offsets by a
+  // two-pass prefix over slot chunks
   std::vector<int> lm_begin(nL + 1, 0);
-  for (int s = 0; s < nL; ++s) lm_begin[s + 1] = lm_begin[s] + kcount[pts[s]];
+  {
+    std::vector<int64_t> part(nks + 1, 0);
+    run_threads(nks, [&](int t) {
+      int64_t acc = 0;
+      for (int s = (int)((int64_t)nL * t / nks); s < (int)((int64_t)nL * (t + 1) / nks); ++s) acc += kcount[pts[s]];
+      part[t + 1] = acc;
+    });
+    for (int t = 0; t < nks; ++t) part[t + 1] += part[t];
+    if (part[nks] > (int64_t)std::numeric_limits<int>::max()) return SQLM_ERR_UNSUPPORTED;
+    run_threads(nks, [&](int t) {
+      int acc = (int)part[t];
+      for (int s = (int)((int64_t)nL * t / nks); s < (int)((int64_t)nL * (t + 1) / nks); ++s) {
+        acc += kcount[pts[s]];
+        lm_begin[s + 1] = acc;
+      }
+    });
+  }
   const int64_t nE = lm_begin[nL];
   if (nE > (int64_t)std::numeric_limits<int>::max()) return SQLM_ERR_UNSUPPORTED;
-  c->dev_edge.assign(nE, 0);
+  c->dev_edge.resize(nE);  // every entry is written by the scatter below
   PinVec<int> obs_lm, obs_cam, obs_camh;
   PinVec<double> obs_uv, obs_info, obs_delta, obs_ur;
   PinVec<float> obs_q;  // u v info delta as float32, exact when obs_f32 (below)
@@ -922,14 +999,52 @@ int prepare(sqlm_ctx *c, int level) {
         (e = pinned(c, P_OBSUR, c->has_stereo ? nE : 0, obs_ur)))
       return e;
   }
-  // Stable scatter of the observations into slot order on a few host threads:
-  // chunk t of the edge range counts its edges per slot, the per-(chunk, slot)
-  // bases follow by a prefix over chunks (edge-id order inside a landmark is
-  // kept), then every chunk scatters its edges; the camera CSR likewise.
+  // Stable scatter of the observations into slot order on a few host threads
+  // (edge-id order inside a landmark). When every landmark's active edges are
+  // one contiguous run of edge ids -- g2o's graphs add a point's edges together
+  // (g2oOptimizer.cc:213-281, 868-912) -- an edge's position is its slot's
+  // base plus its offset in the run: one streaming pass. Otherwise chunk t of the edge range
+  // counts its edges per slot, the per-(chunk, slot) bases follow by a prefix
+  // over chunks, then every chunk scatters its edges.
   const int nth = host_threads(c->n_obs);
   auto par = [&](auto &&fn) { run_threads(nth, fn); };
   std::vector<uint8_t> inexact(nth, 0);
-  {
+  auto put = [&](int64_t e, int o, int sl, bool &bad) {
+    c->dev_edge[o] = e;
+    obs_lm[o] = sl;
+    obs_cam[o] = c->obs_pose[e];
+    obs_camh[o] = phidx[c->obs_pose[e]];
+    const double u = c->obs_uv[2 * e], v = c->obs_uv[2 * e + 1], w = c->obs_info[e], dl = c->obs_delta[e];
+    const float fu = (float)u, fv = (float)v, fw = (float)w, fd = (float)dl;
+    obs_q[4 * (size_t)o] = fu;
+    obs_q[4 * (size_t)o + 1] = fv;
+    obs_q[4 * (size_t)o + 2] = fw;
+    obs_q[4 * (size_t)o + 3] = fd;
+    bad |= (double)fu != u || (double)fv != v || (double)fw != w || (double)fd != dl;
+    if (c->has_stereo) obs_ur[o] = c->obs_ur[e];
+  };
+  bool contig = c->n_obs <= (int64_t)std::numeric_limits<int>::max();
+  if (contig) {
+    std::vector<uint8_t> split(nth, 0);
+    par([&](int t) {
+      for (int sl = (int)((int64_t)nL * t / nth); sl < (int)((int64_t)nL * (t + 1) / nth); ++sl) {
+        const int l = pts[sl];
+        if (elast[l] - efirst[l] + 1 != kcount[l]) { split[t] = 1; break; }
+      }
+    });
+    contig = std::find(split.begin(), split.end(), 1) == split.end();
+  }
+  if (contig) {  // edge order (streaming reads): edge e of landmark l goes to its slot's base + (e - first edge)
+    par([&](int t) {
+      bool bad = false;
+      for (int64_t e = c->n_obs * t / nth; e < c->n_obs * (t + 1) / nth; ++e) {
+        if (c->obs_level[e] != level) continue;
+        const int l = c->obs_pt[e], sl = pt_slot[l];
+        put(e, lm_begin[sl] + (int)(e - efirst[l]), sl, bad);
+      }
+      inexact[t] = bad;
+    });
+  } else {
     auto ebeg = [&](int t) { return c->n_obs * t / nth; };
     std::vector<std::vector<int>> &base = c->scat_base;
     if ((int)base.size() < nth) base.resize(nth);
@@ -952,19 +1067,7 @@ int prepare(sqlm_ctx *c, int level) {
       for (int64_t e = ebeg(t); e < ebeg(t + 1); ++e) {
         if (c->obs_level[e] != level) continue;
         const int sl = pt_slot[c->obs_pt[e]];
-        const int o = fill[sl]++;
-        c->dev_edge[o] = e;
-        obs_lm[o] = sl;
-        obs_cam[o] = c->obs_pose[e];
-        obs_camh[o] = phidx[c->obs_pose[e]];
-        const double u = c->obs_uv[2 * e], v = c->obs_uv[2 * e + 1], w = c->obs_info[e], dl = c->obs_delta[e];
-        const float fu = (float)u, fv = (float)v, fw = (float)w, fd = (float)dl;
-        obs_q[4 * (size_t)o] = fu;
-        obs_q[4 * (size_t)o + 1] = fv;
-        obs_q[4 * (size_t)o + 2] = fw;
-        obs_q[4 * (size_t)o + 3] = fd;
-        bad |= (double)fu != u || (double)fv != v || (double)fw != w || (double)fd != dl;
-        if (c->has_stereo) obs_ur[o] = c->obs_ur[e];
+        put(e, fill[sl]++, sl, bad);
       }
       inexact[t] = bad;
     });
@@ -1088,6 +1191,7 @@ int prepare(sqlm_ctx *c, int level) {
   std::vector<int> s_row(nP + 1, 0), s_col;
   if (!sharded) {
     pattern_from_tiles(nP, tb, s_row, s_col);
+    phase("  S rows");
   } else {
     std::vector<std::vector<int>> rows(nP);
     {  // rows are independent: a few host threads, each with its own marks
