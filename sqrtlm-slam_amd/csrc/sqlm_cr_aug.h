@@ -47,15 +47,16 @@
 namespace sqlm {
 namespace aug {
 
-// wave 0: the diagonal chain; wave 1: its pipe wave (the chain's off-chain
-// MFMAs, on another SIMD); waves 4, 8, 12 (wave 0's SIMD) idle; the other 11
-// are column workers. SQLM_AUG_SOLO (A/B builds): wave 0 alone, 12 workers.
+// wave 0: the diagonal chain; waves 1 and 2 (other SIMDs) its off-chain MFMAs:
+// the PQ wave (U_k,k+1 and the next diagonal) and the T wave (T_k); waves 4,
+// 8, 12 (wave 0's SIMD) idle; the other 10 are column workers.
+// SQLM_AUG_SOLO (A/B builds): wave 0 alone, 12 workers.
 #ifdef SQLM_AUG_SOLO
 constexpr bool kPipe = false;
 #else
 constexpr bool kPipe = true;
 #endif
-constexpr int kWaves = 16, kThreads = 64 * kWaves, kMaxNt = kCRMaxN / 16, kWorkers = kPipe ? 11 : 12;
+constexpr int kWaves = 16, kThreads = 64 * kWaves, kMaxNt = kCRMaxN / 16, kWorkers = kPipe ? 10 : 12;
 constexpr int kPairs = kMaxNt * (kMaxNt - 1) / 2;
 enum : int { kNone = 0, kColD = 1, kColI0 = 3, kColEt = 4, kColE = 5, kColG = 6 };
 
@@ -67,14 +68,14 @@ constexpr int kTp = 17;  // padded row stride of the T_k images
 struct Shared {
   double T[kMaxNt][16 * kTp];  // T_k = L_kk^-1 of step k, row-major (the workers read it as an A operand)
   double U[kPairs][256];    // U_kJ (k < J), accumulator layout: element j of lane l at [64 j + l]
-  double Hp[kMaxNt][256];   // column J's tiles (J-1, J) and (J, J) through step J-3, handed to wave 0
+  double Hp[kMaxNt][256];   // column J's tiles (J-1, J) and (J, J): through step J-3 to wave 0 (solo), through step J-2 to the PQ wave
   double Hq[kMaxNt][256];
   int fT[kMaxNt], fU[kPairs], fH[kMaxNt];
   // diagonal wave -> pipe wave: group a's A operand (W) and rank-4 rows (op),
   // one slot per group reused every step (flag value = step + 1); pipe wave ->
   // diagonal wave: the next diagonal tile (flag value = its step)
-  double Ga[4][64], Go[4][64], Dn[256];
-  int fA[4], fO[4], fD;
+  double Ga[2][4][64], Go[2][4][64], Dn[256];  // slots by step parity (two consumer waves)
+  int fA[2][4], fO[2][4], fD;
   double by[kCRMaxN], bx[kCRMaxN], br[16];  // BACK: y, x and one block row's right-hand side
 };
 
@@ -145,10 +146,15 @@ typedef __attribute__((address_space(3))) int lds_int;
 // the data it goes on with is not the factor, and the trial must not use it.
 // -DSQLM_SPIN_FORCE_TIMEOUT (tests only): every wait reports a timeout after
 // it has completed, so the failure path runs on a correct factor.
+// SQLM_SPIN_SLEEP (build, A/B): s_sleep units between polls (0: poll back to back)
+#ifndef SQLM_SPIN_SLEEP
+#define SQLM_SPIN_SLEEP 1
+#endif
 __device__ __forceinline__ bool spin(int *f) {
   lds_int *p = (lds_int *)f;
   int it = 0;
-  for (; __atomic_load_n(p, __ATOMIC_RELAXED) == 0 && it < kSpinLimit; ++it) __builtin_amdgcn_s_sleep(1);
+  for (; __atomic_load_n(p, __ATOMIC_RELAXED) == 0 && it < kSpinLimit; ++it)
+    if (SQLM_SPIN_SLEEP > 0) __builtin_amdgcn_s_sleep(SQLM_SPIN_SLEEP);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 #ifdef SQLM_SPIN_DEBUG
   if (it >= kSpinLimit && (threadIdx.x & 63) == 0)
@@ -446,12 +452,12 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
   const int n = v.n, nt = n >> 4;
   const bool left = MODE == 0, right = MODE != 1 && I + h < v.p, first = sidx == 0;
   bool tmo = false;
-  for (int t = threadIdx.x; t < 2 * kMaxNt + kPairs + 9; t += blockDim.x) {
+  for (int t = threadIdx.x; t < 2 * kMaxNt + kPairs + 17; t += blockDim.x) {
     if (t < kMaxNt) sh.fT[t] = 0;
     else if (t < kMaxNt + kPairs) sh.fU[t - kMaxNt] = 0;
     else if (t < 2 * kMaxNt + kPairs) sh.fH[t - kMaxNt - kPairs] = 0;
-    else if (t < 2 * kMaxNt + kPairs + 4) sh.fA[t - 2 * kMaxNt - kPairs] = 0;
-    else if (t < 2 * kMaxNt + kPairs + 8) sh.fO[t - 2 * kMaxNt - kPairs - 4] = 0;
+    else if (t < 2 * kMaxNt + kPairs + 8) (&sh.fA[0][0])[t - 2 * kMaxNt - kPairs] = 0;
+    else if (t < 2 * kMaxNt + kPairs + 16) (&sh.fO[0][0])[t - 2 * kMaxNt - kPairs - 8] = 0;
     else sh.fD = 0;
   }
   __syncthreads();
@@ -476,30 +482,36 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
     d4 Dg = dense ? load_tile_sym(Dblk, ldd, 0, lane) : load_tile(Dblk, n, 0, 0, lane);
     for (int k = 0; k < nt; ++k) {
       AUG_STAMP(0, k, 0);
-      if (k > 0) {  // diagonal tile k, updated through step k-1 by the pipe wave
+      const int pk = k & 1;
+      if (k > 0) {  // diagonal tile k, updated through step k-1 by the PQ wave
         tmo |= !spin_to(&sh.fD, k);
         Dg = get_tile(sh.Dn, lane);
       }
+      // this step's slots held step k-2's groups: the T wave must be past that step
+      if (k >= 2) tmo |= !spin(&sh.fT[k - 2]);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         const double aop = group_pivot(Dg, a, lane, bad);
-        sh.Ga[a][lane] = aop;
-        raise_flag(&sh.fA[a], lane, k + 1);
-        if (a == 3) break;  // the last group updates nothing past the tile
+        sh.Ga[pk][a][lane] = aop;
+        raise_flag(&sh.fA[pk][a], lane, k + 1);
+        if (a == 3) {  // the last group updates nothing past the tile
+          AUG_STAMP(0, k, 1);
+          break;
+        }
         // finished rows 4a .. 4a+3 = W M4 (element 0); the rank-4 update of the
         // rows and columns past the group
         const d4 Xd = mfma(aop, Dg[a], zero);
         const double op = c >= 4 * a + 4 ? Xd[0] : 0.0;
         Dg = mfma(-op, op, Dg);
-        sh.Go[a][lane] = op;
-        raise_flag(&sh.fO[a], lane, k + 1);
+        sh.Go[pk][a][lane] = op;
+        raise_flag(&sh.fO[pk][a], lane, k + 1);
       }
     }
     if (bad && lane == 0) v.flags[0] = 0;
     if (tmo) cr_fail(v, lane);
     return;
   }
-  if (kPipe && wave == 1) {  // ---- the pipe wave: T_k, U_k,k+1 and the next diagonal
+  if (kPipe && wave == 1) {  // ---- the PQ wave: U_k,k+1 and the next diagonal
     __builtin_amdgcn_s_setprio(3);
     double *Lb = blk(v.L, I, n);
     const d4 zero = {0.0, 0.0, 0.0, 0.0};
@@ -508,35 +520,65 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
       P = load_tile_t(Dblk, ldd, 0, 16, lane);  // U tile (0, 1) from the lower block (1, 0)
       Q = dense ? load_tile_sym(Dblk, ldd, 16, lane) : load_tile(Dblk, n, 16, 16, lane);
     }
-    for (int k = 0; k < nt; ++k) {
-      d4 Tt = identity_tile(lane);
-      const bool pq = k + 1 < nt;
+    for (int k = 0; k + 1 < nt; ++k) {
+      const int pk = k & 1;
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        tmo |= !spin_to(&sh.fA[a], k + 1);
-        const double aop = sh.Ga[a][lane];
-        const d4 Xt = mfma(aop, Tt[a], zero);
-        d4 Xp = zero;
-        if (pq) {
-          Xp = mfma(aop, P[a], zero);
-          Q = mfma(-Xp[0], Xp[0], Q);
-        }
+        tmo |= !spin_to(&sh.fA[pk][a], k + 1);
+        const double aop = sh.Ga[pk][a][lane];
+        const d4 Xp = mfma(aop, P[a], zero);
+        Q = mfma(-Xp[0], Xp[0], Q);
         double op = 0.0;  // the last group's rows update nothing (the diagonal wave's op is 0 there)
         if (a < 3) {
-          tmo |= !spin_to(&sh.fO[a], k + 1);
-          op = sh.Go[a][lane];
+          tmo |= !spin_to(&sh.fO[pk][a], k + 1);
+          op = sh.Go[pk][a][lane];
+        }
+        P[a] = Xp[0];
+        P = mfma(-op, Xp[0], P);
+      }
+      AUG_STAMP(1, k, 0);
+      put_tile(sh.Dn, Q, lane);  // the next diagonal first: it is the chain
+      raise_flag(&sh.fD, lane, k + 1);
+      // U_k,k+1 feeds the trailing updates of row k+1
+      put_tile(sh.U[pair_id(k, k + 1)], P, lane);
+      raise_flag(&sh.fU[pair_id(k, k + 1)], lane);
+      if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * (k + 1), P, lane);
+      if (k + 2 < nt) {  // the next step's P = (k+1, k+2) and Q = (k+2, k+2) through step k
+        tmo |= !spin(&sh.fU[pair_id(k, k + 2)]);  // U_k,k+2 from column k+2's worker
+        const d4 X = get_tile(sh.U[pair_id(k, k + 2)], lane);
+        tmo |= !spin(&sh.fH[k + 2]);  // its Q, and its P through step k-1
+        d4 P2 = get_tile(sh.Hp[k + 2], lane);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) P2 = mfma(-P[s4], X[s4], P2);
+        P = P2;
+        Q = get_tile(sh.Hq[k + 2], lane);
+      }
+      AUG_STAMP(1, k, 1);
+    }
+    if (tmo) cr_fail(v, lane);
+    return;
+  }
+  if (kPipe && wave == 2) {  // ---- the T wave: T_k = L_kk^-1 (the same groups on the identity)
+    __builtin_amdgcn_s_setprio(3);
+    double *Lb = blk(v.L, I, n);
+    const d4 zero = {0.0, 0.0, 0.0, 0.0};
+    for (int k = 0; k < nt; ++k) {
+      const int pk = k & 1;
+      d4 Tt = identity_tile(lane);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        tmo |= !spin_to(&sh.fA[pk][a], k + 1);
+        const double aop = sh.Ga[pk][a][lane];
+        const d4 Xt = mfma(aop, Tt[a], zero);
+        double op = 0.0;
+        if (a < 3) {
+          tmo |= !spin_to(&sh.fO[pk][a], k + 1);
+          op = sh.Go[pk][a][lane];
         }
         Tt[a] = Xt[0];
         Tt = mfma(-op, Xt[0], Tt);
-        if (pq) {
-          P[a] = Xp[0];
-          P = mfma(-op, Xp[0], P);
-        }
       }
-      if (pq) {  // the next diagonal first: it is the chain
-        put_tile(sh.Dn, Q, lane);
-        raise_flag(&sh.fD, lane, k + 1);
-      }
+      AUG_STAMP(2, k, 0);
       {  // T_k for the workers (row-major) and, U/T layout, for the back substitution
         const int k4 = lane >> 4, c = lane & 15;
 #pragma unroll
@@ -545,23 +587,6 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
         if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * k, Tt, lane);
       }
       AUG_PROF(2 + k);
-      if (pq) {  // U_k,k+1 feeds the trailing updates of row k+1
-        put_tile(sh.U[pair_id(k, k + 1)], P, lane);
-        raise_flag(&sh.fU[pair_id(k, k + 1)], lane);
-        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * (k + 1), P, lane);
-      }
-      if (k + 2 < nt) {  // the next step's P = (k+1, k+2) and Q = (k+2, k+2) through step k
-        tmo |= !spin(&sh.fH[k + 2]);
-        d4 P2 = get_tile(sh.Hp[k + 2], lane), Q2 = get_tile(sh.Hq[k + 2], lane);
-        tmo |= !spin(&sh.fU[pair_id(k, k + 2)]);
-        const d4 X = get_tile(sh.U[pair_id(k, k + 2)], lane);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) Q2 = mfma(-X[s4], X[s4], Q2);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) P2 = mfma(-P[s4], X[s4], P2);
-        P = P2;
-        Q = Q2;
-      }
     }
     if (tmo) cr_fail(v, lane);
     return;
@@ -620,7 +645,7 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
     return;
   }
   if ((wave & 3) == 0) return;  // the diagonal wave's SIMD partners stay idle
-  const int q = wave - (wave >> 2) - (kPipe ? 2 : 1);
+  const int q = wave - (wave >> 2) - (kPipe ? 3 : 1);
   int type, J;
   column_of(q, nt, LINV, left, right, split, sidx, type, J);
   if (type == kNone) return;
@@ -662,11 +687,14 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
         for (int s = 0; s < 4; ++s) t[r] = mfma(-U[64 * s + lane], t[k - 1][s], t[r]);
       }
     }
-    if (type == kColD && k == J - 2 && k + 2 < kMaxNt) {  // rows J-1, J through step J-3: to wave 0
+    if (!kPipe && type == kColD && k == J - 2 && k + 2 < kMaxNt) {  // rows J-1, J through step J-3: to wave 0
       put_tile(sh.Hp[k + 2], t[k + 1], lane);
       put_tile(sh.Hq[k + 2], t[k + 2], lane);
       raise_flag(&sh.fH[k + 2], lane);
     }
+    // the column that hands the next P / Q over is the chain: its MFMAs go first
+    // on the SIMD it shares with other workers
+    if (kPipe && type == kColD && k == J - 2) __builtin_amdgcn_s_setprio(2);
     AUG_STAMP(wave, k, 0);
     // row k: U_kJ (D column, k <= J-2), identity column J+1 (LINV, k > J), T, I0, E, g
     const bool dtile = type == kColD && k <= J - 2;
@@ -677,6 +705,19 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
         put_tile(sh.U[pair_id(k, J)], t[k], lane);
         raise_flag(&sh.fU[pair_id(k, J)], lane);
       }
+    }
+    if (kPipe && type == kColD && k == J - 2 && k + 2 < kMaxNt) {
+      // the PQ wave's next Q = tile (J, J) with step J-2's piece (the MFMAs
+      // wave 0 applied in the one-wave layout, same operands and order), and
+      // tile (J-1, J) through step J-3 (the PQ wave applies its step J-2 piece
+      // with U_J-2,J-1, which it holds)
+      d4 Q2 = t[k + 2];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) Q2 = mfma(-t[k][s4], t[k][s4], Q2);
+      put_tile(sh.Hp[k + 2], t[k + 1], lane);
+      put_tile(sh.Hq[k + 2], Q2, lane);
+      raise_flag(&sh.fH[k + 2], lane);
+      __builtin_amdgcn_s_setprio(0);
     }
     AUG_STAMP(wave, k, 1);
     // trailing of step k, row k+1 (the next step's row)
