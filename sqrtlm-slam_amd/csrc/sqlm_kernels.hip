@@ -1686,7 +1686,11 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool
 // forms its window's trial poses and dx itself (the same trial_pose code, so
 // the same bits) instead of reading them -- one launch less per trial.
 template <int W, bool ST, bool SPEC, bool FUSE = false>
-__global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : 4) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
+// waves per SIMD the mono variants are compiled for (A/B: -DSQLM_UPD_OCC_MONO=3)
+#ifndef SQLM_UPD_OCC_MONO
+#define SQLM_UPD_OCC_MONO 4
+#endif
+__global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
                                                          double lambda, int part_off, const int2 *rng, int nlm_blocks) {
   constexpr bool fuse_pose = FUSE;
   __shared__ double red[4];
