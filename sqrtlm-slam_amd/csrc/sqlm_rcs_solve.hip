@@ -1344,12 +1344,25 @@ __device__ __forceinline__ void trsm_strip(const CRView &v, int h, int I, int s)
     if (r < nt)
       t[r] = et ? aug::load_tile_t(blk(v.E, I - h, n), n, 16 * r, 16 * J, lane)
                 : aug::load_tile(blk(v.E, I, n), n, 16 * r, 16 * J, lane);
+  // step k's operands (T_k and the U_kr row) are loaded during step k-1: the
+  // strip's chain waits on one memory round trip in all, not one per step
+  // (same MFMAs in the same order)
+  double ta[4];
+  d4 u[aug::kMaxNt];
+  auto load_step = [&](int k, double (&a)[4], d4 (&uu)[aug::kMaxNt]) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a[m] = Lb[(size_t)(16 * k + i16) * n + 16 * k + 4 * m + b];  // T_k[i][4m+b]
+#pragma unroll
+    for (int r = 1; r < aug::kMaxNt; ++r)
+      if (r > k && r < nt) uu[r] = aug::load_tile(Lb, n, 16 * k, 16 * r, lane);  // U_kr
+  };
+  load_step(0, ta, u);
 #pragma unroll
   for (int k = 0; k < aug::kMaxNt; ++k) {
     if (k >= nt) break;
-    double ta[4];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) ta[m] = Lb[(size_t)(16 * k + i16) * n + 16 * k + 4 * m + b];  // T_k[i][4m+b]
+    double ta_n[4];
+    d4 u_n[aug::kMaxNt];
+    if (k + 1 < nt) load_step(k + 1, ta_n, u_n);
     d4 x = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int m = 0; m < 4; ++m) x = aug::mfma(ta[m], t[k][m], x);
@@ -1357,10 +1370,15 @@ __device__ __forceinline__ void trsm_strip(const CRView &v, int h, int I, int s)
 #pragma unroll
     for (int r = k + 1; r < aug::kMaxNt; ++r)
       if (r < nt) {
-        const d4 u = aug::load_tile(Lb, n, 16 * k, 16 * r, lane);  // U_kr
 #pragma unroll
-        for (int m = 0; m < 4; ++m) t[r] = aug::mfma(-u[m], t[k][m], t[r]);
+        for (int m = 0; m < 4; ++m) t[r] = aug::mfma(-u[r][m], t[k][m], t[r]);
       }
+    if (k + 1 < nt) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) ta[m] = ta_n[m];
+#pragma unroll
+      for (int r = 1; r < aug::kMaxNt; ++r) u[r] = u_n[r];
+    }
   }
   double *out = blk(et ? v.A : v.C, I, n);
 #pragma unroll
