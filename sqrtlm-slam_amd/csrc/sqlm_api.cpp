@@ -2187,7 +2187,19 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   for (auto &e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   for (auto &pr : c->ev_cam)
     for (auto &e : pr) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
-  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+  // The side stream (the speculative camera pass of large problems, beside the
+  // next trial's RCS tiles) at the lowest priority: the tiles keep the CUs and
+  // the pass fills their tails (config 4 727.7-728.7 -> 729.6-734.6 it/s,
+  // interleaved, profiles/r04/ab_side_prio.log). SQLM_SIDE_PRIO=normal / high: A/B.
+  auto side_stream = [](hipStream_t *s) {
+    const char *pr = std::getenv("SQLM_SIDE_PRIO");
+    int least = 0, greatest = 0;
+    if (pr && std::strcmp(pr, "normal") == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+      return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr && std::strcmp(pr, "high") == 0 ? greatest : least);
+  };
+  if (side_stream(&c->side) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_spec_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
