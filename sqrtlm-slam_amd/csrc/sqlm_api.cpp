@@ -2199,13 +2199,21 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
       return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
     return hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr && std::strcmp(pr, "high") == 0 ? greatest : least);
   };
+  // SQLM_TILE_PRIO=ab (A/B): priorities of the two extra RCS-tile class streams,
+  // each l(owest), n(ormal) or h(ighest); default normal
+  auto tile_stream = [](hipStream_t *s, int k) {
+    const char *pr = std::getenv("SQLM_TILE_PRIO");
+    int least = 0, greatest = 0;
+    if (!pr || (int)std::strlen(pr) <= k || pr[k] == 'n' || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
+      return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr[k] == 'h' ? greatest : least);
+  };
   if (side_stream(&c->side) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_spec_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_spec_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->tiles.s[0], hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->tiles.s[1], hipStreamNonBlocking) != hipSuccess ||
+      tile_stream(&c->tiles.s[0], 0) != hipSuccess || tile_stream(&c->tiles.s[1], 1) != hipSuccess ||
       hipEventCreateWithFlags(&c->tiles.fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->tiles.join[0], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->tiles.join[1], hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess) {
