@@ -178,10 +178,11 @@ def host_cpu() -> dict:
     return {"cpu_model": model, "nproc": usable, "machine_cpus": os.cpu_count()}
 
 
-def cpu_baseline(prob, name: str, omp: bool = False, gba_iters: int = 8, min_s: float = 10.0):
+def cpu_baseline(prob, name: str, omp: bool = False, gba_iters: int = 10, min_s: float = 10.0):
     """The oracle (g2o-semantics port) on a bounded sample of the same
-    workload: a fixed number of LM iterations of the full config-4 problem, or
-    repeated 10-iteration solves of config 2 until >= 10 s. Only the optimize()
+    workload: the whole optimize(10) of the full config-4 problem (the
+    reference's GlobalBundleAdjustemnt call, ~17 s on one core), or repeated
+    10-iteration solves of config 2 until >= 10 s. Only the optimize()
     calls are timed. Single thread by default, matching the reference build
     (G2O_USE_OPENMP=OFF, Thirdparty/g2o/build/CMakeCache.txt:175); omp=True is
     the labelled all-cores variant (g2o's OpenMP loops on OMP_NUM_THREADS
@@ -483,7 +484,7 @@ def bench_orb(args, world):
         dist.destroy_process_group()
 
 
-def run_ba(args, world, rank, local_rank, dist, config, cpu_iters=8, cpu_min_s=10.0):
+def run_ba(args, world, rank, local_rank, dist, config, cpu_iters=10, cpu_min_s=10.0):
     """One BA workload (config 4, the loop-closed config 4, or config 2) on this
     rank's context; returns the bench dict on rank 0 (None elsewhere)."""
     from sqrtlm.optimizer import Context, comm_unique_id
@@ -626,6 +627,50 @@ def summary(out) -> dict:
     return s
 
 
+def free_port() -> int:
+    """A TCP port on 127.0.0.1 nothing listens on right now (rendezvous of the
+    self-launched ranks)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, child_argv: list, timeout_s: float = 3000.0) -> int:
+    """Start n copies of child_argv as ranks 0..n-1 of one job on this node
+    (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR /
+    MASTER_PORT, as torch.distributed.run sets them) and wait for all of them.
+    The parent touches no GPU: every rank is a fresh process. The first rank
+    that fails ends the others (the exact processes started here); returns
+    the worst exit status (0 when every rank succeeded)."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(child_argv, env=env))
+    t0, rc = time.time(), 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:  # one rank failed: the collective job cannot finish
+                    q.terminate()
+        if live and time.time() - t0 > timeout_s:
+            for q in live:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -640,7 +685,18 @@ def main():
                     help="host = exchange through gloo on the host, all ranks on GPU 0 (1-GPU rehearsal of N>1)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        print(f"bench.py: --gpus {args.gpus} must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start the N ranks here (before anything touches a GPU in
+        # this process) and exit with their status
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     if args.config == "eg":
         return bench_eg(args, world)
     if args.config == "orb":

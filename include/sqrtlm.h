@@ -173,12 +173,8 @@ int sqlm_get_rcs_layout(sqlm_ctx *ctx, int out[8]);
  * reference counterpart): out[0] = 1 if the observation inputs (u, v,
  * invSigma2, Huber delta) were all float32 values and travelled as float4,
  * 0 if they took the double arrays; out[1] = reduced-camera solve: 0 none,
- * 1 cyclic reduction as per-level launches, 2 cyclic reduction as one
- * persistent launch (k_cr_persist), 3 band + border, 4 dense Cholesky,
- * 5 sequential block-tridiagonal factorization in one launch (k_cr_seq, a
- * band of at most 5 superblocks; opt-in, SQLM_CR_SEQ=1);
- * out[2] = tasks of the persistent solve, out[3] = its workgroups;
- * out[4..7] = 0 (reserved). */
+ * 1 cyclic reduction (per-level launches), 3 band + border, 4 dense
+ * Cholesky (2 and 5 retired); out[2..7] = 0 (reserved). */
 int sqlm_get_exec_info(sqlm_ctx *ctx, int out[8]);
 
 /* Converter::toSE3Quat / toCvMat(SE3Quat) (src/utils/Converter.cc:55-79,98-109):

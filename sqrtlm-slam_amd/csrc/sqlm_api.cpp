@@ -123,7 +123,6 @@ struct sqlm_ctx {
   int max_row_blocks = 0;
   int n_active_edges = 0;
   CRPlan cr;
-  CRPersist crp;                     // task graph of the persistent band solve (k_cr_persist)
   int n_cu = 0;
   std::vector<int> cam_pos;          // hidx -> band position or -(1 + border index)
   bool use_tiles = false;
@@ -146,13 +145,9 @@ struct sqlm_ctx {
   double *h_scalars = nullptr;  // pinned
   // the trial scalars' mailbox (mapped, coherent page-locked memory written by
   // k_reduce): the host polls its sequence number instead of a copy + stream
-  // synchronize; SQLM_NO_MBOX=1 (A/B), timing runs and sharded runs copy
+  // synchronize; timing runs and sharded runs copy
   double *mbox = nullptr, *mbox_dev = nullptr;
   unsigned long long mbox_seq = 0;
-  // device-side LM loop: the control state on the device, its page-locked
-  // host image, and a mapped word the host mirrors the caller's stop flag into
-  LMCtl *ctl_dev = nullptr, *ctl_host = nullptr;
-  int *stop_map = nullptr, *stop_map_dev = nullptr;
   // SQLM_HOST_TRACE=1: host-side time points of every trial (diagnostic)
   bool htrace = false;
   std::chrono::steady_clock::time_point ht_prev{};
@@ -1182,9 +1177,8 @@ int prepare(sqlm_ctx *c, int level) {
   // landmarks per tile: up to kTileMaxLm, fewer on small problems so that the
   // tiles still cover every CU twice (a local-BA window of 5k landmarks would
   // otherwise run ~40 long tiles on 256 CUs)
-  // (SQLM_TILE_LMDIV=k: nL / k instead of nL / 512, A/B only)
-  static const int lm_div = std::getenv("SQLM_TILE_LMDIV") ? std::max(1, std::atoi(std::getenv("SQLM_TILE_LMDIV"))) : 512;
-  const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / lm_div + 3) & ~3));
+  // (nL / 160, / 80, / 40 measured slower, profiles/r03/ab_lba_tile_lmcap.log)
+  const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
   TileBuild &tb = c->tb;
   build_tiles(nP, nL, lm_begin, obs_camh.data(), lm_cap, tp, tb);
   phase("tiles");
@@ -1428,10 +1422,9 @@ int prepare(sqlm_ctx *c, int level) {
     c->no_pose_fuse = getenv("SQLM_NO_POSE_FUSE") != nullptr;
     c->spec = c->use_tiles && d.obs_P == nullptr && !no_spec;
     // the side stream's fork / join (two event records, two waits: ~20 us of
-    // host API time per trial) pays only when the pass is long enough to hide;
-    // SQLM_CAM_INLINE=0/1 overrides (A/B)
-    const char *ci = std::getenv("SQLM_CAM_INLINE");
-    c->cam_inline = ci ? std::atoi(ci) != 0 : d.nE < (1 << 18);
+    // host API time per trial) pays only when the pass is long enough to hide
+    // (profiles/r03/ab_lba_cam_inline.log)
+    c->cam_inline = d.nE < (1 << 18);
     if (sharded) c->cam_inline = false;
   }
   c->lin_valid = false;
@@ -1506,8 +1499,6 @@ int prepare(sqlm_ctx *c, int level) {
   AL(B_MAXD, 1, d.maxdiag);
   AL(B_FLAGS, 4, d.flags);
   HIP_OK(hipMemsetAsync(d.flags, 0, 4 * sizeof(int), c->stream));  // flags[1]: sticky device error of the solves
-  if (c->cr.enabled && !c->cr.R && cr_persist_enabled())
-    if (cr_persist_plan(c->crp, c->cr.p, c->cr.n, c->n_cu)) return SQLM_ERR_HIP;
   d.hdiag = nullptr;
   d.xstage = nullptr;
   if (c->comm.enabled()) {
@@ -1734,8 +1725,7 @@ int spec_camera_pass(sqlm_ctx *c, hipStream_t st) {
 // behind k_reduce (it runs while the host waits for the scalars and decides)
 int reduce_and_fetch(sqlm_ctx *c, TrialOut &o, bool cam_after = false) {
   DevProblem &d = c->d;
-  static const bool no_mbox = std::getenv("SQLM_NO_MBOX") != nullptr;
-  const bool mb = c->mbox && !no_mbox && !c->timing && !c->comm.enabled();
+  const bool mb = c->mbox && !c->timing && !c->comm.enabled();
   const unsigned long long seq = mb ? ++c->mbox_seq : 0;
   launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream,
                 mb ? c->mbox_dev : nullptr, seq);
@@ -1826,7 +1816,7 @@ int trial_launch(sqlm_ctx *c, double lambda, bool &cam_after) {
   // unsharded CR: the pose update reads dx off the CR solution (no gather launch)
   const bool pose_from_cr = !sharded && c->cr.enabled;
   if (root) {
-    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream, !pose_from_cr, c->cr.R ? nullptr : &c->crp)
+    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream, !pose_from_cr)
                       : launch_dense_solve(d, c->stream);
     if (s) return s == -2 ? SQLM_ERR_HIP : SQLM_ERR_UNSUPPORTED;
   }
@@ -1919,11 +1909,12 @@ void flush_cam_timers(sqlm_ctx *c) {
 }
 
 // Host loop: every trial's scalars come back before the next trial is
-// enqueued, and the host applies lm_decide. The default: the device-side loop
-// (lm_device, SQLM_DLM=1) measured slower on MI355X -- every per-trial kernel
-// then starts with a dependent load of the control block, which costs more
-// than the host turnaround it hides (config 4 703 -> 649-675 it/s, config 2
-// 5.58-5.61k -> 5.40k it/s; profiles/r04/ab_dlm_fuse_r4.log).
+// enqueued, and the host applies lm_decide. (A device-side loop -- k_reduce
+// deciding, trials enqueued two ahead -- measured slower on MI355X: every
+// per-trial kernel then starts with a dependent load of the control block,
+// which costs more than the host turnaround it hides, config 4 703 -> 649-675
+// it/s, config 2 5.58-5.61k -> 5.40k it/s, profiles/r04/ab_dlm_fuse_r4.log;
+// removed in round 5.)
 int lm_host(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
   while (!L.done) {
     if (L.qmax == 0 && L.its > 0) {  // the next iteration (sparse_optimizer.cpp:376-414)
@@ -1941,73 +1932,6 @@ int lm_host(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
   return SQLM_OK;
 }
 
-// Device loop: k_reduce applies lm_decide to each trial on the device and the
-// trial kernels take lambda, the state parity and the done flag from
-// DevProblem::ctl, so the host enqueues trial t+1 while trial t runs (no
-// host round trip between trials: the ~25 us turnaround of a local-BA trial).
-// At most two trials are outstanding; the one enqueued past the end returns
-// from every kernel at once. The caller's stop flag is mirrored into a mapped
-// word the decision reads.
-bool dlm_ok(const sqlm_ctx *c) {
-  const bool on = std::getenv("SQLM_DLM") != nullptr;  // read per run: tests switch it
-  return on && c->ctl_dev && c->ctl_host && c->mbox && c->stop_map_dev && c->spec && c->use_tiles && !c->timing && !c->htrace &&
-         !c->comm.enabled();
-}
-
-int lm_device(sqlm_ctx *c, LMCtl &L, const volatile uint8_t *stop) {
-  constexpr int kAhead = 2;
-  DevProblem &d = c->d;
-  *c->stop_map = stopped(stop) ? 1 : 0;
-  L.stop_src = c->stop_map_dev;
-  L.par = L.par_trial = 0;
-  HIP_OK(hipMemcpyAsync(c->ctl_dev, &L, sizeof(LMCtl), hipMemcpyHostToDevice, c->stream));
-  d.ctl = c->ctl_dev;
-  const long long max_trials = 10LL * L.iterations;
-  const unsigned long long *slot = reinterpret_cast<const unsigned long long *>(c->mbox + kMboxSeq);
-  long long enq = 0, obs = 0;
-  unsigned long long last_seq = 0;
-  int s = SQLM_OK;
-  bool dev_err = false;
-  while (s == SQLM_OK) {
-    while (enq < max_trials && enq - obs < kAhead) {
-      bool cam_after = false;
-      if ((s = trial_launch(c, L.lambda, cam_after))) break;
-      last_seq = ++c->mbox_seq;
-      launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream,
-                    c->mbox_dev, last_seq);
-      if (cam_after && (s = spec_camera_pass(c, c->stream))) break;
-      ++enq;
-    }
-    if (s || obs == enq) break;
-    // the mailbox of trial `obs` (or of a later one: the done flag is sticky)
-    const unsigned long long want = last_seq - (unsigned long long)(enq - obs - 1);
-    Timer t;
-    for (unsigned it = 1; __atomic_load_n(slot, __ATOMIC_ACQUIRE) < want; ++it) {
-      if ((it & 1023) == 0) {
-        const hipError_t q = hipStreamQuery(c->stream);
-        if (q == hipSuccess && __atomic_load_n(slot, __ATOMIC_ACQUIRE) < want) { s = SQLM_ERR_HIP; break; }
-        if ((q != hipSuccess && q != hipErrorNotReady) || t.ms() > 60000.0) { s = SQLM_ERR_HIP; break; }
-        *c->stop_map = stopped(stop) ? 1 : 0;
-      }
-      __builtin_ia32_pause();
-    }
-    if (s) break;
-    obs = enq - (long long)(last_seq - __atomic_load_n(slot, __ATOMIC_ACQUIRE));
-    *c->stop_map = stopped(stop) ? 1 : 0;
-    if (c->mbox[kDevErr] != 0.0) dev_err = true;
-    if (dev_err || c->mbox[kLmDone] != 0.0) break;
-  }
-  d.ctl = nullptr;
-  // the state the device ended in (traces, parity), after every enqueued trial
-  HIP_OK(hipMemcpyAsync(&L, c->ctl_dev, sizeof(LMCtl), hipMemcpyDeviceToHost, c->stream));
-  HIP_OK(hipStreamSynchronize(c->stream));
-  if (s) return s;
-  if (dev_err || c->mbox[kDevErr] != 0.0) return SQLM_ERR_HIP;
-  if (L.par & 1) swap_state(c);  // the host's view of the buffers follows the device's parity
-  c->kernel_ms_n += L.its;
-  return SQLM_OK;
-}
-
 // The Levenberg–Marquardt loop of g2o (levenberg.cpp:61-164 inside
 // sparse_optimizer.cpp:376-414). `bench` keeps iterating after Terminate so a
 // fixed number of iterations can be timed.
@@ -2019,8 +1943,7 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
   st->n_active_edges = c->n_active_edges;
   c->lin_valid = false;  // iteration 0 linearizes in full (lambda_0 needs max diag H)
   Timer tt;
-  static thread_local LMCtl local_ctl;  // (no page-locked image: host loop only)
-  LMCtl &L = c->ctl_host ? *c->ctl_host : local_ctl;
+  LMCtl L;
   std::memset(&L, 0, sizeof(LMCtl));
   L.iterations = iterations;
   L.bench = bench ? 1 : 0;
@@ -2040,7 +1963,7 @@ int run_lm(sqlm_ctx *c, int iterations, double user_lambda, const volatile uint8
     L.ni = 2;
     st->ms_linearize += tl.ms();
     Timer tr;
-    s = dlm_ok(c) ? lm_device(c, L, stop) : lm_host(c, L, stop);
+    s = lm_host(c, L, stop);
     if (s) return s;
     st->ms_trials += tr.ms();
   }
@@ -2175,13 +2098,6 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   } else {
     c->mbox = nullptr;
   }
-  if (hipMalloc((void **)&c->ctl_dev, sizeof(LMCtl)) != hipSuccess ||
-      hipHostMalloc((void **)&c->ctl_host, sizeof(LMCtl)) != hipSuccess)
-    c->ctl_dev = nullptr;  // no device loop: the host decides every trial
-  if (hipHostMalloc((void **)&c->stop_map, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
-    *c->stop_map = 0;
-    if (hipHostGetDevicePointer((void **)&c->stop_map_dev, c->stop_map, 0) != hipSuccess) c->stop_map_dev = nullptr;
-  }
   // timing-only events: no system-scope fence, which would flush caches and
   // leave a ~10 us bubble between the kernels they separate
   for (auto &e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
@@ -2190,24 +2106,16 @@ int sqlm_ctx_create(int device_id, sqlm_ctx **out) {
   // The side stream (the speculative camera pass of large problems, beside the
   // next trial's RCS tiles) at the lowest priority: the tiles keep the CUs and
   // the pass fills their tails (config 4 727.7-728.7 -> 729.6-734.6 it/s,
-  // interleaved, profiles/r04/ab_side_prio.log). SQLM_SIDE_PRIO=normal / high: A/B.
+  // interleaved, profiles/r04/ab_side_prio.log).
   auto side_stream = [](hipStream_t *s) {
-    const char *pr = std::getenv("SQLM_SIDE_PRIO");
     int least = 0, greatest = 0;
-    if (pr && std::strcmp(pr, "normal") == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
     if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
       return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr && std::strcmp(pr, "high") == 0 ? greatest : least);
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
   };
-  // SQLM_TILE_PRIO=ab (A/B): priorities of the two extra RCS-tile class streams,
-  // each l(owest), n(ormal) or h(ighest); default normal
-  auto tile_stream = [](hipStream_t *s, int k) {
-    const char *pr = std::getenv("SQLM_TILE_PRIO");
-    int least = 0, greatest = 0;
-    if (!pr || (int)std::strlen(pr) <= k || pr[k] == 'n' || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess)
-      return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, pr[k] == 'h' ? greatest : least);
-  };
+  // the two extra RCS-tile class streams at normal priority (lowest / highest
+  // measured within noise, profiles/r04/ab_tile_prio.log)
+  auto tile_stream = [](hipStream_t *s, int) { return hipStreamCreateWithFlags(s, hipStreamNonBlocking); };
   if (side_stream(&c->side) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess ||
@@ -2231,7 +2139,6 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   comm_destroy(c->comm);
   if (c->eg) eg_destroy(c->eg);
   if (c->orb) orb_destroy(c->orb);
-  cr_persist_free(c->crp);
   for (auto &b : c->bufs)
     if (b.p) (void)hipFree(b.p);
   for (auto &b : c->pins)
@@ -2240,9 +2147,6 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
     if (e) (void)hipEventDestroy(e);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
   if (c->mbox) (void)hipHostFree(c->mbox);
-  if (c->ctl_dev) (void)hipFree(c->ctl_dev);
-  if (c->ctl_host) (void)hipHostFree(c->ctl_host);
-  if (c->stop_map) (void)hipHostFree(c->stop_map);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   if (c->ev_join) (void)hipEventDestroy(c->ev_join);
   if (c->ev_spec_fork) (void)hipEventDestroy(c->ev_spec_fork);
@@ -2497,13 +2401,9 @@ int sqlm_get_exec_info(sqlm_ctx *c, int out[8]) {
   if (!c || !out) return SQLM_ERR_INVALID_ARG;
   if (!c->has_problem || !c->prepared) return SQLM_ERR_STATE;
   const CRPlan &pl = c->cr;
-  const bool persist = pl.enabled && !pl.R && cr_persist_enabled() && c->crp.p == pl.p && c->crp.n == pl.n;
   for (int k = 0; k < 8; ++k) out[k] = 0;
   out[0] = c->d.obs_f32 ? 1 : 0;
-  const bool seq = pl.enabled && !pl.R && !persist && cr_seq_enabled() && cr_seq_fits(pl.p, pl.n);
-  out[1] = c->d.nP == 0 ? 0 : !pl.enabled ? 4 : pl.R ? 3 : persist ? 2 : seq ? 5 : 1;
-  out[2] = persist ? c->crp.ntasks : 0;
-  out[3] = persist ? c->crp.G : 0;
+  out[1] = c->d.nP == 0 ? 0 : !pl.enabled ? 4 : pl.R ? 3 : 1;
   return SQLM_OK;
 }
 

@@ -317,11 +317,10 @@ __device__ __forceinline__ d4 load_tile_sym(const double *P, int n, int r0, int 
   for (int j = 0; j < 4; ++j) t[j] = k4 + 4 * j >= c ? lo[j] : up[j];
   return t;
 }
-template <bool WT = false>
 __device__ __forceinline__ void store_tile(double *P, int n, int r0, int c0, const d4 &t, int lane) {
   const int k4 = lane >> 4, c = lane & 15;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) st_d<WT>(P + (size_t)(r0 + k4 + 4 * j) * n + c0 + c, t[j]);
+  for (int j = 0; j < 4; ++j) st_d(P + (size_t)(r0 + k4 + 4 * j) * n + c0 + c, t[j]);
 }
 
 // D columns carried by workers: J = 1 .. nt-1 (LINV: 0 .. nt-1, column 0 then
@@ -384,7 +383,6 @@ __device__ __forceinline__ bool takes_update(int type, int J, int k, int I) {
 // step k of a loop from the bottom: lane (q, r) sums U_kj[r][4q..4q+3] x_j over
 // j > k (j descending), the quarter sums are added by two xor shuffles, and
 // x_k = T_k^T (y_k - that).
-template <bool WT>
 __device__ __forceinline__ void top_back(aug::Shared &sh, const CRView &v, int I, int nt, const d4 *t, int lane) {
   using namespace aug;
   const int n = v.n, q = lane >> 4, r = lane & 15, k4 = lane >> 4;
@@ -416,7 +414,7 @@ __device__ __forceinline__ void top_back(aug::Shared &sh, const CRView &v, int I
     x += __shfl_xor(x, 32, 64);
     if (q == 0) {
       sh.bx[16 * i + r] = x;
-      st_d<WT>(v.x + (size_t)I * n + 16 * i + r, x);
+      st_d(v.x + (size_t)I * n + 16 * i + r, x);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -424,10 +422,10 @@ __device__ __forceinline__ void top_back(aug::Shared &sh, const CRView &v, int I
   }
 }
 
-// A wait gave up (aug::spin, or a dependency wait of k_cr_persist): the
-// solve is marked failed (flags[0] = 0: the trial is rejected, as for a
-// non-positive pivot) and flags[1] keeps the error for the host, which returns
-// SQLM_ERR_HIP (never a silently wrong factor).
+// A wait gave up (aug::spin / spin_to): the solve is marked failed (flags[0]
+// = 0: the trial is rejected, as for a non-positive pivot) and flags[1] keeps
+// the error for the host, which returns SQLM_ERR_HIP (never a silently wrong
+// factor).
 constexpr int kCrErrTimeout = 1;
 __device__ __forceinline__ void cr_fail(const CRView &v, int lane) {
   if (lane == 0) {
@@ -437,15 +435,12 @@ __device__ __forceinline__ void cr_fail(const CRView &v, int lane) {
 }
 
 // MODE 0: level step (A_I, C_I, z_I and the back-substitution factor).
-// MODE 1: factor only (z_I and the factor).
-// MODE 2: step I of the sequential block-tridiagonal factorization (k_cr_seq):
-// C_I = L^-1 E_I (when I + h < p), z_I and the factor; no left column. LINV: the factor is Linv_I
+// MODE 1: factor only (z_I and the factor). LINV: the factor is Linv_I
 // (lower, dense tiles); otherwise the upper U tiles with T_k on the diagonal.
 // Superblock I, workgroup sidx of the split that serve it. Every thread of the
 // workgroup enters; waves return as their role ends (no barrier after the
-// first). WT: results stored write-through (sc1) for in-launch consumers in
-// other workgroups (k_cr_persist).
-template <int MODE, bool LINV, bool BACK, bool WT>
+// first).
+template <int MODE, bool LINV, bool BACK>
 __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h, int I, int split, int sidx) {
   using namespace aug;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -542,7 +537,7 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
       // U_k,k+1 feeds the trailing updates of row k+1
       put_tile(sh.U[pair_id(k, k + 1)], P, lane);
       raise_flag(&sh.fU[pair_id(k, k + 1)], lane);
-      if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * (k + 1), P, lane);
+      if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * (k + 1), P, lane);
       if (k + 2 < nt) {  // the next step's P = (k+1, k+2) and Q = (k+2, k+2) through step k
         tmo |= !spin(&sh.fU[pair_id(k, k + 2)]);  // U_k,k+2 from column k+2's worker
         const d4 X = get_tile(sh.U[pair_id(k, k + 2)], lane);
@@ -584,7 +579,7 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
 #pragma unroll
         for (int j = 0; j < 4; ++j) sh.T[k][(k4 + 4 * j) * kTp + c] = Tt[j];
         raise_flag(&sh.fT[k], lane);
-        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * k, Tt, lane);
+        if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * k, Tt, lane);
       }
       AUG_PROF(2 + k);
     }
@@ -613,13 +608,13 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
 #pragma unroll
         for (int j = 0; j < 4; ++j) sh.T[k][(k4 + 4 * j) * kTp + c] = Tt[j];
         raise_flag(&sh.fT[k], lane);
-        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * k, Tt, lane);
+        if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * k, Tt, lane);
       }
       AUG_PROF(2 + k);
       if (k + 1 < nt) {  // U_k,k+1 feeds the trailing updates of row k+1
         put_tile(sh.U[pair_id(k, k + 1)], P, lane);
         raise_flag(&sh.fU[pair_id(k, k + 1)], lane);
-        if (!LINV && first) store_tile<WT>(Lb, n, 16 * k, 16 * (k + 1), P, lane);
+        if (!LINV && first) store_tile(Lb, n, 16 * k, 16 * (k + 1), P, lane);
       }
       if (k + 2 < nt) {  // the next step's P = (k+1, k+2) and Q = (k+2, k+2) through step k
         tmo |= !spin(&sh.fH[k + 2]);
@@ -736,24 +731,24 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
     if (r >= nt) continue;
     if (type == kColD) {
       if (LINV) {
-        if (first && r > J) store_tile<WT>(Lb, n, 16 * r, 16 * (J + 1), t[r], lane);  // Linv block column J+1
+        if (first && r > J) store_tile(Lb, n, 16 * r, 16 * (J + 1), t[r], lane);  // Linv block column J+1
       } else {
-        if (first && r <= J - 2) store_tile<WT>(Lb, n, 16 * r, 16 * J, t[r], lane);  // U tile (r, J); (J-1, J): wave 0
+        if (first && r <= J - 2) store_tile(Lb, n, 16 * r, 16 * J, t[r], lane);  // U tile (r, J); (J-1, J): wave 0
       }
     } else if (type == kColI0) {
-      if (first) store_tile<WT>(Lb, n, 16 * r, 0, t[r], lane);
+      if (first) store_tile(Lb, n, 16 * r, 0, t[r], lane);
     } else if (type == kColEt) {
-      store_tile<WT>(blk(v.A, I, n), n, 16 * r, 16 * J, t[r], lane);
+      store_tile(blk(v.A, I, n), n, 16 * r, 16 * J, t[r], lane);
     } else if (type == kColE) {
-      store_tile<WT>(blk(v.C, I, n), n, 16 * r, 16 * J, t[r], lane);
+      store_tile(blk(v.C, I, n), n, 16 * r, 16 * J, t[r], lane);
     } else if (type == kColG) {
       const int k4 = lane >> 4, c = lane & 15;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (c == 0) st_d<WT>(v.g + (size_t)I * n + 16 * r + k4 + 4 * j, t[r][j]);
+        if (c == 0) st_d(v.g + (size_t)I * n + 16 * r + k4 + 4 * j, t[r][j]);
     }
   }
-  if (BACK && type == kColG) top_back<WT>(sh, v, I, nt, t, lane);
+  if (BACK && type == kColG) top_back(sh, v, I, nt, t, lane);
   if (tmo) cr_fail(v, lane);
   AUG_PROF(16 + wave);
 }
@@ -763,7 +758,7 @@ template <int MODE, bool LINV, bool BACK = false>
 __global__ __launch_bounds__(aug::kThreads) void k_cr_aug(CRView v, int h, int I0, int stride, int split) {
   extern __shared__ __attribute__((aligned(16))) unsigned char aug_lds[];
   const int ob = blockIdx.x / split, sidx = blockIdx.x - ob * split;
-  aug_body<MODE, LINV, BACK, false>(*reinterpret_cast<aug::Shared *>(aug_lds), v, h, I0 + stride * ob, split, sidx);
+  aug_body<MODE, LINV, BACK>(*reinterpret_cast<aug::Shared *>(aug_lds), v, h, I0 + stride * ob, split, sidx);
 }
 
 // Workgroups per odd superblock for the augmented factor: enough to hold the

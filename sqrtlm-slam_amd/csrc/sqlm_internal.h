@@ -25,32 +25,15 @@ constexpr int kTileNtMax = (6 * kTileHardCams + 15) / 16;  // widest tile class 
 constexpr int kBlock = 256;
 
 // ---- Levenberg-Marquardt control (optimization_algorithm_levenberg.cpp:61-164
-// inside sparse_optimizer.cpp:376-414) -------------------------------------
-// One state for the host loop and the device loop (k_reduce decides on the
-// device when the trials are enqueued ahead, DevProblem::ctl): both apply the
-// same lm_decide, so both make the same decisions bit for bit.
+// inside sparse_optimizer.cpp:376-414), host side -------------------------
 struct LMCtl {
   double lambda, ni, currentChi, iniChi;
   double chi2_end, lambda_end;
   int qmax, nbad, its, result, trials, iterations, bench;
-  int par;        // device loop: state buffers swapped iff odd (flipped on accept)
-  int par_trial;  // the parity the current trial's kernels run under (written by k_pose_update)
-  int done;       // the run is over: the kernels of a later trial return at once
-  int accepted;   // the last trial was accepted
-  int stop;       // the caller's stop flag as the device saw it
-  const volatile int *stop_src;  // mapped page-locked word the host mirrors the stop flag into
+  int done;  // the run is over
   double trace_chi2[SQLM_TRACE_MAX], trace_lambda[SQLM_TRACE_MAX];
   int trace_trials[SQLM_TRACE_MAX];
 };
-
-// (2 rho - 1)^3 of levenberg.cpp:136 (std::pow there): the exact cube rounded
-// once (two-product error terms), one formula for host and device
-__host__ __device__ inline double lm_cube(double x) {
-  const double p = x * x, e = fma(x, x, -p);   // x^2 = p + e exactly
-  const double q = p * x, f = fma(p, x, -q);   // p x = q + f exactly
-  if (!isfinite(q)) return q;                   // +-inf / NaN as pow gives them
-  return q + (f + e * x);
-}
 
 // One trial's outcome (computeActiveErrors chi2 at the trial state, the
 // predicted reduction scale, the solve status) applied to the LM state:
@@ -58,18 +41,22 @@ __host__ __device__ inline double lm_cube(double x) {
 // sparse_optimizer.cpp:376-414 with levenberg.cpp:150-163 (Terminate on
 // qmax == 10 or rho == 0, Raul's criterion). Returns true if the trial state
 // is accepted (the caller swaps the state buffers).
-__host__ __device__ inline bool lm_decide(LMCtl &c, double chi_cur, double chi_new, double scale, bool ok, bool stop) {
+inline bool lm_decide(LMCtl &c, double chi_cur, double chi_new, double scale, bool ok, bool stop) {
   if (c.qmax == 0 && c.its > 0) {  // a fresh linearization's computeActiveErrors
     c.currentChi = chi_cur;
     c.iniChi = chi_cur;
   }
-  const double tempChi = ok ? chi_new : DBL_MAX;
+  // a NaN trial chi2 is a failed trial: our sin / cos (include/sqlm_libm.h)
+  // return NaN past fdlibm's medium-range reduction (a rotation step of
+  // > 2^20 pi / 2 rad), where glibc's stay finite and the reference's chi2 is
+  // astronomically large -- rejected with a larger lambda either way
+  const double tempChi = ok && !std::isnan(chi_new) ? chi_new : DBL_MAX;
   double rho = c.currentChi - tempChi;
   const double scl = (ok ? scale : 0.0) + 1e-3;
   rho /= scl;
   bool acc = false;
-  if (rho > 0 && isfinite(tempChi)) {
-    double alpha = 1. - lm_cube(2 * rho - 1);
+  if (rho > 0 && std::isfinite(tempChi)) {
+    double alpha = 1. - std::pow(2 * rho - 1, 3);  // levenberg.cpp:136, the same libm call
     alpha = (2. / 3. < alpha) ? 2. / 3. : alpha;         // std::min(alpha, 2/3)
     const double sf = (1. / 3. < alpha) ? alpha : 1. / 3.;  // std::max(1/3, alpha)
     c.lambda *= sf;
@@ -82,7 +69,6 @@ __host__ __device__ inline bool lm_decide(LMCtl &c, double chi_cur, double chi_n
   }
   c.qmax++;
   c.trials++;
-  c.accepted = acc ? 1 : 0;
   if (!(rho < 0 && c.qmax < 10 && !stop)) {  // the iteration ends
     if (c.qmax == 10 || rho == 0) {
       c.result = 1;
@@ -239,10 +225,9 @@ struct DevProblem {
   int *flags = nullptr;                     // [4] solve_ok, device error, ...
   // device-side LM loop (trials enqueued ahead of their decisions): the trial
   // kernels take lambda, the state parity and the done flag from here
-  LMCtl *ctl = nullptr;
 };
 
-enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kDevErr = 5, kLmDone = 6, kNScalars = 8 };
+enum Scalar { kChiCur = 0, kChiNew = 1, kScale = 2, kMaxDiag = 3, kSolveOk = 4, kDevErr = 5, kNScalars = 8 };
 constexpr int kMboxSeq = 7;  // host mailbox: the scalars, then the sequence number in slot 7
 
 // partial-sum slots
@@ -351,49 +336,13 @@ int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase co
 #endif
 constexpr int kRedLong = 24;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
-struct CRPersist;
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather = true,
-                    CRPersist *ps = nullptr);  // zeroes + scatters unless cr_direct
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st,
+                    bool gather = true);  // zeroes + scatters unless cr_direct
 // band + border layout: clear F^T / the border system before S is assembled into it
 void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st);
-// Persistent cyclic reduction (k_cr_persist, sqlm_rcs_solve.hip): the whole
-// band solve -- every level's factors, eliminations and updates, the top
-// superblock and the back substitution -- as ONE launch of workgroups that
-// take tasks from an in-launch queue in dependency order and hand results
-// over through completion words (agent-scope release / acquire). The task
-// graph of a (p, n) system is built on the host once per plan.
-enum CRTaskType : int { kTkF = 0, kTkFO = 1, kTkTR = 2, kTkUP = 3, kTkTOP = 4, kTkBK = 5 };
-struct CRTask {
-  int type, I, h;
-  int a, b;               // F: split index / split; UP: first item / items; TR: first strip / strips
-  int dep_off, dep_cnt;   // predecessors: deps[dep_off .. +dep_cnt) (task ids)
-  int pad;
-};
-struct CRPersist {
-  int p = -1, n = -1, ntasks = 0, ndeps = 0, G = 0;
-  std::vector<CRTask> h_tasks;
-  std::vector<int> h_deps;
-  CRTask *tasks = nullptr;
-  int *deps = nullptr;
-  int *done = nullptr;                 // [ntasks] epoch of the launch that finished the task
-  unsigned long long *head = nullptr;  // queue head, monotonic over launches
-  unsigned long long qbase = 0;        // head value at the start of the next launch
-  int epoch = 0;
-  size_t cap_tasks = 0, cap_deps = 0;
-};
-// SQLM_CR_PERSIST=1 selects it (until validated on MI355X: per-level launches by default)
-bool cr_persist_enabled();
-// one-launch sequential solve of a small band (k_cr_seq, opt-in: SQLM_CR_SEQ=1)
-// for at most kSeqMaxP superblocks whose factor columns fit one workgroup
-bool cr_seq_enabled();
-bool cr_seq_fits(int p, int n);
-int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu);  // 0 ok, -2 HIP error
-void cr_persist_graph(int p, int n, std::vector<CRTask> &tasks, std::vector<int> &deps);  // host only
-void cr_persist_free(CRPersist &ps);
-// CR levels + top + back substitution on blocks already in CR layout; ps
-// (planned for this p, n): one persistent launch, else the per-level launches
+// CR levels + top + back substitution on blocks already in CR layout
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
-                    hipStream_t st, CRPersist *ps = nullptr, const int *skip = nullptr);
+                    hipStream_t st);
 // Dense SPD solve (sqlm_rcs_solve.hip): A (n x n, lower, n % kCRMaxN == 0) is
 // factored in place into L (+ diagonal block inverses Linv), r is consumed,
 // x = A^-1 r; flags[0] is cleared on a non-positive pivot. band > 0: A is a

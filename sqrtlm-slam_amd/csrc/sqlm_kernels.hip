@@ -32,40 +32,6 @@
 
 namespace sqlm {
 
-// ---- device-side LM loop (DevProblem::ctl) ------------------------------------
-// The trials are enqueued ahead of their decisions (k_reduce decides), so the
-// state buffer pairs cannot be swapped on the host: a trial kernel swaps its
-// own copy of the pointers when the parity it runs under is odd, takes lambda
-// from ctl, and returns at once when the run is over (a trial enqueued past
-// the end must change nothing a caller can read).
-__device__ __forceinline__ void lm_swap(DevProblem &d, int par) {
-  if (!(par & 1)) return;
-  auto sw = [](auto &a, auto &b) {
-    const auto t = a;
-    a = b;
-    b = t;
-  };
-  sw(d.pose_qt[0], d.pose_qt[1]);
-  sw(d.pose_rt[0], d.pose_rt[1]);
-  sw(d.X[0], d.X[1]);
-  sw(d.lm_R, d.lm_R_nx);
-  sw(d.lm_b, d.lm_b_nx);
-  sw(d.obs_s, d.obs_s_nx);
-  sw(d.Hpp, d.Hpp_nx);
-  sw(d.bp, d.bp_nx);
-  sw(d.pc_lm, d.px_lm);
-  sw(d.pc_lid, d.px_lid);
-}
-// false: the run is over, return. trial_par: the parity of the trial the
-// speculative camera pass belongs to (the decision may already have flipped par)
-__device__ __forceinline__ bool lm_enter(DevProblem &d, bool trial_par = false) {
-  if (!d.ctl) return true;
-  if (d.ctl->done) return false;
-  lm_swap(d, trial_par ? d.ctl->par_trial : d.ctl->par);
-  return true;
-}
-__device__ __forceinline__ double lm_lam(const DevProblem &d, double lambda) { return d.ctl ? d.ctl->lambda : lambda; }
-
 // ---------------------------------------------------------------- helpers
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -441,11 +407,8 @@ __device__ __forceinline__ void lin_butterfly(int lane, double R[6], double &b0,
 // ---------------------------------------------------------------- linearize
 
 // per-landmark kernels: at most this many blocks per bucket launch (grid-stride
-// beyond); SQLM_UPD_GRID overrides it for A/B runs (read once per process)
-static int max_grid() {
-  static const int g = std::getenv("SQLM_UPD_GRID") ? std::max(256, std::min(4096, std::atoi(std::getenv("SQLM_UPD_GRID")))) : 2048;
-  return g;
-}
+// beyond; 1024 / 4096 measured within noise, profiles/r03 + r04/ab_split_grid.log)
+static int max_grid() { return 2048; }
 
 int linearize_blocks(const Bucket &b) {
   const int nseg = b.slot_end - b.slot_begin;
@@ -536,7 +499,6 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
 // into Hpp_nx / bp_nx, launched after k_landmark_update<SPEC>.
 template <bool ST>
 __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
-  if (!lm_enter(d, true)) return;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const double *pose_rt_s = spec ? d.pose_rt[1] : d.pose_rt[0], *X_s = spec ? d.X[1] : d.X[0];
   const double *pose_qt_s = spec ? d.pose_qt[1] : d.pose_qt[0];
@@ -1035,8 +997,6 @@ constexpr int tile_occ() {
 template <int NT, bool ST>
 __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_tile(DevProblem d, double lambda,
                                                                                    int cls_off) {
-  if (!lm_enter(d)) return;
-  lambda = lm_lam(d, lambda);
   // wave w owns the accumulator tiles q with q % kTileWaves == w; 3 waves per SIMD
   // for mono problems (167 VGPRs), 2 with the stereo row (spill-free)
   constexpr int TH = kTileThreads, NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileWaves - 1) / kTileWaves;
@@ -1420,8 +1380,6 @@ constexpr int kRedThreads = SQLM_RED_THREADS;
 constexpr int kRedGroupsS = kRedThreads / 36, kRedGroupsG = kRedThreads / 6;
 
 __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double lambda, int short_blocks) {
-  if (!lm_enter(d)) return;
-  lambda = lm_lam(d, lambda);
   if ((int)blockIdx.x >= short_blocks) {  // one long S block or g row per workgroup
     __shared__ double part[kRedThreads];
     const int w = blockIdx.x - short_blocks, tid = threadIdx.x;
@@ -1491,9 +1449,9 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     // one round of long-running workgroups) then 4 on the second
     int ncls = 0;
     for (int k = 0; k <= kTileNtMax; ++k) ncls += d.tile_cls_cnt[k] > 0;
-    // one class (small windows): no fork / join; SQLM_TILE_SERIAL=1: one stream (A/B only)
-    static const bool serial = std::getenv("SQLM_TILE_SERIAL") != nullptr;
-    const bool par = ts && ts->s[0] && ts->s[1] && ncls > 1 && !serial;
+    // one class (small windows): no fork / join (one stream for all classes
+    // measured 687 -> 624 it/s, profiles/r03/ab_tile_serial_grid.log)
+    const bool par = ts && ts->s[0] && ts->s[1] && ncls > 1;
     if (par) {
       (void)hipEventRecord(ts->fork, st);
       (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
@@ -1640,21 +1598,8 @@ __device__ __forceinline__ double pose_update_item(const DevProblem &d, double l
   return sc;
 }
 
-// DLM: the parity this trial runs under, for its speculative camera pass
-// (which may run after the decision has flipped par); block `b0` writes it
-__device__ __forceinline__ bool pose_enter(DevProblem &d, int b0) {
-  if (d.ctl) {
-    if (d.ctl->done) return false;
-    if (b0 == 0 && threadIdx.x == 0) d.ctl->par_trial = d.ctl->par;
-  }
-  lm_enter(d);
-  return true;
-}
-
 template <bool CR>
 __global__ __launch_bounds__(256) void k_pose_update(DevProblem d, double lambda) {
-  if (!pose_enter(d, blockIdx.x)) return;
-  lambda = lm_lam(d, lambda);
   __shared__ double red[4];
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   double sc = 0.0;
@@ -1697,17 +1642,13 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
   if (fuse_pose && (int)blockIdx.x >= nlm_blocks) {  // k_pose_update<true>
     const int pb = blockIdx.x - nlm_blocks;
-    if (!pose_enter(d, pb)) return;
-    lambda = lm_lam(d, lambda);
-    const int p = pb * blockDim.x + threadIdx.x;
+      const int p = pb * blockDim.x + threadIdx.x;
     double sc = 0.0;
     if (p < d.n_pose) sc = pose_update_item<true>(d, lambda, p);
     const double s = block_sum(sc, red);
     if (threadIdx.x == 0) d.partials[kPartScaleCam + pb] = s;
     return;
   }
-  if (!lm_enter(d)) return;
-  lambda = lm_lam(d, lambda);
   constexpr int SPB = kBlock / W;
   const int lane = threadIdx.x & (W - 1);
   const int nseg = slot_end - slot_begin;
@@ -1895,7 +1836,6 @@ void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda,
 }
 
 __global__ __launch_bounds__(256) void k_lidar_chi2(DevProblem d) {
-  if (!lm_enter(d)) return;
   __shared__ double red[4];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   double chi = 0.0;
@@ -1930,8 +1870,6 @@ constexpr int kReduceThreads = 1024;
 __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_lm_cur, int n_lm_new, int n_cam,
                                                           int n_lid, double *mbox, unsigned long long seq) {
   __shared__ double red[6][kReduceThreads / 64];
-  const bool dlm = d.ctl != nullptr, live = dlm && !d.ctl->done;
-  if (live) lm_swap(d, d.ctl->par);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const double *p = d.partials;
   const double *base[6] = {p + d.pc_lm, p + d.pc_lid, p + kPartChiNewLm, p + kPartChiNewLid, p + kPartScaleCam,
@@ -1974,14 +1912,6 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
     *d.maxdiag = 0ull;  // ready for the next linearization's atomicMax
     d.scalars[kSolveOk] = (double)d.flags[0];
     d.scalars[kDevErr] = (double)d.flags[1];
-    if (live) {  // the trial's decision on the device (the host only watches)
-      LMCtl &c = *d.ctl;
-      const int stop = c.stop_src ? __hip_atomic_load(c.stop_src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
-      c.stop = stop;
-      const bool ok = d.flags[0] != 0 && d.flags[1] == 0;
-      if (lm_decide(c, part[0] + part[1], part[2] + part[3], part[4] + part[5], ok, stop != 0)) c.par ^= 1;
-    }
-    d.scalars[kLmDone] = dlm ? (double)d.ctl->done : 0.0;
     if (mbox) {
       mbox[kChiCur] = part[0] + part[1];
       mbox[kChiNew] = part[2] + part[3];
@@ -1989,7 +1919,6 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
       mbox[kMaxDiag] = d.scalars[kMaxDiag];
       mbox[kSolveOk] = (double)d.flags[0];
       mbox[kDevErr] = (double)d.flags[1];
-      mbox[kLmDone] = d.scalars[kLmDone];
       __threadfence_system();
       __hip_atomic_store(reinterpret_cast<unsigned long long *>(mbox + kMboxSeq), seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);

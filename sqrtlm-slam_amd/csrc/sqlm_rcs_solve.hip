@@ -40,14 +40,7 @@ namespace sqlm {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-// Result stores. WT (the persistent solve, k_cr_persist): write-through (sc1),
-// so a consumer workgroup elsewhere on the chip reads them after its agent
-// acquire without a release fence (L2 write-back) by the producer.
-template <bool WT>
-__device__ __forceinline__ void st_d(double *p, double v) {
-  if constexpr (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
+__device__ __forceinline__ void st_d(double *p, double v) { *p = v; }
 
 // Phase timestamps for tools/cr_bench (compiled with -DSQLM_CR_PROF only).
 #ifdef SQLM_CR_PROF
@@ -358,7 +351,6 @@ struct CRView {
   int *flags;
   double *L;  // [p][n][n]: Linv_I of every factored superblock
   int ld;     // k_cr_aug<1, *> only: nonzero = D is one block with this row stride (dense solve)
-  const int *skip = nullptr;  // k_cr_persist: nonzero *skip = the LM run is over (LMCtl::done), solve nothing
 };
 
 __device__ __forceinline__ double *blk(double *base, int I, int n) { return base + (size_t)I * n * n; }
@@ -481,9 +473,8 @@ __global__ __launch_bounds__(512) void k_cr_factor(CRView v, int h) {
 
 // One wavefront computes one 16x16 tile acc = op(A) op(B) over K = n,
 // skipping K blocks that are zero because A is lower triangular (LA).
-// CH: K pairs whose operands are loaded together (all of them by default;
-// the persistent solve's 128-VGPR budget takes them in chunks -- the MFMA
-// order, and so the result, is the same)
+// CH: K pairs whose operands are loaded together (all of them by default; a
+// smaller chunk changes the register budget only, not the MFMA order)
 template <bool TA, bool TB, bool LA, int CH = kCRMaxN / 8>
 __device__ __forceinline__ d4 tile_gemm(const double *A, const double *B, int n, int ti, int tj) {
   // K order within each pair of MFMA steps m: lane k4 feeds k = 8m + 2 k4 to the
@@ -527,14 +518,13 @@ __device__ __forceinline__ d4 tile_gemm(const double *A, const double *B, int n,
   return acc;
 }
 
-template <bool WT = false>
 __device__ __forceinline__ void tile_store(double *C, int n, int ti, int tj, const d4 &acc, double alpha,
                                            bool accumulate) {
   const int lane = threadIdx.x & 63, r16 = lane & 15, k4 = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     double *c = C + (ti * 16 + k4 + 4 * j) * n + tj * 16 + r16;
-    st_d<WT>(c, accumulate ? *c + alpha * acc[j] : alpha * acc[j]);
+    st_d(c, accumulate ? *c + alpha * acc[j] : alpha * acc[j]);
   }
 }
 
@@ -653,7 +643,6 @@ inline int cr_split(int n_odd, int nt) { return std::max(1, std::min(2 * nt, 256
 // D_J -= A_{J+h}^T A_{J+h} + C_{J-h}^T C_{J-h} (lower tiles only);
 // E_J = -A_{J+h}^T C_{J+h}; g_J -= A_{J+h}^T z_{J+h} + C_{J-h}^T z_{J-h}.
 // Work items per even block: nt(nt+1)/2 D tiles, nt^2 E tiles, nt g slices.
-template <bool WT = false, int CH = kCRMaxN / 8>
 __device__ __forceinline__ void cr_update_item(const CRView &v, int h, int lb) {
   const int n = v.n, nt = n >> 4, nd = nt * (nt + 1) / 2, items = nd + nt * nt + nt;
   const int ev = lb / items, rem = lb - ev * items;
@@ -664,17 +653,17 @@ __device__ __forceinline__ void cr_update_item(const CRView &v, int h, int lb) {
     int ti = 0, tj = rem;
     while (tj > ti) { tj -= ti + 1; ++ti; }
     d4 acc = {0.0, 0.0, 0.0, 0.0};
-    if (right) acc = tile_gemm<true, false, false, CH>(blk(v.A, J + h, n), blk(v.A, J + h, n), n, ti, tj);
+    if (right) acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.A, J + h, n), n, ti, tj);
     if (left) {
-      const d4 a2 = tile_gemm<true, false, false, CH>(blk(v.C, J - h, n), blk(v.C, J - h, n), n, ti, tj);
+      const d4 a2 = tile_gemm<true, false, false>(blk(v.C, J - h, n), blk(v.C, J - h, n), n, ti, tj);
       acc += a2;
     }
-    if (right || left) tile_store<WT>(blk(v.D, J, n), n, ti, tj, acc, -1.0, true);
+    if (right || left) tile_store(blk(v.D, J, n), n, ti, tj, acc, -1.0, true);
   } else if (rem < nd + nt * nt) {
     const int t = rem - nd, ti = t / nt, tj = t - ti * nt;
     if (right && J + 2 * h < v.p) {
-      const d4 acc = tile_gemm<true, false, false, CH>(blk(v.A, J + h, n), blk(v.C, J + h, n), n, ti, tj);
-      tile_store<WT>(blk(v.E, J, n), n, ti, tj, acc, -1.0, false);
+      const d4 acc = tile_gemm<true, false, false>(blk(v.A, J + h, n), blk(v.C, J + h, n), n, ti, tj);
+      tile_store(blk(v.E, J, n), n, ti, tj, acc, -1.0, false);
     }
   } else {  // right-hand side rows 16 ti .. +16
     const int ar = 16 * (rem - nd - nt * nt) + r16;
@@ -696,7 +685,7 @@ __device__ __forceinline__ void cr_update_item(const CRView &v, int h, int lb) {
       }
     }
     s = k4_sum(s);
-    if (k4 == 0) st_d<WT>(v.g + (size_t)J * n + ar, v.g[(size_t)J * n + ar] - s);
+    if (k4 == 0) st_d(v.g + (size_t)J * n + ar, v.g[(size_t)J * n + ar] - s);
   }
 }
 
@@ -832,7 +821,7 @@ __global__ __launch_bounds__(512) void k_cr_back(CRView v, int h) {
 // Wave i owns block row i: its U tiles and T_i are loaded up front, each U_ij x_j
 // term is added as soon as x_j is flagged in LDS, so after x_{i+1} only one
 // 16x16 product, two 16-lane sums and T_i^T remain on the chain.
-template <bool TOP, bool WT>
+template <bool TOP>
 __device__ __forceinline__ void back_u_body(double *sm, const CRView &v, int h, int I) {
   double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN;
   int *fx = reinterpret_cast<int *>(sm + 3 * kCRMaxN);
@@ -880,7 +869,7 @@ __device__ __forceinline__ void back_u_body(double *sm, const CRView &v, int h, 
   x += __shfl_xor(x, 32, 64);
   if (q == 0) {
     xs[16 * i + r] = x;
-    st_d<WT>(v.x + (size_t)I * n + 16 * i + r, x);
+    st_d(v.x + (size_t)I * n + 16 * i + r, x);
   }
   aug::raise_flag(&fx[i], lane);
   if (tmo) cr_fail(v, lane);
@@ -889,7 +878,7 @@ __device__ __forceinline__ void back_u_body(double *sm, const CRView &v, int h, 
 template <bool TOP>
 __global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  back_u_body<TOP, false>(sm, v, h, TOP ? 0 : h + 2 * h * blockIdx.x);
+  back_u_body<TOP>(sm, v, h, TOP ? 0 : h + 2 * h * blockIdx.x);
 }
 
 
@@ -1331,7 +1320,6 @@ __global__ __launch_bounds__(512) void k_cr_factor_at(CRView v, int I) {
 // k_cr_aug. One wavefront per 16-column strip: the levels with many odd
 // superblocks (the fused kernel would need more workgroups than CUs) run the
 // factor and this kernel instead.
-template <bool WT>
 __device__ __forceinline__ void trsm_strip(const CRView &v, int h, int I, int s) {
   const int n = v.n, nt = n >> 4, lane = threadIdx.x & 63, b = lane >> 4, i16 = lane & 15;
   const bool et = s < nt;
@@ -1383,21 +1371,21 @@ __device__ __forceinline__ void trsm_strip(const CRView &v, int h, int I, int s)
   double *out = blk(et ? v.A : v.C, I, n);
 #pragma unroll
   for (int r = 0; r < aug::kMaxNt; ++r)
-    if (r < nt) aug::store_tile<WT>(out, n, 16 * r, 16 * J, t[r], lane);
+    if (r < nt) aug::store_tile(out, n, 16 * r, 16 * J, t[r], lane);
 }
 
 __global__ __launch_bounds__(256) void k_cr_trsm(CRView v, int h, int total) {
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (gw >= total) return;
   const int nt = v.n >> 4, ob = gw / (2 * nt), s = gw - ob * 2 * nt;
-  trsm_strip<false>(v, h, h + 2 * h * ob, s);
+  trsm_strip(v, h, h + 2 * h * ob, s);
 }
 
 // SQLM_CR_LEGACY=1: the round-2 factor (panel Cholesky + explicit Linv in LDS,
 // k_cr_factor / k_cr_factor_elim / k_cr_top) instead of k_cr_aug (A/B only).
 // odd superblocks x minimum split above which a level runs factor + TRSM
-// instead of the fused k_cr_aug (SQLM_CR_WIDE overrides)
-static const int kCrAugWideWGs = std::getenv("SQLM_CR_WIDE") ? std::atoi(std::getenv("SQLM_CR_WIDE")) : 160;
+// instead of the fused k_cr_aug (160 and 300 / 1000 measured, profiles/r04)
+constexpr int kCrAugWideWGs = 160;
 
 inline bool cr_legacy() {
   static const bool on = std::getenv("SQLM_CR_LEGACY") != nullptr;
@@ -1425,7 +1413,7 @@ static bool cr_level_wide(int n_odd, int nt, bool linv) {
 }
 
 // Level h, steps 1 + 2: every odd superblock factored, A_I / C_I / z_I formed.
-static void launch_cr_level(const CRView &v, int h, int n_odd, int fuse_min, bool fuse_ok, bool linv, hipStream_t st) {
+static void launch_cr_level(const CRView &v, int h, int n_odd, bool linv, hipStream_t st) {
   const int nt = v.n / 16;
   if (!cr_legacy()) {
     const int sp = aug_split(n_odd, nt, linv, aug::extra_columns(nt, true, true));
@@ -1448,15 +1436,11 @@ static void launch_cr_level(const CRView &v, int h, int n_odd, int fuse_min, boo
       hipLaunchKernelGGL((k_cr_aug<0, false>), dim3(n_odd * sp), dim3(aug::kThreads), sizeof(aug::Shared), st, v, h, h, 2 * h, sp);
     return;
   }
+  // legacy: the fused factor + elimination, one workgroup per odd superblock
+  // from 128 of them up, several below (round 2)
   const size_t lds = cr_factor_lds(v.n);
-  if (fuse_ok) {
-    const int sp = n_odd >= fuse_min ? 1 : cr_split(n_odd, nt);
-    hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd * sp), dim3(512), lds, st, v, h, sp);
-  } else {
-    const int per = nt * nt;
-    hipLaunchKernelGGL(k_cr_factor, dim3(n_odd), dim3(512), lds, st, v, h);
-    hipLaunchKernelGGL(k_cr_elim_gemm, dim3(xcd_grid(n_odd * 2 * per)), dim3(64), 0, st, v, h, n_odd * 2 * per);
-  }
+  const int sp = n_odd >= 128 ? 1 : cr_split(n_odd, nt);
+  hipLaunchKernelGGL(k_cr_factor_elim, dim3(n_odd * sp), dim3(512), lds, st, v, h, sp);
 }
 
 int launch_cr_multi(double *D, double *L, double *E, double *A, double *C, double *gs, double *xs, double *G,
@@ -1673,8 +1657,6 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
   CRView v{p, n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
   ArwView a{p, n, R, d.cr_L, d.cr_A, d.cr_C, d.arw_G, d.arw_Z, d.cr_g};
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt, rhs = nt * (R / 16);
-  static const int fuse_min = std::getenv("SQLM_CR_FUSE_MIN") ? std::atoi(std::getenv("SQLM_CR_FUSE_MIN")) : 128;
-  static const bool fuse_ok = std::getenv("SQLM_CR_UNFUSED") == nullptr;
   const int *S = pl.sched_dev;
   int h = 1, lv = 0;
   for (; h < p; h *= 2, ++lv) {
@@ -1686,7 +1668,7 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
       const int nel = n_odd * 2 * per, tot = nel + fc * rhs;
       hipLaunchKernelGGL(k_arw_elim, dim3(xcd_grid(tot)), dim3(64), 0, st, v, a, h, nel, S + fo, tot);
     } else {
-      launch_cr_level(v, h, n_odd, fuse_min, fuse_ok, true, st);
+      launch_cr_level(v, h, n_odd, true, st);
       if (fc) hipLaunchKernelGGL(k_arw_fwd, dim3(xcd_grid(fc * rhs)), dim3(64), 0, st, a, S + fo, fc * rhs);
     }
     const int ncr = n_even * upd, tot = ncr + uc * rhs;
@@ -1715,491 +1697,24 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
   }
 }
 
-// ---- persistent cyclic reduction ---------------------------------------------
-// One launch runs the whole band solve of launch_cr_core (the SimplicialLDLT
-// solve of linear_solver_eigen.h:94-124 on the block-tridiagonal S): the
-// per-level kernels cost >= 4.5 us each as dependent launches (28 per config-4
-// solve) and every level waited for its slowest workgroup. Here each
-// workgroup (16 waves, the k_cr_aug geometry, one per CU) takes the next task
-// of a host-built list in dependency order from a queue word, waits for the
-// task's predecessors' completion words, runs the body of the kernel the
-// task replaces (same device code, same order of operations: the solution is
-// bit-identical to the per-level launches), and publishes.
-//   F   k_cr_aug<0> share sidx of odd superblock I at level h (factor, A, C, z)
-//   FO  k_cr_aug<1> on I (wide levels: factor and z only), then
-//   TR  k_cr_trsm strips a .. a+b-1 of I (A_I, C_I from the factor)
-//   UP  cr_update_item a .. a+b-1 of even superblock I (one wave per item)
-//   TOP k_cr_aug<1, BACK> on superblock 0;  BK  k_cr_back_u<false> on I
-// Hand-off (MI355X: per-XCD L2s, per-CU L1s): results are stored
-// write-through (sc1) and drained (s_waitcnt vmcnt(0)) by every storing wave,
-// a barrier, then one lane stores the task's completion word = epoch (sc1).
-// A consumer's wave 0 polls its predecessors' words relaxed (one lane each,
-// s_sleep between polls), then ONE agent acquire (L1 invalidate) + vmcnt(0) +
-// barrier before any load. Tasks are dequeued in list order, so every
-// predecessor of a dequeued task is held by a running workgroup: no deadlock
-// at any residency. Every wait is bounded; a timeout fails the solve loudly
-// (cr_fail). Completion words carry the launch's epoch and the queue head is
-// monotonic (the host adds the launch's dequeues), so nothing is reset.
-constexpr int kPersistUpdItems = 16;  // UP task: one item per wave
-
-// the task bodies as separate functions: inlined into one switch they share
-// one register allocation (the union of their live ranges spills). Each
-// names the dynamic LDS itself (extern __shared__), so its LDS accesses stay
-// DS instructions (a generic pointer parameter would turn them into FLAT
-// accesses, which do not keep the DS ordering the in-workgroup flags rely on).
-extern __shared__ __attribute__((aligned(16))) unsigned char cr_persist_lds[];
-__device__ __forceinline__ aug::Shared &persist_shared() { return *reinterpret_cast<aug::Shared *>(cr_persist_lds); }
-__device__ __noinline__ void pt_f(const CRView v, int h, int I, int split, int sidx) {
-  aug_body<0, false, false, true>(persist_shared(), v, h, I, split, sidx);
-}
-__device__ __noinline__ void pt_fo(const CRView v, int h, int I) {
-  aug_body<1, false, false, true>(persist_shared(), v, h, I, 1, 0);
-}
-__device__ __noinline__ void pt_top(const CRView v) { aug_body<1, false, true, true>(persist_shared(), v, 0, 0, 1, 0); }
-__device__ __noinline__ void pt_tr(const CRView v, int h, int I, int s) { trsm_strip<true>(v, h, I, s); }
-__device__ __noinline__ void pt_up(const CRView v, int h, int lb) { cr_update_item<true, 4>(v, h, lb); }
-
-// k_cr_back_u<false> for the persistent solve (16 waves, <= 128 VGPRs): the
-// neighbours' solutions staged in LDS, y = z_I - A_I x_{I-h} - C_I x_{I+h}
-// with one 8-row slice per wave, then the blocked backward substitution of
-// back_u_body. LEFT = false (k_cr_seq): no A_I term, y = z_I - C_I x_{I+h}.
-// WT: x stored write-through (read by other workgroups of the launch).
-template <bool LEFT, bool WT>
-__device__ __forceinline__ void back_lean_body(const CRView &v, int h, int I) {
-  double *sm = reinterpret_cast<double *>(cr_persist_lds);
-  double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN, *xl = sm + 3 * kCRMaxN, *xr = sm + 4 * kCRMaxN;
-  int *fx = reinterpret_cast<int *>(sm + 5 * kCRMaxN);
-  const int n = v.n, nt = n >> 4;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
-  const bool right = I + h < v.p;
-  if (threadIdx.x < aug::kMaxNt) fx[threadIdx.x] = 0;
-  for (int k = threadIdx.x; k < 2 * n; k += blockDim.x) {
-    if (k < n) xl[k] = LEFT ? v.x[(size_t)(I - h) * n + k] : 0.0;
-    else xr[k - n] = right ? v.x[(size_t)(I + h) * n + k - n] : 0.0;
-  }
-  // this wave's U row and T_i (waves < nt): in flight during the right-hand side
-  const int i = wave < nt ? wave : nt - 1;
-  const double *Lb = blk(v.L, I, n);
-  double u[aug::kMaxNt][4], tv[4];
-#pragma unroll
-  for (int j = 0; j < aug::kMaxNt; ++j)
-    if (j > i && j < nt) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) u[j][m] = Lb[(size_t)(16 * i + r) * n + 16 * j + 4 * q + m];  // U_ij[r][4q+m]
-    }
-#pragma unroll
-  for (int m = 0; m < 4; ++m) tv[m] = Lb[(size_t)(16 * i + 4 * q + m) * n + 16 * i + r];  // T_i[4q+m][r]
-  __syncthreads();
-  if (wave < 2 * nt) {  // row 8 wave + (lane >> 3), columns 16 u + 2 lo (+1)
-    using d2 = HIP_vector_type<double, 2>;
-    const int lo = lane & 7, row = 8 * wave + (lane >> 3), hn = n >> 1;
-    const d2 *A = reinterpret_cast<const d2 *>(blk(v.A, I, n)), *C = reinterpret_cast<const d2 *>(blk(v.C, I, n));
-    d2 a[kCRMaxN / 16], c[kCRMaxN / 16];
-#pragma unroll
-    for (int uu = 0; uu < kCRMaxN / 16; ++uu) {
-      const int cc = kclamp(16 * uu + 2 * lo, n) >> 1;
-      a[uu] = LEFT ? A[row * hn + cc] : d2{0.0, 0.0};
-      c[uu] = right ? C[row * hn + cc] : d2{0.0, 0.0};
-    }
-    double s = 0.0;
-#pragma unroll
-    for (int uu = 0; uu < kCRMaxN / 16; ++uu)
-      if (16 * uu < n) {
-        const int cc = 16 * uu + 2 * lo;
-        if (LEFT) s += a[uu].x * xl[cc] + a[uu].y * xl[cc + 1];
-        if (right) s += c[uu].x * xr[cc] + c[uu].y * xr[cc + 1];
-      }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) s += __shfl_xor(s, m, 64);
-    if (lo == 0) y[row] = v.g[(size_t)I * n + row] - s;
-  }
-  __syncthreads();
-  if (wave >= nt) return;
-  bool tmo = false;
-  double acc = 0.0;
-#pragma unroll
-  for (int j = aug::kMaxNt - 1; j > 0; --j)
-    if (j > i && j < nt) {
-      tmo |= !aug::spin(&fx[j]);
-#pragma unroll
-      for (int m = 0; m < 4; ++m) acc = fma(u[j][m], xs[16 * j + 4 * q + m], acc);
-    }
-  acc += __shfl_xor(acc, 16, 64);
-  acc += __shfl_xor(acc, 32, 64);
-  if (q == 0) rr[16 * i + r] = y[16 * i + r] - acc;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double x = 0.0;
-#pragma unroll
-  for (int m = 0; m < 4; ++m) x = fma(tv[m], rr[16 * i + 4 * q + m], x);  // lane (q, c = r)
-  x += __shfl_xor(x, 16, 64);
-  x += __shfl_xor(x, 32, 64);
-  if (q == 0) {
-    xs[16 * i + r] = x;
-    st_d<WT>(v.x + (size_t)I * n + 16 * i + r, x);
-  }
-  aug::raise_flag(&fx[i], lane);
-  if (tmo) cr_fail(v, lane);
-}
-__device__ __noinline__ void pt_bk(const CRView v, int h, int I) { back_lean_body<true, true>(v, h, I); }
-
-// ---- sequential block-tridiagonal solve (small systems, one launch) ----------
-// For a band of a few superblocks every cyclic-reduction level is a chain of
-// dependent launches (factor, update, back substitution: >= 4.5 us each). One
-// workgroup instead runs the block Thomas factorization of the same system
-// (linear_solver_eigen.h:94-124's Cholesky of S, block-tridiagonal):
-//   D'_I = D_I - C_{I-1}^T C_{I-1},  g'_I = g_I - C_{I-1}^T z_{I-1},
-//   D'_I = L_I L_I^T,  C_I = L_I^-1 E_I,  z_I = L_I^-1 g'_I   (k_cr_aug MODE 2)
-//   x_{p-1} = L^-T z_{p-1},  x_I = L_I^-T (z_I - C_I x_{I+1})  (back_lean_body)
-// with a barrier between the steps: the whole solve is one launch. Needs the
-// factor's columns in one workgroup: (nt - 1) D + nt E + g <= kWorkers.
-constexpr int kSeqMaxP = 5;
-bool cr_seq_fits(int p, int n) {
-  const int nt = n / 16;
-  return p >= 2 && p <= kSeqMaxP && aug::fixed_columns(nt, false) + aug::extra_columns(nt, false, true) <= aug::kWorkers;
-}
-
-// D'_I's lower tiles (R >= c) -= C_{I-1}^T C_{I-1} (MFMA over the 16-row slices
-// of C, in slice order), g'_I -= C_{I-1}^T z_{I-1}; every thread of the workgroup
-__device__ __noinline__ void seq_update(const CRView v, int I) {
-  const int n = v.n, nt = n >> 4, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const double *Cp = blk(v.C, I - 1, n);
-  double *D = blk(v.D, I, n);
-  int idx = 0;
-  for (int R = 0; R < nt; ++R)
-    for (int c = 0; c <= R; ++c, ++idx) {
-      if (idx % aug::kWaves != wave) continue;
-      d4 acc = aug::load_tile(D, n, 16 * R, 16 * c, lane);
-      for (int K = 0; K < nt; ++K) {
-        const d4 a = aug::load_tile(Cp, n, 16 * K, 16 * R, lane), b = aug::load_tile(Cp, n, 16 * K, 16 * c, lane);
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) acc = aug::mfma(-a[s4], b[s4], acc);
-      }
-      aug::store_tile<false>(D, n, 16 * R, 16 * c, acc, lane);
-    }
-  for (int r = threadIdx.x; r < n; r += blockDim.x) {
-    double s = 0.0;
-    for (int k = 0; k < n; ++k) s = fma(Cp[(size_t)k * n + r], v.g[(size_t)(I - 1) * n + k], s);
-    v.g[(size_t)I * n + r] -= s;
-  }
-}
-
-// the steps as separate functions (one register allocation each, as k_cr_persist)
-__device__ __noinline__ void seq_factor(const CRView v, int I) { aug_body<2, false, false, false>(persist_shared(), v, 1, I, 1, 0); }
-__device__ __noinline__ void seq_back(const CRView v, int I) { back_lean_body<false, false>(v, 1, I); }
-
-// The back substitution of the deepest cyclic-reduction levels in one
-// workgroup launch, right after the top solve: level by level from h_top / 2
-// down to h_stop, every odd superblock's x_I in turn (levels whose few odd
-// superblocks would each be a dependent launch of a few microseconds), by
-// k_cr_back_u's own body: the same bits.
-constexpr int kDeepBackOdd = 4;  // fold a back-substitution level with at most this many odd superblocks
-
-// (k_cr_back_u's geometry: one wave per 16-row slice, blockDim = 64 nt)
-// (a call per superblock: one register allocation for the body, as in the
-// single-level kernel, instead of one stretched over the loop)
-__device__ __noinline__ void deep_back_pass(const CRView v, int h, int I) {
-  back_u_body<false, false>(reinterpret_cast<double *>(cr_persist_lds), v, h, I);
-}
-__global__ __launch_bounds__(512) void k_cr_deep_back(CRView v, int h_top, int h_stop) {
-  for (int h = h_top / 2; h >= h_stop && h >= 1; h /= 2) {
-    const int n_odd = (v.p - h + 2 * h - 1) / (2 * h);
-    for (int k = 0; k < n_odd; ++k) {
-      deep_back_pass(v, h, h + 2 * h * k);
-      __syncthreads();
-    }
-  }
-}
-
-__global__ __launch_bounds__(aug::kThreads) void k_cr_seq(CRView v) {
-  const int p = v.p;
-  for (int I = 0; I < p; ++I) {
-    if (I > 0) {
-      seq_update(v, I);
-      __syncthreads();
-    }
-    seq_factor(v, I);
-    __syncthreads();
-  }
-  for (int I = p - 1; I >= 0; --I) {
-    seq_back(v, I);
-    __syncthreads();
-  }
-}
-
-__global__ __launch_bounds__(aug::kThreads) void k_cr_persist(CRView v, const CRTask *__restrict__ tasks,
-                                                             const int *__restrict__ deps, int ntasks, int *done,
-                                                             unsigned long long *head, unsigned long long qbase,
-                                                             int epoch) {
-  __shared__ CRTask s_task;
-  __shared__ int s_id;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // a trial enqueued past the end of a device-side LM run: take the tasks (the
-  // queue head must advance as the host counts) but run none
-  const bool skip = __builtin_amdgcn_readfirstlane(v.skip && *v.skip ? 1 : 0) != 0;
-  // thread 0 takes the next task into LDS (after publishing the previous one)
-  auto take = [&]() {
-    const unsigned long long q = __hip_atomic_fetch_add(head, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const long long t = (long long)(q - qbase);
-    s_id = (t >= 0 && t < ntasks) ? (int)t : -1;
-    if (t >= 0 && t < ntasks) s_task = tasks[t];
-  };
-  if (tid == 0) take();
-  __syncthreads();
-  // the task id and fields are workgroup-uniform: say so (readfirstlane), so
-  // the loop and the switch are uniform branches (a loop the compiler takes for
-  // divergent is restructured around the barriers and the dequeue)
-  int id = __builtin_amdgcn_readfirstlane(s_id);
-  while (id >= 0) {
-    CRTask tk;
-    tk.type = __builtin_amdgcn_readfirstlane(s_task.type);
-    tk.I = __builtin_amdgcn_readfirstlane(s_task.I);
-    tk.h = __builtin_amdgcn_readfirstlane(s_task.h);
-    tk.a = __builtin_amdgcn_readfirstlane(s_task.a);
-    tk.b = __builtin_amdgcn_readfirstlane(s_task.b);
-    tk.dep_off = __builtin_amdgcn_readfirstlane(s_task.dep_off);
-    tk.dep_cnt = __builtin_amdgcn_readfirstlane(s_task.dep_cnt);
-#ifdef SQLM_SPIN_DEBUG
-    if (lane == 0 && (wave == 0 || wave == 9))
-      printf("persist blk %d wave %d task %d type %d I %d h %d deps %d\n", (int)blockIdx.x, wave, id, tk.type, tk.I, tk.h,
-             tk.dep_cnt);
-#endif
-    if (!skip) {
-      if (wave == 0 && tk.dep_cnt > 0) {
-        bool ok = true;
-        for (int base = 0; base < tk.dep_cnt; base += 64) {
-          const int k = base + lane;
-          int *f = k < tk.dep_cnt ? done + deps[tk.dep_off + k] : nullptr;
-          for (int it = 0;; ++it) {
-            const bool mine = !f || __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
-            if (__all(mine)) break;
-            if (it >= aug::kSpinLimit) {
-              ok = false;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-        if (!ok) cr_fail(v, lane);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      switch (tk.type) {
-        case kTkF:
-          pt_f(v, tk.h, tk.I, tk.b, tk.a);
-          break;
-        case kTkFO:
-          pt_fo(v, tk.h, tk.I);
-          break;
-        case kTkTR:
-          if (wave < tk.b) pt_tr(v, tk.h, tk.I, tk.a + wave);
-          break;
-        case kTkUP: {
-          const int nt = v.n >> 4, items = nt * (nt + 1) / 2 + nt * nt + nt;
-          if (wave < tk.b) pt_up(v, tk.h, (tk.I / (2 * tk.h)) * items + tk.a + wave);
-          break;
-        }
-        case kTkTOP:
-          pt_top(v);
-          break;
-        default:  // kTkBK
-          pt_bk(v, tk.h, tk.I);
-          break;
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();  // every wave's results drained; s_task / s_id read by all
-    if (tid == 0) {
-      if (!skip) __hip_atomic_store(done + id, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      take();
-    }
-    __syncthreads();
-    id = __builtin_amdgcn_readfirstlane(s_id);
-  }
-}
-
-// SQLM_CR_DEEP_BACK=1: the deepest back-substitution levels in one launch
-// after the top (k_cr_deep_back). Folded into the top factor's own launch it
-// measured slower on MI355X (config-4 band solve 0.485 -> 0.592 ms,
-// tools/cr_bench; profiles/r04/cr_ab_r4.log); opt-in until measured.
-static bool deep_back_enabled() {
-  static const bool v = std::getenv("SQLM_CR_DEEP_BACK") != nullptr;
-  return v;
-}
-
-// SQLM_CR_SEQ=1: bands of <= kSeqMaxP superblocks by the one-launch sequential
-// factorization (k_cr_seq). Measured slower than the cyclic reduction on
-// MI355X (4 x 64: 0.162 vs 0.096 ms; 5 x 80: 0.245 vs 0.142 ms): opt-in only
-// (tests cover it). Read per call.
-bool cr_seq_enabled() { return std::getenv("SQLM_CR_SEQ") != nullptr; }
-
-bool cr_persist_enabled() {  // read per call (prepare, trial): tests switch it
-  const char *e = std::getenv("SQLM_CR_PERSIST");
-  return e && std::atoi(e) != 0 && !cr_legacy();
-}
-
-void cr_persist_free(CRPersist &ps) {
-  if (ps.tasks) (void)hipFree(ps.tasks);
-  if (ps.deps) (void)hipFree(ps.deps);
-  if (ps.done) (void)hipFree(ps.done);
-  if (ps.head) (void)hipFree(ps.head);
-  ps = CRPersist{};
-}
-
-// The task list of launch_cr_core's schedule for p superblocks of n rows, in
-// the order of its launches (a task's predecessors come before it).
-void cr_persist_graph(int p, int n, std::vector<CRTask> &T, std::vector<int> &D) {
-  const int nt = n / 16, items = nt * (nt + 1) / 2 + nt * nt + nt;
-  T.clear();
-  D.clear();
-  std::vector<std::vector<int>> lastw(p), prod(p);  // last writers of D/E/g_I; producers of L/A/C/z_I
-  std::vector<int> xprod(p, -1);
-  auto add = [&](CRTask t, std::vector<int> dp) {
-    std::sort(dp.begin(), dp.end());
-    dp.erase(std::unique(dp.begin(), dp.end()), dp.end());
-    t.dep_off = (int)D.size();
-    t.dep_cnt = (int)dp.size();
-    t.pad = 0;
-    D.insert(D.end(), dp.begin(), dp.end());
-    T.push_back(t);
-    return (int)T.size() - 1;
-  };
-  auto cat = [](std::vector<int> a, const std::vector<int> &b) {
-    a.insert(a.end(), b.begin(), b.end());
-    return a;
-  };
-  int h = 1;
-  for (; h < p; h *= 2) {
-    const int n_odd = (p - h + 2 * h - 1) / (2 * h), n_even = (p + 2 * h - 1) / (2 * h);
-    const bool wide = cr_level_wide(n_odd, nt, false);
-    const int sp = aug_split(n_odd, nt, false, aug::extra_columns(nt, true, true));
-    for (int o = 0; o < n_odd; ++o) {
-      const int I = h + 2 * h * o;
-      const std::vector<int> dp = cat(lastw[I], lastw[I - h]);
-      if (wide) {
-        const int f = add(CRTask{kTkFO, I, h, 0, 1}, dp);
-        const int tr = add(CRTask{kTkTR, I, h, 0, 2 * nt}, {f});
-        prod[I] = {f, tr};
-      } else {
-        for (int s = 0; s < sp; ++s) prod[I].push_back(add(CRTask{kTkF, I, h, s, sp}, dp));
-      }
-    }
-    for (int e = 0; e < n_even; ++e) {
-      const int J = 2 * h * e;
-      const bool right = J + h < p, left = J >= h;
-      if (!right && !left) continue;
-      std::vector<int> dp = lastw[J];
-      if (right) dp = cat(dp, prod[J + h]);
-      if (left) dp = cat(dp, prod[J - h]);
-      std::vector<int> ids;
-      for (int a = 0; a < items; a += kPersistUpdItems)
-        ids.push_back(add(CRTask{kTkUP, J, h, a, std::min(kPersistUpdItems, items - a)}, dp));
-      lastw[J] = ids;
-    }
-  }
-  xprod[0] = add(CRTask{kTkTOP, 0, 0, 0, 1}, lastw[0]);
-  for (h /= 2; h >= 1; h /= 2) {
-    const int n_odd = (p - h + 2 * h - 1) / (2 * h);
-    for (int o = 0; o < n_odd; ++o) {
-      const int I = h + 2 * h * o;
-      std::vector<int> dp = cat(prod[I], {xprod[I - h]});
-      if (I + h < p) dp.push_back(xprod[I + h]);
-      xprod[I] = add(CRTask{kTkBK, I, h, 0, 1}, dp);
-    }
-  }
-}
-
-int cr_persist_plan(CRPersist &ps, int p, int n, int n_cu) {
-  if (ps.p == p && ps.n == n && ps.tasks) return 0;
-  std::vector<CRTask> T;
-  std::vector<int> D;
-  cr_persist_graph(p, n, T, D);
-  if (T.size() > ps.cap_tasks || D.size() > ps.cap_deps || !ps.head) {
-    cr_persist_free(ps);
-    ps.cap_tasks = std::max<size_t>(T.size(), 64);
-    ps.cap_deps = std::max<size_t>(D.size(), 64);
-    if (hipMalloc(&ps.tasks, ps.cap_tasks * sizeof(CRTask)) != hipSuccess ||
-        hipMalloc(&ps.deps, ps.cap_deps * sizeof(int)) != hipSuccess ||
-        hipMalloc(&ps.done, ps.cap_tasks * sizeof(int)) != hipSuccess ||
-        hipMalloc(&ps.head, sizeof(unsigned long long)) != hipSuccess)
-      return -2;
-    if (hipMemset(ps.done, 0, ps.cap_tasks * sizeof(int)) != hipSuccess ||
-        hipMemset(ps.head, 0, sizeof(unsigned long long)) != hipSuccess)
-      return -2;
-    ps.qbase = 0;
-  }
-  if (hipMemcpy(ps.tasks, T.data(), T.size() * sizeof(CRTask), hipMemcpyHostToDevice) != hipSuccess ||
-      (!D.empty() && hipMemcpy(ps.deps, D.data(), D.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess))
-    return -2;
-  ps.p = p;
-  ps.n = n;
-  ps.ntasks = (int)T.size();
-  ps.ndeps = (int)D.size();
-  ps.G = std::max(1, std::min(n_cu, ps.ntasks));
-  ps.h_tasks = std::move(T);
-  ps.h_deps = std::move(D);
-  return 0;
-}
-
-static void launch_cr_persist(const CRView &v, CRPersist &ps, hipStream_t st) {
-  ++ps.epoch;
-  hipLaunchKernelGGL(k_cr_persist, dim3(ps.G), dim3(aug::kThreads), sizeof(aug::Shared), st, v, ps.tasks, ps.deps,
-                     ps.ntasks, ps.done, ps.head, ps.qbase, ps.epoch);
-  ps.qbase += (unsigned long long)ps.ntasks + (unsigned long long)ps.G;  // every workgroup's last dequeue overshoots once
-}
-
-// SQLM_CR_TOP_SPLIT=1: the top factor and its back substitution as two launches (A/B)
-static bool top_split() {
-  static const bool v = std::getenv("SQLM_CR_TOP_SPLIT") != nullptr;
-  return v;
-}
-
 // Levels, top solve and back substitution on D/E/g already in CR layout.
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p,
-                    int n, hipStream_t st, CRPersist *ps, const int *skip) {
+                    int n, hipStream_t st) {
   CRView v{p, n, 0, 0, D, E, A, C, g, x, flags, L};
-  v.skip = skip;
-  if (ps && ps->p == p && ps->n == n && ps->tasks && cr_persist_enabled()) {
-    launch_cr_persist(v, *ps, st);
-    return;
-  }
-  if (cr_seq_enabled() && cr_seq_fits(p, n) && !cr_legacy()) {  // a few superblocks: one launch
-    hipLaunchKernelGGL(k_cr_seq, dim3(1), dim3(aug::kThreads), sizeof(aug::Shared), st, v);
-    return;
-  }
   const size_t lds = cr_factor_lds(n);
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt;
-  // SQLM_CR_UNFUSED=1: separate factor and elimination launches (A/B only)
-  // SQLM_CR_FUSE_MIN: fewest odd superblocks for which a level runs fused
-  static const int fuse_min = std::getenv("SQLM_CR_FUSE_MIN") ? std::atoi(std::getenv("SQLM_CR_FUSE_MIN")) : 128;
-  static const bool fuse_ok = std::getenv("SQLM_CR_UNFUSED") == nullptr;
   int h = 1;
   for (; h < p; h *= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
-    launch_cr_level(v, h, n_odd, fuse_min, fuse_ok, false, st);
+    launch_cr_level(v, h, n_odd, false, st);
     hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
   }
   const size_t back_lds = 3 * kCRMaxN * sizeof(double) + aug::kMaxNt * sizeof(int);
-  if (cr_legacy()) {
+  if (cr_legacy())
     hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
-  } else if (top_split()) {  // x_0 = U_0^-1 z_0 (A/B: factor and back substitution as two launches)
-    launch_cr_factor(v, 0, 0, 0, 1, false, st);
-    hipLaunchKernelGGL(k_cr_back_u<true>, dim3(1), dim3(64 * nt), back_lds, st, v, 0);
-  } else {  // x_0 = U_0^-1 z_0 by the top factor's workgroup
+  else  // x_0 = U_0^-1 z_0 by the top factor's workgroup
     hipLaunchKernelGGL((k_cr_aug<1, false, true>), dim3(1), dim3(aug::kThreads), sizeof(aug::Shared), st, v, 0, 0, 0, 1);
-    if (deep_back_enabled()) {  // ... and the deepest back-substitution levels in one more launch
-      int h_stop = h;
-      while (h_stop > 1 && (p - h_stop / 2 + h_stop - 1) / h_stop <= kDeepBackOdd) h_stop /= 2;
-      if (h_stop < h) {
-        const size_t lds = 3 * kCRMaxN * sizeof(double) + aug::kMaxNt * sizeof(int);
-        hipLaunchKernelGGL(k_cr_deep_back, dim3(1), dim3(64 * nt), lds, st, v, h, h_stop);
-      }
-      h = h_stop;
-    }
-  }
   for (h /= 2; h >= 1; h /= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     if (cr_legacy())
@@ -2209,9 +1724,8 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
   }
 }
 
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather, CRPersist *ps) {
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather) {
   CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
-  v.skip = d.ctl ? &d.ctl->done : nullptr;
   if (!d.cr_direct) {  // BSR S (sharded runs / row-kernel RCS): zero the superblocks and scatter
     const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
     if (hipMemsetAsync(d.cr_D, 0, blkbytes, st) != hipSuccess) return -2;
@@ -2220,7 +1734,7 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool 
     hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
   }
   if (pl.R) launch_arrow_solve(d, pl, st);
-  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st, ps, v.skip);
+  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
   if (gather) hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }

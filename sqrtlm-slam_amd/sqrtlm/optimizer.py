@@ -108,8 +108,8 @@ class Context:
         """Device paths of the last optimize() (sqlm_get_exec_info)."""
         out = (C.c_int * 8)()
         check(lib().sqlm_get_exec_info(self._h, out), "sqlm_get_exec_info")
-        solve = {0: "none", 1: "cr_levels", 2: "cr_persistent", 3: "band+border", 4: "dense", 5: "cr_seq"}[out[1]]
-        return dict(obs_f32=bool(out[0]), solve=solve, persist_tasks=out[2], persist_grid=out[3])
+        solve = {0: "none", 1: "cr_levels", 3: "band+border", 4: "dense"}[out[1]]
+        return dict(obs_f32=bool(out[0]), solve=solve)
 
     def bench(self, warmup: int, n: int, timers: bool = True):
         """(ms per LM iteration, per-phase ms from HIP events or {} without

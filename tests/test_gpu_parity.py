@@ -51,25 +51,18 @@ def test_optimize_local_window(gpu_ctx, oracle, seed):
 
 @pytest.mark.parametrize("n_pose", [9, 16, 28, 43, 48])
 @pytest.mark.parametrize("b_min", [True, False])
-@pytest.mark.parametrize("seq", [True, False])
-def test_small_rcs_superblock_counts(gpu_ctx, oracle, n_pose, b_min, seq, monkeypatch):
+def test_small_rcs_superblock_counts(gpu_ctx, oracle, n_pose, b_min, monkeypatch):
     """Local-BA-sized reduced camera systems of 2, 3, 5, 8 and 9 superblocks
     (cyclic reduction with 1..4 levels, odd and even counts) against the
     oracle's Cholesky (linear_solver_eigen.h:94-124). b_min: superblocks of
     bandwidth + 1 cameras (SQLM_CR_B_MIN, the level counts above); otherwise
     the width the planner's latency estimate picks (fewer, wider superblocks,
-    down to a single one). seq: bands of 2..5 superblocks whose factor fits one
-    workgroup take the one-launch sequential factorization (SQLM_CR_SEQ=1,
-    k_cr_seq, asserted through sqlm_get_exec_info); otherwise the per-level
-    cyclic reduction."""
+    down to a single one); the per-level cyclic reduction either way
+    (sqlm_get_exec_info)."""
     if b_min:
         monkeypatch.setenv("SQLM_CR_B_MIN", "1")
     else:
         monkeypatch.delenv("SQLM_CR_B_MIN", raising=False)
-    if seq:
-        monkeypatch.setenv("SQLM_CR_SEQ", "1")
-    else:
-        monkeypatch.delenv("SQLM_CR_SEQ", raising=False)
     prob = synth.make_problem(n_pose, 50 * n_pose, pair_window=4, n_fixed=3, seed=100 + n_pose, robust=True)
     ref = oracle.OracleGraph(prob)
     nr, sr = ref.optimize(0, 10)
@@ -77,8 +70,7 @@ def test_small_rcs_superblock_counts(gpu_ctx, oracle, n_pose, b_min, seq, monkey
     ng, sg = gpu_ctx.optimize(0, 10)
     lay = gpu_ctx.rcs_layout()
     assert lay["kind"] == "band" and (lay["p"] >= 2 or not b_min)
-    fits = 2 <= lay["p"] <= 5 and (lay["n"] // 16 - 1) + (lay["n"] // 16) + 1 <= 11
-    assert gpu_ctx.exec_info()["solve"] == ("cr_seq" if seq and fits else "cr_levels")
+    assert gpu_ctx.exec_info()["solve"] == "cr_levels"
     print(f"n_pose {n_pose}: {lay['p']} superblocks of {lay['B']} cameras, {gpu_ctx.exec_info()['solve']}")
     assert ng == nr
     _compare_stats(sg, sr)

@@ -1,14 +1,10 @@
-"""Round-4 schedules against each other, bit for bit.
-
-* the pose update folded into the first landmark-update launch (default for
-  small problems) vs its own launch (SQLM_NO_POSE_FUSE=1);
-* the device-side LM loop (SQLM_DLM=1: k_reduce applies lm_decide, trials
-  enqueued ahead with parity-resolved state buffers; measured slower on
-  MI355X, so opt-in) vs the host loop (default).
-Each replaces launches or host decisions only -- the arithmetic is the same
-device code in the same order -- so poses, points, edge chi2, outlier tags and
-the whole LM trace must be equal (==), on the problems of test_gpu_spec.py
-(including rejected trials and the three-pass local-BA schedule).
+"""Launch schedules against each other, bit for bit: the pose update folded
+into the first landmark-update launch (default for small problems) vs its own
+launch (SQLM_NO_POSE_FUSE=1). It replaces a launch only -- the arithmetic is
+the same device code in the same order -- so poses, points, edge chi2,
+outlier tags and the whole LM trace must be equal (==), on the problems of
+test_gpu_spec.py (including rejected trials and the three-pass local-BA
+schedule).
 """
 import numpy as np
 import pytest
@@ -37,11 +33,9 @@ def _run(ctx, prob, kind, monkeypatch, env):
     return out, q.copy(), t.copy(), ctx.points().copy(), ctx.edge_chi2().copy(), info
 
 
-NEW = {"SQLM_CR_PERSIST": None, "SQLM_DLM": None, "SQLM_NO_POSE_FUSE": None}
+NEW = {"SQLM_NO_POSE_FUSE": None}
 OLD = {
-    "device_loop": {"SQLM_DLM": "1"},
     "pose_launch": {"SQLM_NO_POSE_FUSE": "1"},
-    "device_loop_pose_launch": {"SQLM_DLM": "1", "SQLM_NO_POSE_FUSE": "1"},
 }
 
 

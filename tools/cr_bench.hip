@@ -140,12 +140,6 @@ int main(int argc, char **argv) {
     }
   }
   const int one[4] = {1, 0, 0, 0};
-  // the persistent solve (one launch; SQLM_CR_PERSIST=0: the per-level launches)
-  sqlm::CRPersist ps;
-  int ncu = 0;
-  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
-  if (sqlm::cr_persist_plan(ps, p, n, ncu)) { std::printf("persist plan failed\n"); return 2; }
-  std::printf("{\"persist_tasks\": %d, \"persist_deps\": %d, \"persist_grid\": %d}\n", ps.ntasks, ps.ndeps, ps.G);
   double best = 1e30, sum = 0.0;
   for (int it = 0; it < reps + 2; ++it) {  // 2 warmups
     CK(hipMemcpyAsync(dD, D.data(), nb * 8, hipMemcpyHostToDevice, st));
@@ -154,7 +148,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpyAsync(dflags, one, 16, hipMemcpyHostToDevice, st));
     CK(hipEventRecord(e0, st));
     if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "launch %d ...\n", it);
-    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st, &ps);
+    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st);
     CK(hipEventRecord(e1, st));
     CK(hipStreamSynchronize(st));
     CK(hipGetLastError());
@@ -168,26 +162,6 @@ int main(int argc, char **argv) {
   CK(hipMemcpy(x.data(), dx, x.size() * 8, hipMemcpyDeviceToHost));
   CK(hipMemcpy(fl, dflags, 16, hipMemcpyDeviceToHost));
   flag = fl[0];
-  if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "persistent launches done\n");
-  if (!std::getenv("CRB_NO_LEVELS")) {  // the same system through the per-level launches: the persistent solve must give the same bits
-    CK(hipMemcpy(dD, D.data(), nb * 8, hipMemcpyHostToDevice));
-    CK(hipMemcpy(dE, E.data(), nb * 8, hipMemcpyHostToDevice));
-    CK(hipMemcpy(dg, g.data(), g.size() * 8, hipMemcpyHostToDevice));
-    CK(hipMemcpy(dflags, one, 16, hipMemcpyHostToDevice));
-    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st, nullptr);
-    CK(hipStreamSynchronize(st));
-    std::vector<double> x2(g.size());
-    CK(hipMemcpy(x2.data(), dx, x2.size() * 8, hipMemcpyDeviceToHost));
-    size_t ndiff = 0;
-    double dmax = 0.0;
-    for (size_t k = 0; k < x.size(); ++k) {
-      ndiff += x[k] != x2[k];
-      dmax = std::max(dmax, std::fabs(x[k] - x2[k]));
-    }
-    std::printf("{\"persist_vs_levels\": {\"differing\": %zu, \"max_abs\": %.3e}, \"dev_err\": %d}\n", ndiff, dmax,
-                fl[1]);
-  }
-  if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "levels comparison done\n");
   if (p == 2 && std::getenv("SQLM_CR_LEGACY")) {  // stage-by-stage host check of the one-level solve (Linv layout)
     std::vector<double> dDh(nb), dLh(nb), dAh(nb), dgh(g.size());
     CK(hipMemcpy(dDh.data(), dD, nb * 8, hipMemcpyDeviceToHost));
