@@ -143,6 +143,7 @@ struct sqlm_ctx {
   std::vector<DevBuf> bufs;
   std::vector<DevBuf> pins;  // page-locked host staging of the large uploads (async DMA)
   double *h_scalars = nullptr;  // pinned
+  CRSync crs;                   // completion words of the one-launch back substitution
   // the trial scalars' mailbox (mapped, coherent page-locked memory written by
   // k_reduce): the host polls its sequence number instead of a copy + stream
   // synchronize; timing runs and sharded runs copy
@@ -271,7 +272,8 @@ enum BufId {
   B_TPART, B_OBSLOC, B_PART2, B_GPART, B_REDP, B_REDI, B_GREDP, B_GREDI, B_TGPART, B_TLD, B_URANGE,
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
-  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL, B_CAMKEY0, B_CAMKEY1, B_CAMVAL, B_SORTTMP, B_OBSQ, B_CAMQ
+  B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL, B_CAMKEY0, B_CAMKEY1, B_CAMVAL, B_SORTTMP, B_OBSQ, B_CAMQ,
+  B_CRDONE
 };
 
 // Persistent host worker pool for the setup passes (a prepare() runs ~20
@@ -1466,6 +1468,12 @@ int prepare(sqlm_ctx *c, int level) {
     AL(B_CRC, nb, d.cr_C);
     AL(B_CRG, (size_t)c->cr.p * c->cr.n, d.cr_g);
     AL(B_CRX, (size_t)c->cr.p * c->cr.n, d.cr_x);
+    {  // completion words of the one-launch back substitution, from epoch 0
+      int *dn = nullptr;
+      AL(B_CRDONE, (size_t)c->cr.p, dn);
+      HIP_OK(hipMemsetAsync(dn, 0, (size_t)c->cr.p * sizeof(int), c->stream));
+      c->crs = CRSync{dn, c->cr.p, 0};
+    }
     if (c->cr.R) {  // band + border layout
       const size_t fr = (size_t)c->cr.p * c->cr.n * c->cr.R, rp = (size_t)c->cr.Rp;
       UP(B_CAMPOS, c->cam_pos, d.cam_pos);
@@ -1816,7 +1824,7 @@ int trial_launch(sqlm_ctx *c, double lambda, bool &cam_after) {
   // unsharded CR: the pose update reads dx off the CR solution (no gather launch)
   const bool pose_from_cr = !sharded && c->cr.enabled;
   if (root) {
-    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream, !pose_from_cr)
+    s = c->cr.enabled ? launch_cr_solve(d, c->cr, c->stream, !pose_from_cr, &c->crs)
                       : launch_dense_solve(d, c->stream);
     if (s) return s == -2 ? SQLM_ERR_HIP : SQLM_ERR_UNSUPPORTED;
   }

@@ -56,6 +56,7 @@ constexpr bool kPipe = false;
 #else
 constexpr bool kPipe = true;
 #endif
+
 constexpr int kWaves = 16, kThreads = 64 * kWaves, kMaxNt = kCRMaxN / 16, kWorkers = kPipe ? 10 : 12;
 constexpr int kPairs = kMaxNt * (kMaxNt - 1) / 2;
 enum : int { kNone = 0, kColD = 1, kColI0 = 3, kColEt = 4, kColE = 5, kColG = 6 };
@@ -201,18 +202,24 @@ __device__ __forceinline__ d4 get_tile(const double *src, int lane) {
   return t;
 }
 
-// Group a of a diagonal step: the 4x4 pivot block of Dg (rows / columns
-// 4a .. 4a+3, element a of lanes 16 r + 4a + c), its Cholesky on uniform values
-// from readlane, and W = (U44^T)^-1 as the A operand of the group's MFMAs:
-// lane (b, i) holds W[i][b] (column b; zero for i >= 4).
-__device__ __forceinline__ double group_pivot(const d4 &Dg, int a, int lane, bool &bad) {
+// The 4x4 pivot block of group a of a diagonal tile Dg (rows / columns
+// 4a .. 4a+3, element a of lanes 16 r + 4a + c) as uniform values from
+// readlane: m00 m01 m02 m03 m11 m12 m13 m22 m23 m33.
+__device__ __forceinline__ void pivot_block(const d4 &Dg, int a, double (&m)[10]) {
+  m[0] = rl(Dg[a], 4 * a), m[1] = rl(Dg[a], 4 * a + 1), m[2] = rl(Dg[a], 4 * a + 2), m[3] = rl(Dg[a], 4 * a + 3);
+  m[4] = rl(Dg[a], 16 + 4 * a + 1), m[5] = rl(Dg[a], 16 + 4 * a + 2), m[6] = rl(Dg[a], 16 + 4 * a + 3);
+  m[7] = rl(Dg[a], 32 + 4 * a + 2), m[8] = rl(Dg[a], 32 + 4 * a + 3);
+  m[9] = rl(Dg[a], 48 + 4 * a + 3);
+}
+
+// The Cholesky of a group's 4x4 pivot block on uniform values, and W =
+// (U44^T)^-1 as the A operand of the group's MFMAs: lane (b, i) holds W[i][b]
+// (column b; zero for i >= 4).
+__device__ __forceinline__ double group_pivot_m(const double (&m)[10], int lane, bool &bad) {
   const int b = lane >> 4, i = lane & 15;
   const bool b0 = b == 0, b1 = b == 1, b2 = b == 2, b3 = b == 3, i3 = i == 3;
-  const double m00 = rl(Dg[a], 4 * a), m01 = rl(Dg[a], 4 * a + 1), m02 = rl(Dg[a], 4 * a + 2),
-               m03 = rl(Dg[a], 4 * a + 3);
-  const double m11 = rl(Dg[a], 16 + 4 * a + 1), m12 = rl(Dg[a], 16 + 4 * a + 2), m13 = rl(Dg[a], 16 + 4 * a + 3);
-  const double m22 = rl(Dg[a], 32 + 4 * a + 2), m23 = rl(Dg[a], 32 + 4 * a + 3);
-  const double m33 = rl(Dg[a], 48 + 4 * a + 3);
+  const double m00 = m[0], m01 = m[1], m02 = m[2], m03 = m[3], m11 = m[4], m12 = m[5], m13 = m[6], m22 = m[7],
+               m23 = m[8], m33 = m[9];
   // U44 (upper, U44^T U44 = M44) with d_r = 1 / U44[r][r]
   const double d0 = rsqn(m00, bad);
   const double u01 = m01 * d0, u02 = m02 * d0, u03 = m03 * d0;
@@ -243,6 +250,13 @@ __device__ __forceinline__ double group_pivot(const d4 &Dg, int a, int lane, boo
   }
   const double w3b = sel(b3, W[3][3], sel(b2, W[3][2], sel(b1, W[3][1], W[3][0])));
   return sel(i3, w3b, r012);
+}
+
+// Group a of a diagonal step: pivot block from Dg, then group_pivot_m.
+__device__ __forceinline__ double group_pivot(const d4 &Dg, int a, int lane, bool &bad) {
+  double m[10];
+  pivot_block(Dg, a, m);
+  return group_pivot_m(m, lane, bad);
 }
 
 // Step k on the diagonal tile Dg, in four rank-4 groups, all on one wave
@@ -486,7 +500,9 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
       if (k >= 2) tmo |= !spin(&sh.fT[k - 2]);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
+        AUG_PROF(600 + 16 * k + 4 * a);  // (cr_bench stamps: group start, pivot done, X ready)
         const double aop = group_pivot(Dg, a, lane, bad);
+        AUG_PROF(601 + 16 * k + 4 * a);
         sh.Ga[pk][a][lane] = aop;
         raise_flag(&sh.fA[pk][a], lane, k + 1);
         if (a == 3) {  // the last group updates nothing past the tile
@@ -497,6 +513,7 @@ __device__ __forceinline__ void aug_body(aug::Shared &sh, const CRView &v, int h
         // rows and columns past the group
         const d4 Xd = mfma(aop, Dg[a], zero);
         const double op = c >= 4 * a + 4 ? Xd[0] : 0.0;
+        AUG_PROF(602 + 16 * k + 4 * a);
         Dg = mfma(-op, op, Dg);
         sh.Go[pk][a][lane] = op;
         raise_flag(&sh.fO[pk][a], lane, k + 1);

@@ -336,13 +336,20 @@ int tile_profile_read(long long *out);  // diagnostic build: k_rcs_tile phase co
 #endif
 constexpr int kRedLong = 24;
 int launch_dense_solve(const DevProblem &d, hipStream_t st);  // returns SQLM status for setup errors
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st,
-                    bool gather = true);  // zeroes + scatters unless cr_direct
+// completion words of the one-launch back substitution (k_cr_back_all): one
+// per superblock, zeroed when allocated; every solve publishes a new epoch
+struct CRSync {
+  int *done = nullptr;
+  int cap = 0, epoch = 0;
+};
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather = true,
+                    CRSync *sync = nullptr);  // zeroes + scatters unless cr_direct
 // band + border layout: clear F^T / the border system before S is assembled into it
 void launch_arrow_clear(const DevProblem &d, const CRPlan &pl, hipStream_t st);
 // CR levels + top + back substitution on blocks already in CR layout
+// (sync: every back-substitution level in one launch; null: one launch per level)
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p, int n,
-                    hipStream_t st);
+                    hipStream_t st, CRSync *sync = nullptr);
 // Dense SPD solve (sqlm_rcs_solve.hip): A (n x n, lower, n % kCRMaxN == 0) is
 // factored in place into L (+ diagonal block inverses Linv), r is consumed,
 // x = A^-1 r; flags[0] is cleared on a non-positive pivot. band > 0: A is a

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 
 #include "sqlm_internal.h"
@@ -351,6 +352,8 @@ struct CRView {
   int *flags;
   double *L;  // [p][n][n]: Linv_I of every factored superblock
   int ld;     // k_cr_aug<1, *> only: nonzero = D is one block with this row stride (dense solve)
+  int *done = nullptr;  // k_cr_back_all: done[I] == epoch once x_I is published
+  int epoch = 0;
 };
 
 __device__ __forceinline__ double *blk(double *base, int I, int n) { return base + (size_t)I * n * n; }
@@ -879,6 +882,169 @@ template <bool TOP>
 __global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   back_u_body<TOP>(sm, v, h, TOP ? 0 : h + 2 * h * blockIdx.x);
+}
+
+// ---- every back-substitution level in one launch ----------------------------
+// The levels of k_cr_back_u<false> are a chain of dependent launches whose
+// work is tiny next to their launch and load latency (9 x 7-12 us on config
+// 4's band for ~2 us of arithmetic each). Here one launch holds a workgroup per
+// odd superblock of every level, coarsest level first: each loads its
+// operands (A_I, C_I, z_I, U_I, T), written by earlier launches, at once, then
+// waits for its neighbours' solutions x_{I-h}, x_{I+h} -- superblock 0 (the top
+// solve, an earlier launch) or superblocks of coarser levels, i.e. workgroups
+// with lower ids, dispatched before it, so the launch drains at any residency
+// -- and runs k_cr_back_u's arithmetic in the same order (the same bits).
+// Hand-off across the chip (per-XCD L2s): x_I is stored write-through (agent
+// scope, sc1), drained (vmcnt(0)) by every storing wave, then after a barrier
+// one lane stores done[I] = epoch (sc1; a per-solve counter, so nothing is
+// reset); the consumer polls that word with sc1 loads and s_sleep and reads x
+// with sc1 loads only. Bounded: a wait that gives up fails the solve
+// (cr_fail -> SQLM_ERR_HIP), and every wave still reaches the end.
+__device__ __forceinline__ bool wait_x(const CRView &v, int J) {
+  if (J == 0) return true;  // the top superblock: solved by an earlier launch
+  const int *f = v.done + J;
+  for (int it = 0; it < aug::kSpinLimit; ++it) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v.epoch) return true;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+__device__ __forceinline__ double ld_x(const double *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void back_all_body(double *sm, const CRView &v, int h, int I) {
+  double *y = sm, *rr = sm + kCRMaxN, *xs = sm + 2 * kCRMaxN;
+  int *fx = reinterpret_cast<int *>(sm + 3 * kCRMaxN);
+  __shared__ int tmo_s;
+  const int n = v.n, nt = n >> 4;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, q = lane >> 4, r = lane & 15;
+  const int lo = lane & 7, hi = lane >> 3;
+  const bool right = I + h < v.p;
+  if (threadIdx.x < aug::kMaxNt) fx[threadIdx.x] = 0;
+  // this wave's U row and T_i (blockDim = 64 nt: wave i owns block row i)
+  const int i = wave;
+  const double *Lb = blk(v.L, I, n);
+  double u[aug::kMaxNt][4], tv[4];
+#pragma unroll
+  for (int j = 0; j < aug::kMaxNt; ++j)
+    if (j > i && j < nt) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) u[j][m] = Lb[(size_t)(16 * i + r) * n + 16 * j + 4 * q + m];  // U_ij[r][4q+m]
+    }
+#pragma unroll
+  for (int m = 0; m < 4; ++m) tv[m] = Lb[(size_t)(16 * i + 4 * q + m) * n + 16 * i + r];  // T_i[4q+m][r]
+  // A_I, C_I rows and z_I (cr_back_body's lane map: rows 16 wave + hi (+8),
+  // columns 16 u + 2 lo (+1))
+  using d2 = HIP_vector_type<double, 2>;
+  const int ca = 2 * lo;
+  const d2 *A = reinterpret_cast<const d2 *>(blk(v.A, I, n)), *C = reinterpret_cast<const d2 *>(blk(v.C, I, n));
+  const int r0 = 16 * wave + hi, hn = n >> 1;
+  d2 a0[kCRMaxN / 16], a1[kCRMaxN / 16], c0[kCRMaxN / 16], c1[kCRMaxN / 16];
+#pragma unroll
+  for (int uu = 0; uu < kCRMaxN / 16; ++uu) {
+    const int c = kclamp(16 * uu + ca, n) >> 1;
+    a0[uu] = A[r0 * hn + c];
+    a1[uu] = A[(r0 + 8) * hn + c];
+  }
+  if (right) {
+#pragma unroll
+    for (int uu = 0; uu < kCRMaxN / 16; ++uu) {
+      const int c = kclamp(16 * uu + ca, n) >> 1;
+      c0[uu] = C[r0 * hn + c];
+      c1[uu] = C[(r0 + 8) * hn + c];
+    }
+  }
+  const double z0 = v.g[(size_t)I * n + r0], z1 = v.g[(size_t)I * n + r0 + 8];
+  // the neighbours' solutions: every load of them is an sc1 load (ld_x) of
+  // bytes stored sc1 and drained before the flag, so no acquire fence (an
+  // L1 invalidate, ~1.7 us) is needed (MI355X_MICROARCH.md, hand-off table
+  // row 1: one flag per storing workgroup, one workgroup per CU)
+  if (threadIdx.x == 0) {
+    bool ok = wait_x(v, I - h);
+    if (right) ok = wait_x(v, I + h) && ok;
+    tmo_s = ok ? 0 : 1;
+  }
+  __syncthreads();
+  const bool tmo = tmo_s != 0;
+  const double *xl = v.x + (size_t)(I - h) * n, *xr = v.x + (size_t)(I + (right ? h : 0)) * n;
+  d2 vl[kCRMaxN / 16], vr[kCRMaxN / 16];
+#pragma unroll
+  for (int uu = 0; uu < kCRMaxN / 16; ++uu) {
+    const int c = (kclamp(16 * uu + ca, n) >> 1) << 1;  // the pair cr_back_body's 16-byte load takes
+    vl[uu].x = ld_x(xl + c);
+    vl[uu].y = ld_x(xl + c + 1);
+    if (right) {
+      vr[uu].x = ld_x(xr + c);
+      vr[uu].y = ld_x(xr + c + 1);
+    }
+  }
+  // y = z - A x_{I-h} - C x_{I+h} (cr_back_body<false>, the same expressions)
+  double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+  for (int uu = 0; uu < kCRMaxN / 16; ++uu)
+    if (16 * uu < n) {
+      s0 += a0[uu].x * vl[uu].x + a0[uu].y * vl[uu].y;
+      s1 += a1[uu].x * vl[uu].x + a1[uu].y * vl[uu].y;
+      if (right) {
+        s0 += c0[uu].x * vr[uu].x + c0[uu].y * vr[uu].y;
+        s1 += c1[uu].x * vr[uu].x + c1[uu].y * vr[uu].y;
+      }
+    }
+#pragma unroll
+  for (int m = 1; m < 8; m <<= 1) {
+    s0 += __shfl_xor(s0, m, 64);
+    s1 += __shfl_xor(s1, m, 64);
+  }
+  if (lo == 0) {
+    y[r0] = z0 - s0;
+    y[r0 + 8] = z1 - s1;
+  }
+  __syncthreads();
+  // x_I = U^-1 y from the bottom (back_u_body's chain)
+  bool tw = false;
+  double acc = 0.0;
+#pragma unroll
+  for (int j = aug::kMaxNt - 1; j > 0; --j)
+    if (j > i && j < nt) {
+      tw |= !aug::spin(&fx[j]);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc = fma(u[j][m], xs[16 * j + 4 * q + m], acc);
+    }
+  acc += __shfl_xor(acc, 16, 64);
+  acc += __shfl_xor(acc, 32, 64);
+  if (q == 0) rr[16 * i + r] = y[16 * i + r] - acc;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double x = 0.0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) x = fma(tv[m], rr[16 * i + 4 * q + m], x);  // lane (q, c = r)
+  x += __shfl_xor(x, 16, 64);
+  x += __shfl_xor(x, 32, 64);
+  if (q == 0) {
+    xs[16 * i + r] = x;
+    __hip_atomic_store(v.x + (size_t)I * n + 16 * i + r, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  aug::raise_flag(&fx[i], lane);
+  if (tmo || tw) cr_fail(v, lane);
+  // publish x_I: every wave's stores drained, then the completion word
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(v.done + I, v.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// blockIdx -> (level h, odd superblock I), coarsest level (h_top) first
+__global__ __launch_bounds__(512) void k_cr_back_all(CRView v, int h_top) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  int b = blockIdx.x, h = h_top;
+  for (;;) {
+    const int n_odd = (v.p - h + 2 * h - 1) / (2 * h);
+    if (b < n_odd || h == 1) break;
+    b -= n_odd;
+    h >>= 1;
+  }
+  back_all_body(sm, v, h, h + 2 * h * b);
 }
 
 
@@ -1699,7 +1865,7 @@ static void launch_arrow_solve(const DevProblem &d, const CRPlan &pl, hipStream_
 
 // Levels, top solve and back substitution on D/E/g already in CR layout.
 void launch_cr_core(double *D, double *L, double *E, double *A, double *C, double *g, double *x, int *flags, int p,
-                    int n, hipStream_t st) {
+                    int n, hipStream_t st, CRSync *sync) {
   CRView v{p, n, 0, 0, D, E, A, C, g, x, flags, L};
   const size_t lds = cr_factor_lds(n);
   const int nt = n / 16, per = nt * nt, upd = nt * (nt + 1) / 2 + per + nt;
@@ -1715,6 +1881,16 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
     hipLaunchKernelGGL(k_cr_top, dim3(1), dim3(512), lds, st, v);
   else  // x_0 = U_0^-1 z_0 by the top factor's workgroup
     hipLaunchKernelGGL((k_cr_aug<1, false, true>), dim3(1), dim3(aug::kThreads), sizeof(aug::Shared), st, v, 0, 0, 0, 1);
+  if (!cr_legacy() && p > 1 && sync && sync->done && sync->cap >= p) {  // every back level in one launch
+    if (sync->epoch == INT_MAX) {  // (never in practice) restart the completion words
+      (void)hipMemsetAsync(sync->done, 0, (size_t)sync->cap * sizeof(int), st);
+      sync->epoch = 0;
+    }
+    v.done = sync->done;
+    v.epoch = ++sync->epoch;
+    hipLaunchKernelGGL(k_cr_back_all, dim3(p - 1), dim3(64 * nt), back_lds, st, v, h / 2);
+    return;
+  }
   for (h /= 2; h >= 1; h /= 2) {
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     if (cr_legacy())
@@ -1724,7 +1900,7 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
   }
 }
 
-int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather) {
+int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool gather, CRSync *sync) {
   CRView v{pl.p, pl.n, pl.B, d.nP, d.cr_D, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, d.cr_L};
   if (!d.cr_direct) {  // BSR S (sharded runs / row-kernel RCS): zero the superblocks and scatter
     const size_t blkbytes = (size_t)pl.p * pl.n * pl.n * sizeof(double);
@@ -1734,7 +1910,7 @@ int launch_cr_solve(const DevProblem &d, const CRPlan &pl, hipStream_t st, bool 
     hipLaunchKernelGGL(k_cr_scatter, dim3(d.nP), dim3(64), 0, st, d, v);
   }
   if (pl.R) launch_arrow_solve(d, pl, st);
-  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st);
+  else launch_cr_core(d.cr_D, d.cr_L, d.cr_E, d.cr_A, d.cr_C, d.cr_g, d.cr_x, d.flags, pl.p, pl.n, st, sync);
   if (gather) hipLaunchKernelGGL(k_cr_gather, dim3((6 * d.nP + 255) / 256), dim3(256), 0, st, d, v);
   return 0;
 }

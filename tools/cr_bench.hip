@@ -97,6 +97,18 @@ int main(int argc, char **argv) {
       std::printf("]%s", w == 15 ? "" : ", ");
     }
     std::printf("}}\n");
+    // wave 0's diagonal groups: per step k, group a: start, pivot done, X issued
+    std::printf("{\"w0_groups_%d\": [", mode);
+    for (int k = 0; k < 7; ++k)
+      for (int a = 0; a < 4; ++a) {
+        std::printf("[%d, %d", k, a);
+        for (int e = 0; e < 3; ++e) {
+          const long long v = prof[600 + 16 * k + 4 * a + e];
+          std::printf(", %lld", v ? v - prof[0] : -1);
+        }
+        std::printf("]%s", (k == 6 && a == 3) ? "" : ", ");
+      }
+    std::printf("]}\n");
     CK(hipFree(dprof));
   }
   {  // factor alone (h = 1): Linv D Linv^T == I and z == Linv g on every odd block
@@ -140,6 +152,13 @@ int main(int argc, char **argv) {
     }
   }
   const int one[4] = {1, 0, 0, 0};
+  // the back substitution in one launch (k_cr_back_all); CRB_LEVELS=1: one
+  // launch per level (A/B: the same bits)
+  int *dDone = nullptr;
+  CK(hipMalloc(&dDone, (size_t)p * sizeof(int)));
+  CK(hipMemset(dDone, 0, (size_t)p * sizeof(int)));
+  sqlm::CRSync sync{dDone, p, 0};
+  sqlm::CRSync *psync = std::getenv("CRB_LEVELS") ? nullptr : &sync;
   double best = 1e30, sum = 0.0;
   for (int it = 0; it < reps + 2; ++it) {  // 2 warmups
     CK(hipMemcpyAsync(dD, D.data(), nb * 8, hipMemcpyHostToDevice, st));
@@ -148,7 +167,7 @@ int main(int argc, char **argv) {
     CK(hipMemcpyAsync(dflags, one, 16, hipMemcpyHostToDevice, st));
     CK(hipEventRecord(e0, st));
     if (std::getenv("CRB_VERBOSE")) std::fprintf(stderr, "launch %d ...\n", it);
-    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st);
+    sqlm::launch_cr_core(dD, dL, dE, dA, dC, dg, dx, dflags, p, n, st, psync);
     CK(hipEventRecord(e1, st));
     CK(hipStreamSynchronize(st));
     CK(hipGetLastError());
