@@ -18,5 +18,6 @@ done
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/updprof -o run -- ./tools/cr_bench 278 112 5 > /dev/null 2>&1 || exit 1
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/updprof1 -o run -- ./tools/cr_bench_u1 278 112 5 > /dev/null 2>&1 || exit 1
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/updprofs -o run -- ./tools/cr_bench_ts 278 112 5 > /dev/null 2>&1 || exit 1
 timeout -k 5 60 ./tools/mfma_probe > gpurun_out/mfma_probe_r5.log 2>&1 || exit 1
 echo done

@@ -497,12 +497,23 @@ void launch_linearize(const DevProblem &d, const Bucket &b, int part_off, hipStr
 // (numeric Jacobian, base_unary_edge.hpp:82-122).
 // spec: the speculative pass at the trial state (pose / landmark buffers 1)
 // into Hpp_nx / bp_nx, launched after k_landmark_update<SPEC>.
-template <bool ST>
-__global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
+// LID: the instantiation with LiDAR edges. Their numeric Jacobian needs
+// ~2.5x the registers; without it the pass is compiled for 5 waves per SIMD
+// (96 VGPRs, a dozen spilled), which holds the whole config-4 grid -- 5000
+// waves -- resident at once: 0.095 -> 0.061 ms beside the tiles, 748 -> 760
+// it/s (one observation prefetched ahead at 4 waves per SIMD: 0.073 ms,
+// profiles/r05/ab_cam_pass_r5h.log).
+#ifndef SQLM_CAM_OCC
+#define SQLM_CAM_OCC 5
+#endif
+template <bool ST, bool LID>
+__global__ __launch_bounds__(256, LID ? 1 : SQLM_CAM_OCC) void k_camera_pass(DevProblem d, int spec) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const double *pose_rt_s = spec ? d.pose_rt[1] : d.pose_rt[0], *X_s = spec ? d.X[1] : d.X[0];
   const double *pose_qt_s = spec ? d.pose_qt[1] : d.pose_qt[0];
-  const int i = blockIdx.x * 4 + wave;
+  // the camera index is wave-uniform: said so, its pose is read with scalar
+  // loads into SGPRs (32 VGPRs less)
+  const int i = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave);
   double H[21], b[6], chi = 0.0;
 #pragma unroll
   for (int k = 0; k < 21; ++k) H[k] = 0.0;
@@ -551,7 +562,7 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
         }
       }
     }
-    if (d.nLid > 0) {
+    if (LID) {
       const int p = d.hidx_pose[i];
       const double *qt = pose_qt_s + 8 * p;
       const double q[4] = {qt[0], qt[1], qt[2], qt[3]}, t3[3] = {qt[4], qt[5], qt[6]};
@@ -598,8 +609,14 @@ __global__ __launch_bounds__(256) void k_camera_pass(DevProblem d, int spec) {
 
 void launch_camera_pass(const DevProblem &d, hipStream_t st, bool spec) {
   if (d.nP == 0) return;
-  if (d.has_stereo) hipLaunchKernelGGL(k_camera_pass<true>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d, (int)spec);
-  else hipLaunchKernelGGL(k_camera_pass<false>, dim3((d.nP + 3) / 4), dim3(256), 0, st, d, (int)spec);
+  const dim3 g((d.nP + 3) / 4);
+  if (d.nLid > 0) {
+    if (d.has_stereo) hipLaunchKernelGGL((k_camera_pass<true, true>), g, dim3(256), 0, st, d, (int)spec);
+    else hipLaunchKernelGGL((k_camera_pass<false, true>), g, dim3(256), 0, st, d, (int)spec);
+  } else {
+    if (d.has_stereo) hipLaunchKernelGGL((k_camera_pass<true, false>), g, dim3(256), 0, st, d, (int)spec);
+    else hipLaunchKernelGGL((k_camera_pass<false, false>), g, dim3(256), 0, st, d, (int)spec);
+  }
 }
 
 // Sharded runs, iteration 0: the pose Hessian diagonals of this rank (summed
@@ -1657,19 +1674,38 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
   // one tile: P0 / P1 = pose rows (R t fx fy cx cy) at the linearization / trial
   // state indexed by pose id, DX = dx rows (by pose id in the window, by free
   // camera otherwise)
-  auto tile_body = [&](int tile, const double *P0, const double *P1, const double *DX, auto in_win) {
-    constexpr bool WIN = decltype(in_win)::value;
+  // The tile's own first inputs (track bounds, the landmark's position) are
+  // requested before the window is staged, so their latency overlaps the
+  // window's instead of following it; the observations follow the window.
+  struct TileIn {
+    int slot, beg, end;
+    bool valid;
+    double L0, L1, L2;
+  };
+  auto tile_load = [&](int tile) {
+    TileIn t;
     const int seg = tile * SPB + threadIdx.x / W;
-    const int slot = slot_begin + seg;
-    const bool valid = seg < nseg;
-    double a0 = 0, a1 = 0, a2 = 0;
-    int beg = 0, end = 0;
-    if (valid) { beg = d.lm_begin[slot]; end = d.lm_begin[slot + 1]; }
+    t.slot = slot_begin + seg;
+    t.valid = seg < nseg;
+    t.beg = t.end = 0;
+    t.L0 = t.L1 = t.L2 = 0.0;
+    if (t.valid) {
+      t.beg = d.lm_begin[t.slot];
+      t.end = d.lm_begin[t.slot + 1];
+      const double *Xl = d.X[0] + 4 * t.slot;
+      t.L0 = Xl[0]; t.L1 = Xl[1]; t.L2 = Xl[2];
+    }
+    return t;
+  };
+  auto tile_body = [&](const TileIn &tin, const double *P0, const double *P1, const double *DX, auto in_win) {
+    constexpr bool WIN = decltype(in_win)::value;
+    const int slot = tin.slot, beg = tin.beg, end = tin.end;
+    const bool valid = tin.valid;
     ObsIn o[kObsPreload];
 #pragma unroll
     for (int i = 0; i < kObsPreload; ++i) o[i] = load_obs<ST, true>(d, beg + lane + i * W, beg + lane + i * W < end);
-    double L0 = 0.0, L1 = 0.0, L2 = 0.0;
-    if (valid) { L0 = d.X[0][4 * slot]; L1 = d.X[0][4 * slot + 1]; L2 = d.X[0][4 * slot + 2]; }
+    double a0 = 0, a1 = 0, a2 = 0;
+    const double L0 = tin.L0, L1 = tin.L1, L2 = tin.L2;
     // H_lp dx_cam = jl^T (jp dx_cam), Jacobians recomputed at the linearization point
     auto hlp_dx = [&](const ObsIn &o) {
       if (o.camh < 0) return;
@@ -1761,9 +1797,13 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
   };
   for (int tile = blockIdx.x; tile < ntiles; tile += nlm_blocks) {
     const int2 rg = rng[tile];  // pose id range of the tile's observations (x > y: none)
+    // (the fused variant, which forms the window's trial poses itself, keeps
+    // them after the window: hoisted there they spill)
+    TileIn tin;
+    if constexpr (!FUSE) tin = tile_load(tile);
     const int nw = rg.y - rg.x + 1;
     if (nw <= kUpdWin) {
-      __syncthreads();  // the previous tile's readers are done with the window
+      lds_barrier();  // the previous tile's readers are done with the window (the loads above stay in flight)
       if constexpr (FUSE) {
         for (int k = threadIdx.x; k < 16 * nw; k += blockDim.x) Wp0[k] = d.pose_rt[0][16 * rg.x + k];
         for (int c = threadIdx.x; c < nw; c += blockDim.x) {
@@ -1791,10 +1831,12 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
           Wdx[k] = (h >= 0 && r < 6) ? d.dx[6 * h + r] : 0.0;
         }
       }
-      __syncthreads();
-      tile_body(tile, Wp0 - 16 * rg.x, Wp1 - 16 * rg.x, Wdx - 8 * rg.x, std::true_type{});
+      lds_barrier();
+      if constexpr (FUSE) tin = tile_load(tile);
+      tile_body(tin, Wp0 - 16 * rg.x, Wp1 - 16 * rg.x, Wdx - 8 * rg.x, std::true_type{});
     } else {
-      tile_body(tile, d.pose_rt[0], d.pose_rt[1], d.dx, std::false_type{});
+      if constexpr (FUSE) tin = tile_load(tile);
+      tile_body(tin, d.pose_rt[0], d.pose_rt[1], d.dx, std::false_type{});
     }
   }
   const double s1 = block_sum(chi_acc, red);
