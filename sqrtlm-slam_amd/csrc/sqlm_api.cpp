@@ -53,7 +53,7 @@ const char *kTimerNames[SQLM_NKERNEL_TIMERS] = {"k_linearize", "k_camera_pass", 
 // cameras fit a window of <= kTileMaxCams cameras (sorted), plus the reduction
 // lists that sum each S block / g row from its tiles in tile order.
 struct TilePlan {
-  std::vector<int> lm_ptr{0}, cam_ptr{0}, cams, obs_local, ld, red_ptr, gred_ptr;
+  std::vector<int> lm_ptr{0}, cam_ptr{0}, cams, ld, red_ptr, gred_ptr;
   std::vector<int2> urange, gred_idx;
   std::vector<int64_t> red_off;   // absolute offset (doubles) of each contribution's 6x6 block in part
   std::vector<int64_t> gred_off;  // ... and of each g contribution's 6 doubles in gpart
@@ -70,7 +70,7 @@ struct TilePlan {
     cam_ptr.assign(1, 0);
     part_ptr.assign(1, 0);
     gpart_ptr.assign(1, 0);
-    for (auto *v : {&cams, &obs_local, &ld, &red_ptr, &gred_ptr, &long_s, &long_g, &order}) v->clear();
+    for (auto *v : {&cams, &ld, &red_ptr, &gred_ptr, &long_s, &long_g, &order}) v->clear();
     urange.clear();
     gred_idx.clear();
     red_off.clear();
@@ -262,7 +262,8 @@ int upload(sqlm_ctx *c, int idx, const PinVec<T> &v, T **out) {
   return SQLM_OK;
 }
 
-enum PinId { P_OBSLM, P_OBSCAM, P_OBSCAMH, P_OBSUV, P_OBSINFO, P_OBSDELTA, P_OBSUR, P_RQT, P_RX, P_RERR, P_RERR3, P_RLERR, P_OBSQ };
+enum PinId { P_OBSLM, P_OBSCAM, P_OBSCAMH, P_OBSUV, P_OBSINFO, P_OBSDELTA, P_OBSUR, P_RQT, P_RX, P_RERR, P_RERR3, P_RLERR, P_OBSQ,
+             P_X, P_OBSLOC };
 
 enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
@@ -385,7 +386,7 @@ void fill_par(std::vector<T> &v, size_t n, T x) {
 }
 
 void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *obs_camh, int lm_cap, TilePlan &tp,
-                 TileBuild &tb) {
+                 TileBuild &tb, int *obs_local) {
   const int64_t nE = lm_begin[nL];
   const bool ptime = std::getenv("SQLM_PREP_TIMING") != nullptr;
   auto pt0 = std::chrono::steady_clock::now();
@@ -396,7 +397,6 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
     pt0 = now;
   };
   tp.reset();
-  tp.obs_local.assign(nE, -1);
   tp.urange.assign(nL, int2{-1, -1});
   // pass 1 (greedy): tile boundaries -- a tile closes before the landmark that
   // would push its window past kTileMaxCams cameras or lm_cap. The slots are
@@ -459,6 +459,7 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
   run_threads(nth, [&](int th) {
     std::vector<int> lidx(nP, -1), lcams;
     std::vector<uint8_t> pst;
+    std::vector<uint64_t> rowm;
     for (int t = th; t < nt; t += nth) {
       // the window's cameras: first sight marks (lidx = -2), then sorted (<= 24 of them)
       std::vector<int> &cur = out[t].cams;
@@ -469,18 +470,33 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
       std::sort(cur.begin(), cur.end());
       const int cp = (int)cur.size();
       for (int u = 0; u < cp; ++u) lidx[cur[u]] = u;
-      pst.assign((size_t)cp * cp, 0);
+      // co-observed camera pairs (u <= v): as one bit row per camera when the
+      // window fits 64 (a landmark ORs its camera set into the rows of its
+      // cameras: linear in its track, not quadratic), else as a byte matrix
+      const bool bits = cp <= 64;
+      if (bits) rowm.assign(cp, 0);
+      else pst.assign((size_t)cp * cp, 0);
       for (int sl = tstart[t]; sl < tstart[t + 1]; ++sl) {
         lcams.clear();
         int lo = cp, hi = -1;
+        uint64_t set = 0;
         for (int o = lm_begin[sl]; o < lm_begin[sl + 1]; ++o) {
           const int h = obs_camh[o];
           const int u = h >= 0 ? lidx[h] : -1;
-          tp.obs_local[o] = u;
-          if (u >= 0) { lcams.push_back(u); lo = std::min(lo, u); hi = std::max(hi, u); }
+          obs_local[o] = u;
+          if (u >= 0) {
+            lcams.push_back(u);
+            lo = std::min(lo, u);
+            hi = std::max(hi, u);
+            if (bits) set |= uint64_t(1) << u;
+          }
         }
         if (hi < 0) continue;
         tp.urange[sl] = int2{lo, hi};
+        if (bits) {
+          for (const int u : lcams) rowm[u] |= set;
+          continue;
+        }
         const size_t m = lcams.size();  // (a repeated camera only marks its pairs twice)
         for (size_t a = 0; a < m; ++a)
           for (size_t b = a; b < m; ++b) {
@@ -490,7 +506,8 @@ void build_tiles(int nP, int nL, const std::vector<int> &lm_begin, const int *ob
       }
       for (int u = 0; u < cp; ++u)
         for (int v = u; v < cp; ++v)
-          if (pst[(size_t)u * cp + v]) out[t].red.push_back({cur[u], t, tile_blk(u, v, cp), cur[v]});
+          if (bits ? (rowm[u] >> v & 1) : pst[(size_t)u * cp + v])
+            out[t].red.push_back({cur[u], t, tile_blk(u, v, cp), cur[v]});
       for (int u = 0; u < cp; ++u) lidx[cur[u]] = -1;
     }
   });
@@ -1182,7 +1199,11 @@ int prepare(sqlm_ctx *c, int level) {
   // (nL / 160, / 80, / 40 measured slower, profiles/r03/ab_lba_tile_lmcap.log)
   const int lm_cap = std::max(16, std::min(kTileMaxLm, (nL / 512 + 3) & ~3));
   TileBuild &tb = c->tb;
-  build_tiles(nP, nL, lm_begin, obs_camh.data(), lm_cap, tp, tb);
+  // every observation's camera in its tile's window, written straight into the
+  // page-locked upload buffer
+  PinVec<int> obs_loc;
+  if (int e = pinned(c, P_OBSLOC, (size_t)nE, obs_loc)) return e;
+  build_tiles(nP, nL, lm_begin, obs_camh.data(), lm_cap, tp, tb, obs_loc.data());
   phase("tiles");
   std::vector<int> s_row(nP + 1, 0), s_col;
   if (!sharded) {
@@ -1315,13 +1336,28 @@ int prepare(sqlm_ctx *c, int level) {
   d.cr_nband = c->cr.nband;
   d.arw_R = c->cr.R;
   d.arw_Rp = c->cr.Rp;
-  std::vector<double> qt(8 * (size_t)c->n_pose, 0.0), X(4 * (size_t)nL, 0.0);
+  std::vector<double> qt(8 * (size_t)c->n_pose, 0.0);
   for (int p = 0; p < c->n_pose; ++p) {
     for (int k = 0; k < 4; ++k) qt[8 * p + k] = c->pose_q[4 * p + k];
     for (int k = 0; k < 3; ++k) qt[8 * p + 4 + k] = c->pose_t[3 * p + k];
   }
-  for (int s = 0; s < nL; ++s)
-    for (int k = 0; k < 3; ++k) X[4 * s + k] = c->pt[3 * pts[s] + k];
+  // the landmark states in slot order go through a page-locked buffer filled
+  // on host threads, like obs_local (a pageable copy is staged by the runtime
+  // on the calling thread: ~3 ms for these two arrays, 36 MB)
+  PinVec<double> X;
+  {
+    if (int e = pinned(c, P_X, 4 * (size_t)nL, X)) return e;
+    par([&](int t) {
+      for (int sl = (int)((int64_t)nL * t / nth); sl < (int)((int64_t)nL * (t + 1) / nth); ++sl) {
+        const double *src = c->pt.data() + 3 * (size_t)pts[sl];
+        double *dst = X.data() + 4 * (size_t)sl;
+        dst[0] = src[0];
+        dst[1] = src[1];
+        dst[2] = src[2];
+        dst[3] = 0.0;
+      }
+    });
+  }
   int st = 0;
 #define UP(id, vec, ptr) \
   if ((st = upload(c, id, vec, &ptr))) return st;
@@ -1335,7 +1371,8 @@ int prepare(sqlm_ctx *c, int level) {
   UP(B_PHIDX, phidx, d.pose_hidx);
   UP(B_HIDXP, hidxp, d.hidx_pose);
   UP(B_X0, X, d.X[0]);
-  UP(B_X1, X, d.X[1]);
+  AL(B_X1, 4 * (size_t)nL, d.X[1]);
+  if (nL) HIP_OK(hipMemcpyAsync(d.X[1], d.X[0], 4 * (size_t)nL * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
   UP(B_LMBEG, lm_begin, d.lm_begin);
   AL(B_LMR, 8 * (size_t)nL, d.lm_R);
   AL(B_LMB, 4 * (size_t)nL, d.lm_b);
@@ -1360,7 +1397,7 @@ int prepare(sqlm_ctx *c, int level) {
     UP(B_TGPART, tp.gpart_ptr, d.tile_gpart_ptr);
     UP(B_TLD, tp.ld, d.tile_ld);
     UP(B_URANGE, tp.urange, d.lm_urange);
-    UP(B_OBSLOC, tp.obs_local, d.obs_local);
+    UP(B_OBSLOC, obs_loc, d.obs_local);
     AL(B_PART2, (size_t)tp.part_ptr.back(), d.part);
     AL(B_GPART, (size_t)tp.gpart_ptr.back(), d.gpart);
     UP(B_REDP, tp.red_ptr, d.red_ptr);
