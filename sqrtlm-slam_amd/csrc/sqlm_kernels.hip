@@ -25,6 +25,10 @@
 #include <algorithm>
 
 #include <cstring>
+#ifdef SQLM_TILE_HTRACE
+#include <chrono>
+#include <cstdio>
+#endif
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "se3_dev.h"
@@ -1469,10 +1473,27 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     // one class (small windows): no fork / join (one stream for all classes
     // measured 687 -> 624 it/s, profiles/r03/ab_tile_serial_grid.log)
     const bool par = ts && ts->s[0] && ts->s[1] && ncls > 1;
+#ifdef SQLM_TILE_HTRACE
+    static double acc[8] = {};
+    static int nacc = 0;
+    auto tnow = [] { return std::chrono::steady_clock::now(); };
+    auto tp0 = tnow();
+    int tk = 0;
+    auto tm = [&] {
+      const auto n = tnow();
+      acc[tk++] += std::chrono::duration<double, std::micro>(n - tp0).count();
+      tp0 = n;
+    };
+#define TH_MARK tm()
+#else
+#define TH_MARK
+#endif
     if (par) {
       (void)hipEventRecord(ts->fork, st);
+      TH_MARK;
       (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
       (void)hipStreamWaitEvent(ts->s[1], ts->fork, 0);
+      TH_MARK;
     }
 #define SQLM_TILE(NTT, S)                                                                                     \
   do {                                                                                                        \
@@ -1486,15 +1507,28 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
   } while (0)
     const hipStream_t sm = par ? ts->s[0] : st, sn = par ? ts->s[1] : st;
     SQLM_TILE(8, st);
+    TH_MARK;
     SQLM_TILE(6, sm);
+    TH_MARK;
     SQLM_TILE(9, sn); SQLM_TILE(4, sn); SQLM_TILE(3, sn);
+    TH_MARK;
 #undef SQLM_TILE
     if (par) {
       (void)hipEventRecord(ts->join[0], ts->s[0]);
       (void)hipEventRecord(ts->join[1], ts->s[1]);
+      TH_MARK;
       (void)hipStreamWaitEvent(st, ts->join[0], 0);
       (void)hipStreamWaitEvent(st, ts->join[1], 0);
+      TH_MARK;
     }
+#ifdef SQLM_TILE_HTRACE
+    if (++nacc % 20 == 0) {
+      std::fprintf(stderr, "tile launch host us (fork rec, fork waits, cls8, cls6, cls9/4/3, join recs, join waits):");
+      for (int k = 0; k < tk; ++k) std::fprintf(stderr, " %.1f", acc[k] / nacc);
+      std::fprintf(stderr, "\n");
+    }
+#endif
+#undef TH_MARK
   }
 }
 
