@@ -263,7 +263,7 @@ int upload(sqlm_ctx *c, int idx, const PinVec<T> &v, T **out) {
 }
 
 enum PinId { P_OBSLM, P_OBSCAM, P_OBSCAMH, P_OBSUV, P_OBSINFO, P_OBSDELTA, P_OBSUR, P_RQT, P_RX, P_RERR, P_RERR3, P_RLERR, P_OBSQ,
-             P_X, P_OBSLOC };
+             P_X, P_OBSLOC, P_ARENA };
 
 enum BufId {
   B_QT0, B_QT1, B_RT0, B_RT1, B_INTR, B_PHIDX, B_HIDXP, B_X0, B_X1, B_LMBEG, B_LMR, B_LMB, B_LMM, B_LMV,
@@ -274,7 +274,28 @@ enum BufId {
   B_OBSUR, B_OBSERR3, B_POSEBF, B_CAMUR, B_HDIAG, B_XSTAGE, B_DENSEL, B_DENSELI, B_DENSER, B_DENSEX,
   B_LMR_NX, B_LMB_NX, B_OBSS_NX, B_HPP_NX, B_BP_NX, B_CAMPOS, B_ARWS, B_ARWG, B_ARWZ, B_BDA, B_BDL, B_BDLI,
   B_BDR, B_BDX, B_LONGS, B_LONGG, B_UPDRNG, B_CRL, B_CAMKEY0, B_CAMKEY1, B_CAMVAL, B_SORTTMP, B_OBSQ, B_CAMQ,
-  B_CRDONE
+  B_CRDONE, B_ARENA
+};
+
+// The small host arrays of a setup go to the device in one copy: their bytes
+// are gathered into one block (256-byte aligned pieces) and their device
+// pointers point into one arena buffer. A local-BA setup is otherwise ~35
+// hipMemcpyAsync calls of a few KB at 3-10 us of host time each.
+constexpr size_t kSmallUpload = 64 << 10;
+template <class T>
+struct is_pinvec : std::false_type {};
+template <class T>
+struct is_pinvec<PinVec<T>> : std::true_type {};
+struct SmallUploads {
+  std::vector<uint8_t> host;
+  std::vector<std::pair<size_t, void **>> dst;
+  template <class T>
+  void add(const std::vector<T> &v, T **out) {
+    const size_t off = host.size(), bytes = v.size() * sizeof(T);
+    host.resize(off + ((std::max<size_t>(bytes, 1) + 255) & ~size_t(255)));
+    if (bytes) std::memcpy(host.data() + off, v.data(), bytes);
+    dst.push_back({off, reinterpret_cast<void **>(out)});
+  }
 };
 
 // Persistent host worker pool for the setup passes (a prepare() runs ~20
@@ -853,6 +874,15 @@ int prepare(sqlm_ctx *c, int level) {
       int rl = -1, rk = 0, rlo = 0, rhi = 0, rf = 0, rla = 0;
       auto flush = [&] {
         if (rl < 0) return;
+        if (nth == 1) {  // one thread (a local-BA window): plain updates (the min / max atomics are CAS loops)
+          pt_act[rl] = 1;
+          kcount[rl] += rk;
+          span_lo[rl] = std::min(span_lo[rl], rlo);
+          span_hi[rl] = std::max(span_hi[rl], rhi);
+          efirst[rl] = std::min(efirst[rl], rf);
+          elast[rl] = std::max(elast[rl], rla);
+          return;
+        }
         __atomic_store_n(&pt_act[rl], (uint8_t)1, __ATOMIC_RELAXED);
         __atomic_fetch_add(&kcount[rl], rk, __ATOMIC_RELAXED);
         __atomic_fetch_min(&span_lo[rl], rlo, __ATOMIC_RELAXED);
@@ -1359,7 +1389,22 @@ int prepare(sqlm_ctx *c, int level) {
     });
   }
   int st = 0;
+  SmallUploads small;
+  auto up = [&](int id, auto &vec, auto **ptr) -> int {  // std::vector: small ones into the arena
+    using V = std::decay_t<decltype(vec)>;
+    if constexpr (!is_pinvec<V>::value) {
+      if (vec.size() * sizeof(typename V::value_type) <= kSmallUpload) {
+        small.add(vec, ptr);
+        return SQLM_OK;
+      }
+    }
+    return upload(c, id, vec, ptr);
+  };
+  // UP: small arrays' device pointers are set when the arena is copied (before
+  // the first kernel that reads them); UPD: a direct copy, pointer set now
 #define UP(id, vec, ptr) \
+  if ((st = up(id, vec, &ptr))) return st;
+#define UPD(id, vec, ptr) \
   if ((st = upload(c, id, vec, &ptr))) return st;
 #define AL(id, n, ptr) \
   if ((st = ensure(c, id, n, &ptr))) return st;
@@ -1419,8 +1464,8 @@ int prepare(sqlm_ctx *c, int level) {
   }
   AL(B_OBSERR, 2 * (size_t)nE, d.obs_err);
   if (sharded) {
-    UP(B_CAMPTR, cam_ptr, d.cam_obs_ptr);
-    UP(B_CAMOBS, cam_obs, d.cam_obs);
+    UPD(B_CAMPTR, cam_ptr, d.cam_obs_ptr);  // (k_cam_gather below reads them)
+    UPD(B_CAMOBS, cam_obs, d.cam_obs);
   } else {  // the stable counting sort on the device (same result as the host's)
     unsigned *k0 = nullptr, *k1 = nullptr;
     int *v0 = nullptr;
@@ -1515,7 +1560,7 @@ int prepare(sqlm_ctx *c, int level) {
       const size_t fr = (size_t)c->cr.p * c->cr.n * c->cr.R, rp = (size_t)c->cr.Rp;
       UP(B_CAMPOS, c->cam_pos, d.cam_pos);
       int *sd = nullptr;
-      UP(B_ARWS, c->cr.sched, sd);
+      UPD(B_ARWS, c->cr.sched, sd);
       c->cr.sched_dev = sd;
       AL(B_ARWG, fr, d.arw_G);
       AL(B_ARWZ, fr, d.arw_Z);
@@ -1583,7 +1628,17 @@ int prepare(sqlm_ctx *c, int level) {
     }
     if (me == 0) AL(B_XSTAGE, (size_t)std::max<int64_t>(off, 1), d.xstage);
   }
+  if (!small.host.empty()) {  // the arena: one page-locked block, one copy
+    uint8_t *dev = nullptr;
+    AL(B_ARENA, small.host.size(), dev);
+    PinVec<uint8_t> stg;
+    if ((st = pinned(c, P_ARENA, small.host.size(), stg))) return st;
+    std::memcpy(stg.data(), small.host.data(), small.host.size());
+    HIP_OK(hipMemcpyAsync(dev, stg.data(), small.host.size(), hipMemcpyHostToDevice, c->stream));
+    for (const auto &[off, p] : small.dst) *p = dev + off;
+  }
 #undef UP
+#undef UPD
 #undef AL
   HIP_OK(hipMemsetAsync(d.partials, 0, sizeof(double) * kMaxPartials, c->stream));
   HIP_OK(hipMemsetAsync(d.maxdiag, 0, sizeof(unsigned long long), c->stream));
