@@ -19,10 +19,14 @@ import sys; sys.path.insert(0, {os.path.join(ROOT, 'sqrtlm-slam_amd')!r})
 import numpy as np
 from sqrtlm import synth
 from sqrtlm.optimizer import Context
-for gen in ("band", "loop"):
-    p = synth.config4(seed=4, scale={scale}) if gen == "band" else synth.config4_loop(seed=4, scale={scale})
+for gen in ("band", "loop", "lba"):
     with Context(0) as c:
-        c.set_problem(p); n, st = c.global_ba(5); q, t = c.poses()
+        if gen == "lba":  # config 2 through the three-pass local-BA schedule (small-problem paths)
+            c.set_problem(synth.config2()); ran, tags, sts = c.local_ba(); st = sts[-1]
+        else:
+            p = synth.config4(seed=4, scale={scale}) if gen == "band" else synth.config4_loop(seed=4, scale={scale})
+            c.set_problem(p); n, st = c.global_ba(5)
+        q, t = c.poses()
         np.savez({out!r} + gen, q=q, t=t, X=c.points(), chi=np.array(st["trace_chi2"]))
 """
     subprocess.run([sys.executable, "-c", code], env=env, check=True)
@@ -31,7 +35,7 @@ for gen in ("band", "loop"):
 scale = float(sys.argv[2]) if len(sys.argv) > 2 else 0.2
 run(sys.argv[1], scale, "/tmp/ab_a_")
 run("", scale, "/tmp/ab_b_")
-for gen in ("band", "loop"):
+for gen in ("band", "loop", "lba"):
     a, b = np.load(f"/tmp/ab_a_{gen}.npz"), np.load(f"/tmp/ab_b_{gen}.npz")
     same = all(np.array_equal(a[k], b[k]) for k in ("q", "t", "X", "chi"))
     print(gen, "bitwise equal" if same else f"DIFFER max dq {np.abs(a['q'] - b['q']).max():.3e} chi {a['chi'][-1]} {b['chi'][-1]}")

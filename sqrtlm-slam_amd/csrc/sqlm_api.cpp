@@ -116,6 +116,7 @@ struct sqlm_ctx {
   DevProblem d;
   std::vector<Bucket> buckets;
   std::vector<int> bucket_part_off;
+  UpdLaunch upd;  // every bucket's landmark update in one launch (nb = 0: per bucket)
   int n_lm_parts = 0;
   std::vector<int> slot_pt;          // device slot -> point id
   std::vector<int64_t> dev_edge;     // device obs -> edge id
@@ -995,6 +996,7 @@ int prepare(sqlm_ctx *c, int level) {
   });
   c->slot_pt = pts;
   c->buckets.clear();
+  c->upd = UpdLaunch{};
   c->bucket_part_off.clear();
   c->n_lm_parts = 0;
   // the slots ascend in segment width (the sort's major key): each bucket ends
@@ -1218,6 +1220,7 @@ int prepare(sqlm_ctx *c, int level) {
       b.wide = false;
       for (size_t k = b.rng_off; k < k1 && k < nb; ++k) b.wide |= upd_rng[k].y - upd_rng[k].x + 1 > kUpdWin;
     }
+    if (upd_launch_plan(c->buckets, c->bucket_part_off, c->upd)) c->upd = UpdLaunch{};  // per-bucket launches
   }
   // RCS tiles (passes 1-2: windows, local cameras, camera pairs), then the
   // reduced-camera-system pattern (upper, diagonal first) from the tiles'
@@ -1821,8 +1824,24 @@ int spec_camera_pass(sqlm_ctx *c, hipStream_t st) {
   return SQLM_OK;
 }
 
-// cam_after: the speculative camera pass goes on the context stream right
-// behind k_reduce (it runs while the host waits for the scalars and decides)
+// The speculative camera pass behind the work enqueued so far: inline on the
+// context stream (small problems), else forked to the side stream and joined
+// before the next trial's RCS reduce.
+int spec_camera_launch(sqlm_ctx *c) {
+  if (!c->cam_inline) {
+    HIP_OK(hipEventRecord(c->ev_spec_fork, c->stream));
+    HIP_OK(hipStreamWaitEvent(c->side, c->ev_spec_fork, 0));
+  }
+  if (int s = spec_camera_pass(c, c->cam_inline ? c->stream : c->side)) return s;
+  if (!c->cam_inline) {
+    HIP_OK(hipEventRecord(c->ev_spec_join, c->side));
+    c->spec_outstanding = true;
+  }
+  return SQLM_OK;
+}
+
+// cam_after: the speculative camera pass goes right behind k_reduce (it runs
+// while the host waits for the scalars and decides)
 int reduce_and_fetch(sqlm_ctx *c, TrialOut &o, bool cam_after = false) {
   DevProblem &d = c->d;
   const bool mb = c->mbox && !c->timing && !c->comm.enabled();
@@ -1830,7 +1849,7 @@ int reduce_and_fetch(sqlm_ctx *c, TrialOut &o, bool cam_after = false) {
   launch_reduce(d, c->n_lm_parts, c->n_lm_parts, (c->n_pose + 255) / 256, (int)((d.nLid + 255) / 256), c->stream,
                 mb ? c->mbox_dev : nullptr, seq);
   if (cam_after) {
-    if (int e = spec_camera_pass(c, c->stream)) return e;
+    if (int e = spec_camera_launch(c)) return e;
   }
   int s = comm_allreduce_scalars(c->comm, d.scalars, c->need_maxdiag, c->stream);
   if (s) return s;
@@ -1940,8 +1959,14 @@ int trial_launch(sqlm_ctx *c, double lambda, bool &cam_after) {
   tmark(c, 6, false);
   // (the buckets on three streams, like the tile classes, measured slower:
   // 686 -> 647 it/s, the CR solve after them 0.54 -> 0.61 ms; profiles/r03/ab_upd_streams.log)
-  for (size_t b = 0; b < c->buckets.size(); ++b)
-    launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream, c->spec, fuse && b == 0);
+  // every bucket in one launch (the fused first bucket of a small problem
+  // keeps its own launch: the fused form of the merged kernel measured slower)
+  if (!fuse && c->upd.nb > 0) {
+    launch_landmark_update_all(d, c->upd, lambda, c->stream, c->spec);
+  } else {
+    for (size_t b = 0; b < c->buckets.size(); ++b)
+      launch_landmark_update(d, c->buckets[b], lambda, c->bucket_part_off[b], c->stream, c->spec, fuse && b == 0);
+  }
   launch_lidar_chi2(d, c->stream);
   tmark(c, 6, true);
   hmark(c, 4);  // pose + landmark updates
@@ -1949,19 +1974,10 @@ int trial_launch(sqlm_ctx *c, double lambda, bool &cam_after) {
   // host's decision and the next trial; small problems (cam_inline) keep it on
   // the context stream behind k_reduce instead -- the fork / join costs the
   // host more than the overlap saves there
+  // (config 4 with the fork after k_reduce too, so that the host's scalars
+  // come ~4 us sooner: within noise, profiles/r05/ab_stream_order_rejected.log)
   cam_after = c->spec && c->cam_inline && !c->timing;
-  if (c->spec && !cam_after) {
-    if (!c->cam_inline) {
-      HIP_OK(hipEventRecord(c->ev_spec_fork, c->stream));
-      HIP_OK(hipStreamWaitEvent(c->side, c->ev_spec_fork, 0));
-    }
-    s = spec_camera_pass(c, c->cam_inline ? c->stream : c->side);
-    if (s) return s;
-    if (!c->cam_inline) {
-      HIP_OK(hipEventRecord(c->ev_spec_join, c->side));
-      c->spec_outstanding = true;
-    }
-  }
+  if (c->spec && !cam_after) return spec_camera_launch(c);
   return SQLM_OK;
 }
 

@@ -374,6 +374,16 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool
 // (band / border CR solves, a bucket without wide windows)
 void launch_landmark_update(const DevProblem &d, const Bucket &b, double lambda, int part_off, hipStream_t st,
                             bool spec = false, bool fuse_pose = false);
+// every bucket's landmark update in one launch (by value: the block ranges,
+// heaviest bucket first); upd_launch_plan fails past kMaxUpdBuckets buckets
+constexpr int kMaxUpdBuckets = 6;
+struct UpdLaunch {
+  int nb = 0, grid = 0;
+  int W[kMaxUpdBuckets], slot_begin[kMaxUpdBuckets], slot_end[kMaxUpdBuckets], part_off[kMaxUpdBuckets],
+      rng_off[kMaxUpdBuckets], nblk[kMaxUpdBuckets], blk0[kMaxUpdBuckets];
+};
+int upd_launch_plan(const std::vector<Bucket> &bk, const std::vector<int> &part_off, UpdLaunch &u);
+void launch_landmark_update_all(const DevProblem &d, const UpdLaunch &u, double lambda, hipStream_t st, bool spec);
 void launch_lidar_chi2(const DevProblem &d, hipStream_t st);
 void launch_reduce(const DevProblem &d, int n_lm_parts_cur, int n_lm_parts_new, int n_cam_parts,
                    int n_lid_parts, hipStream_t st, double *mbox = nullptr, unsigned long long seq = 0);

@@ -1491,8 +1491,10 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     if (par) {
       (void)hipEventRecord(ts->fork, st);
       TH_MARK;
+#ifndef SQLM_TILE_FIRST8
       (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
       (void)hipStreamWaitEvent(ts->s[1], ts->fork, 0);
+#endif
       TH_MARK;
     }
 #define SQLM_TILE(NTT, S)                                                                                     \
@@ -1505,8 +1507,17 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
         hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);     \
     }                                                                                                         \
   } while (0)
+    // (the chain 9, 4, 3 on the context stream instead, so that the reduce
+    // follows its last kernel in-queue: within noise, profiles/r05/
+    // ab_stream_order_rejected.log)
     const hipStream_t sm = par ? ts->s[0] : st, sn = par ? ts->s[1] : st;
     SQLM_TILE(8, st);
+#ifdef SQLM_TILE_FIRST8
+    if (par) {
+      (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
+      (void)hipStreamWaitEvent(ts->s[1], ts->fork, 0);
+    }
+#endif
     TH_MARK;
     SQLM_TILE(6, sm);
     TH_MARK;
@@ -1681,19 +1692,18 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool
 // blocks past nlm_blocks do k_pose_update<true>'s work, and every block tile
 // forms its window's trial poses and dx itself (the same trial_pose code, so
 // the same bits) instead of reading them -- one launch less per trial.
-template <int W, bool ST, bool SPEC, bool FUSE = false>
 // waves per SIMD the mono variants are compiled for (A/B: -DSQLM_UPD_OCC_MONO=3)
 #ifndef SQLM_UPD_OCC_MONO
 #define SQLM_UPD_OCC_MONO 4
 #endif
-__global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
-                                                         double lambda, int part_off, const int2 *rng, int nlm_blocks) {
+template <int W, bool ST, bool SPEC, bool FUSE>
+__device__ __forceinline__ void landmark_update_body(const DevProblem &d, int slot_begin, int slot_end, double lambda,
+                                                    int part_off, const int2 *rng, int nlm_blocks, int bid,
+                                                    double *red, double *Wp0, double *Wp1, double *Wdx) {
   constexpr bool fuse_pose = FUSE;
-  __shared__ double red[4];
-  __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
-  if (fuse_pose && (int)blockIdx.x >= nlm_blocks) {  // k_pose_update<true>
-    const int pb = blockIdx.x - nlm_blocks;
-      const int p = pb * blockDim.x + threadIdx.x;
+  if (fuse_pose && bid >= nlm_blocks) {  // k_pose_update<true>
+    const int pb = bid - nlm_blocks;
+    const int p = pb * blockDim.x + threadIdx.x;
     double sc = 0.0;
     if (p < d.n_pose) sc = pose_update_item<true>(d, lambda, p);
     const double s = block_sum(sc, red);
@@ -1829,7 +1839,7 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
     }
     if (valid && lane == 0) chi_acc += chi;
   };
-  for (int tile = blockIdx.x; tile < ntiles; tile += nlm_blocks) {
+  for (int tile = bid; tile < ntiles; tile += nlm_blocks) {
     const int2 rg = rng[tile];  // pose id range of the tile's observations (x > y: none)
     // (the fused variant, which forms the window's trial poses itself, keeps
     // them after the window: hoisted there they spill)
@@ -1876,9 +1886,84 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
   const double s1 = block_sum(chi_acc, red);
   const double s2 = block_sum(sc_acc, red);
   if (threadIdx.x == 0) {
-    d.partials[kPartChiNewLm + part_off + blockIdx.x] = s1;
-    d.partials[kPartScaleLm + part_off + blockIdx.x] = s2;
-    if (SPEC) d.partials[d.px_lm + part_off + blockIdx.x] = s1;  // chi2 of the next linearization
+    d.partials[kPartChiNewLm + part_off + bid] = s1;
+    d.partials[kPartScaleLm + part_off + bid] = s2;
+    if (SPEC) d.partials[d.px_lm + part_off + bid] = s1;  // chi2 of the next linearization
+  }
+}
+
+template <int W, bool ST, bool SPEC, bool FUSE = false>
+__global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_landmark_update(DevProblem d, int slot_begin, int slot_end,
+                                                         double lambda, int part_off, const int2 *rng, int nlm_blocks) {
+  __shared__ double red[4];
+  __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
+  landmark_update_body<W, ST, SPEC, FUSE>(d, slot_begin, slot_end, lambda, part_off, rng, nlm_blocks, blockIdx.x, red,
+                                          Wp0, Wp1, Wdx);
+}
+
+// Every bucket of a trial in one launch: the block range [blk0[b], blk0[b] +
+// nblk[b]) runs bucket b exactly as its own launch would (same tiles, same
+// partial slots), so the results are the same bits; one launch instead of
+// one per bucket, the heaviest bucket's blocks dispatched first, and no
+// bucket's tail idles the chip before the next starts (config 4: 0.205 ->
+// 0.178 ms, profiles/r05/ab_upd_merged_r5o.log). The fused-pose form (every
+// bucket forming its trial poses, small problems) measured slower than the
+// fused single bucket (local BA 7.33k -> 7.21k it/s, ab_upd_merged_fused_rejected.log).
+template <bool ST, bool SPEC>
+__global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_landmark_update_all(DevProblem d,
+                                                                                                 double lambda,
+                                                                                                 UpdLaunch u) {
+  __shared__ double red[4];
+  __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
+  const int bx = blockIdx.x;
+  int b = 0;
+#pragma unroll
+  for (int k = 1; k < kMaxUpdBuckets; ++k)
+    if (k < u.nb && bx >= u.blk0[k]) b = k;
+  const int bid = bx - u.blk0[b];
+  const int2 *rng = d.upd_rng + u.rng_off[b];
+#define SQLM_UCASE(WW)                                                                                       \
+  case WW:                                                                                                   \
+    landmark_update_body<WW, ST, SPEC, false>(d, u.slot_begin[b], u.slot_end[b], lambda, u.part_off[b], rng, \
+                                              u.nblk[b], bid, red, Wp0, Wp1, Wdx);                           \
+    break;
+  switch (u.W[b]) {
+    SQLM_UCASE(2) SQLM_UCASE(4) SQLM_UCASE(8) SQLM_UCASE(16) SQLM_UCASE(32) SQLM_UCASE(64)
+    default: break;
+  }
+#undef SQLM_UCASE
+}
+
+int upd_launch_plan(const std::vector<Bucket> &bk, const std::vector<int> &part_off, UpdLaunch &u) {
+  u = UpdLaunch{};
+  if (bk.size() > (size_t)kMaxUpdBuckets) return -1;
+  std::vector<int> ord(bk.size());
+  for (size_t b = 0; b < ord.size(); ++b) ord[b] = (int)b;
+  std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return bk[x].W > bk[y].W; });
+  for (int b : ord) {
+    const int nb = linearize_blocks(bk[b]);
+    if (nb <= 0) continue;
+    const int k = u.nb++;
+    u.W[k] = bk[b].W;
+    u.slot_begin[k] = bk[b].slot_begin;
+    u.slot_end[k] = bk[b].slot_end;
+    u.part_off[k] = part_off[b];
+    u.rng_off[k] = bk[b].rng_off;
+    u.nblk[k] = nb;
+    u.blk0[k] = u.grid;
+    u.grid += nb;
+  }
+  return 0;
+}
+
+void launch_landmark_update_all(const DevProblem &d, const UpdLaunch &u, double lambda, hipStream_t st, bool spec) {
+  if (u.nb <= 0 || u.grid <= 0) return;
+  if (d.has_stereo) {
+    if (spec) hipLaunchKernelGGL((k_landmark_update_all<true, true>), dim3(u.grid), dim3(kBlock), 0, st, d, lambda, u);
+    else hipLaunchKernelGGL((k_landmark_update_all<true, false>), dim3(u.grid), dim3(kBlock), 0, st, d, lambda, u);
+  } else {
+    if (spec) hipLaunchKernelGGL((k_landmark_update_all<false, true>), dim3(u.grid), dim3(kBlock), 0, st, d, lambda, u);
+    else hipLaunchKernelGGL((k_landmark_update_all<false, false>), dim3(u.grid), dim3(kBlock), 0, st, d, lambda, u);
   }
 }
 
