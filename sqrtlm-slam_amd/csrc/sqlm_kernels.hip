@@ -1491,11 +1491,6 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     if (par) {
       (void)hipEventRecord(ts->fork, st);
       TH_MARK;
-#ifndef SQLM_TILE_FIRST8
-      (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
-      (void)hipStreamWaitEvent(ts->s[1], ts->fork, 0);
-#endif
-      TH_MARK;
     }
 #define SQLM_TILE(NTT, S)                                                                                     \
   do {                                                                                                        \
@@ -1512,12 +1507,13 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     // ab_stream_order_rejected.log)
     const hipStream_t sm = par ? ts->s[0] : st, sn = par ? ts->s[1] : st;
     SQLM_TILE(8, st);
-#ifdef SQLM_TILE_FIRST8
+    // the side streams' waits (≈10 us of host time each) after the first
+    // class is on its way: the fork event already marks st's position before it
+    // (tile phase 0.520 -> 0.516 ms, profiles/r05/ab_tile_first8_r5p.log)
     if (par) {
       (void)hipStreamWaitEvent(ts->s[0], ts->fork, 0);
       (void)hipStreamWaitEvent(ts->s[1], ts->fork, 0);
     }
-#endif
     TH_MARK;
     SQLM_TILE(6, sm);
     TH_MARK;
@@ -1534,7 +1530,7 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
     }
 #ifdef SQLM_TILE_HTRACE
     if (++nacc % 20 == 0) {
-      std::fprintf(stderr, "tile launch host us (fork rec, fork waits, cls8, cls6, cls9/4/3, join recs, join waits):");
+      std::fprintf(stderr, "tile launch host us (fork rec, -, cls8 + fork waits, cls6, cls9/4/3, join recs, join waits):");
       for (int k = 0; k < tk; ++k) std::fprintf(stderr, " %.1f", acc[k] / nacc);
       std::fprintf(stderr, "\n");
     }
