@@ -2035,11 +2035,21 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
   int nmax = 0;
 #pragma unroll
   for (int r = 0; r < 6; ++r) nmax = max(nmax, n[r]);
+  // the words thread 0 publishes, requested with the partials (not after the barrier)
+  unsigned long long md = 0ull;
+  int f0 = 0, f1 = 0;
+  if (tid == 0) {
+    md = *d.maxdiag;
+    f0 = d.flags[0];
+    f1 = d.flags[1];
+  }
   double acc[6] = {0, 0, 0, 0, 0, 0};
-  for (int k0 = tid; k0 < nmax; k0 += 4 * kReduceThreads) {
-    double v[4][6];
+  // groups of four strides, two groups' loads in flight together (8192
+  // partials per memory round trip); each group summed as its own step, in order
+  for (int k0 = tid; k0 < nmax; k0 += 8 * kReduceThreads) {
+    double v[8][6];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < 8; ++u)
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
         const int k = k0 + u * kReduceThreads;
@@ -2047,6 +2057,10 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
       }
 #pragma unroll
     for (int r = 0; r < 6; ++r) acc[r] += (v[0][r] + v[1][r]) + (v[2][r] + v[3][r]);
+    if (k0 + 4 * kReduceThreads < nmax) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r) acc[r] += (v[4][r] + v[5][r]) + (v[6][r] + v[7][r]);
+    }
   }
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
@@ -2065,17 +2079,17 @@ __global__ __launch_bounds__(kReduceThreads) void k_reduce(DevProblem d, int n_l
     d.scalars[kChiCur] = part[0] + part[1];
     d.scalars[kChiNew] = part[2] + part[3];
     d.scalars[kScale] = part[4] + part[5];
-    d.scalars[kMaxDiag] = __longlong_as_double((long long)*d.maxdiag);
+    d.scalars[kMaxDiag] = __longlong_as_double((long long)md);
     *d.maxdiag = 0ull;  // ready for the next linearization's atomicMax
-    d.scalars[kSolveOk] = (double)d.flags[0];
-    d.scalars[kDevErr] = (double)d.flags[1];
+    d.scalars[kSolveOk] = (double)f0;
+    d.scalars[kDevErr] = (double)f1;
     if (mbox) {
       mbox[kChiCur] = part[0] + part[1];
       mbox[kChiNew] = part[2] + part[3];
       mbox[kScale] = part[4] + part[5];
-      mbox[kMaxDiag] = d.scalars[kMaxDiag];
-      mbox[kSolveOk] = (double)d.flags[0];
-      mbox[kDevErr] = (double)d.flags[1];
+      mbox[kMaxDiag] = __longlong_as_double((long long)md);
+      mbox[kSolveOk] = (double)f0;
+      mbox[kDevErr] = (double)f1;
       __threadfence_system();
       __hip_atomic_store(reinterpret_cast<unsigned long long *>(mbox + kMboxSeq), seq, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
