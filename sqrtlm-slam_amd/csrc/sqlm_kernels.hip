@@ -1515,20 +1515,11 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
       (void)hipStreamWaitEvent(ts->s[1], ts->fork, 0);
     }
     TH_MARK;
-#if SQLM_TILE_ORDER == 1
-    SQLM_TILE(6, sm); SQLM_TILE(4, sm);
-    TH_MARK;
-    SQLM_TILE(9, sn); SQLM_TILE(3, sn);
-#elif SQLM_TILE_ORDER == 2
-    SQLM_TILE(4, st);
-    SQLM_TILE(6, sm);
-    TH_MARK;
-    SQLM_TILE(9, sn); SQLM_TILE(3, sn);
-#else
+    // (4 behind 6, or behind 8: config 4 777 -> 776 / 761 it/s,
+    // profiles/r05/ab_tile_stream_assign_rejected.log)
     SQLM_TILE(6, sm);
     TH_MARK;
     SQLM_TILE(9, sn); SQLM_TILE(4, sn); SQLM_TILE(3, sn);
-#endif
     TH_MARK;
 #undef SQLM_TILE
     if (par) {
