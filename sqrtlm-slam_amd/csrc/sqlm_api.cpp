@@ -1005,7 +1005,15 @@ int prepare(sqlm_ctx *c, int level) {
     const int W = seg_width(kcount[pts[s]]);
     const int e = (int)(std::partition_point(pts.begin() + s, pts.end(), [&](int l) { return seg_width(kcount[l]) <= W; }) -
                         pts.begin());
-    Bucket b{W, s, e};
+    // The per-landmark kernels run a bucket with half the lanes its slot-order
+    // width names (up to 2 kObsPerLane observations per lane from W = 4 up):
+    // longer per-lane Givens chains, fewer idle lanes and butterfly rounds.
+    // The slot order -- which the RCS tiles inherit -- stays bucketed at
+    // kObsPerLane (config 4: landmark update 0.177 -> 0.160 ms, 775 -> 787
+    // it/s, profiles/r05/ab_upd_half_lanes_cr_upd2w.log; the order itself at 4
+    // per lane made the tiles 0.05 ms slower, ab_obs_per_lane_rejected.log).
+    // (a quarter of the lanes from W = 8 up: 0.160 -> 0.182 ms, ab_uq.log)
+    Bucket b{W >= 4 ? W / 2 : W, s, e};
     c->buckets.push_back(b);
     c->bucket_part_off.push_back(c->n_lm_parts);
     c->n_lm_parts += linearize_blocks(b);

@@ -1874,6 +1874,8 @@ void launch_cr_core(double *D, double *L, double *E, double *A, double *C, doubl
     const int n_odd = (p - h + 2 * h - 1) / (2 * h);
     const int n_even = (p + 2 * h - 1) / (2 * h);
     launch_cr_level(v, h, n_odd, false, st);
+    // (two waves per workgroup, a D tile's A^T A and C^T C at once: solve
+    // 0.458 -> 0.473 ms, profiles/r05/ab_upd_half_lanes_cr_upd2w.log)
     hipLaunchKernelGGL(k_cr_update_gemm, dim3(xcd_grid(n_even * upd)), dim3(64), 0, st, v, h, n_even * upd);
   }
   const size_t back_lds = 3 * kCRMaxN * sizeof(double) + aug::kMaxNt * sizeof(int);
