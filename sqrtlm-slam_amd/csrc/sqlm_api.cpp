@@ -1013,6 +1013,8 @@ int prepare(sqlm_ctx *c, int level) {
     // it/s, profiles/r05/ab_upd_half_lanes_cr_upd2w.log; the order itself at 4
     // per lane made the tiles 0.05 ms slower, ab_obs_per_lane_rejected.log).
     // (a quarter of the lanes from W = 8 up: 0.160 -> 0.182 ms, ab_uq.log)
+    // (one lane per landmark for the shortest tracks: config 4 the same, local
+    // BA 7.37k -> 7.22k it/s, ab_upd_one_lane_rejected.log)
     Bucket b{W >= 4 ? W / 2 : W, s, e};
     c->buckets.push_back(b);
     c->bucket_part_off.push_back(c->n_lm_parts);
