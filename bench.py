@@ -484,37 +484,66 @@ def bench_orb(args, world):
         dist.destroy_process_group()
 
 
+class CommInitFailed(SystemExit):
+    """Every rank leaves with this status when the RCCL communicator cannot be
+    built: a multi-GPU line is an RCCL measurement or no line at all."""
+    STATUS = 3
+
+
+def connect_rccl(ctx, rank, world, dist, make_uid):
+    """Build the context's RCCL communicator over `world` ranks (rank 0 makes
+    the id, the gloo group broadcasts it). Collective: every rank learns
+    whether every other one succeeded and whether the communicator reports
+    `world` ranks (ncclCommCount). On any failure every rank exits with
+    CommInitFailed.STATUS -- there is no silent fallback to the host transport.
+    Returns the description recorded in the line's config.comm and the rank
+    count the communicator reports."""
+    import torch
+    from sqrtlm._lib import SqlmError
+    uid = make_uid() if rank == 0 else b""
+    t = torch.tensor([len(uid)], dtype=torch.int64)
+    dist.broadcast(t, 0)
+    if rank != 0:
+        uid = bytes(int(t[0]))
+    tu = torch.tensor(list(uid), dtype=torch.uint8)
+    dist.broadcast(tu, 0)
+    ok = torch.tensor([1], dtype=torch.int32)
+    why = ""
+    try:
+        ctx.set_comm(bytes(tu.tolist()), rank, world)
+        info = ctx.comm_info()
+        if info["transport"] != "rccl" or info["nranks"] != world or info["rank"] != rank:
+            why = f"communicator reports {info}, expected rccl rank {rank} of {world}"
+            ok[0] = 0
+    except SqlmError as err:
+        why = str(err)
+        ok[0] = 0
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok[0]) == 0:
+        print(f"bench.py rank {rank}: RCCL communicator init failed on "
+              f"{'this rank' if why else 'another rank'}{': ' + why if why else ''}; no line is written",
+              file=sys.stderr)
+        raise CommInitFailed(CommInitFailed.STATUS)
+    return f"rccl ({info['nranks']} ranks reported by ncclCommCount)", info["nranks"]
+
+
 def run_ba(args, world, rank, local_rank, dist, config, cpu_iters=10, cpu_min_s=10.0):
     """One BA workload (config 4, the loop-closed config 4, or config 2) on this
     rank's context; returns the bench dict on rank 0 (None elsewhere)."""
-    from sqrtlm.optimizer import Context, comm_unique_id
+    from sqrtlm.optimizer import Context
     from sqrtlm.shard import shard
     prob, desc = make_workload(config, args.scale)
     local = shard(prob, rank, world)
     # SQLM_BENCH_ONE_GPU=1 puts every rank on GPU 0 (1-GPU rehearsal of the RCCL transport)
     one_gpu = args.comm == "host" or os.environ.get("SQLM_BENCH_ONE_GPU") == "1"
     ctx = Context(0 if one_gpu else local_rank)
-    comm_used = "none" if world == 1 else args.comm
+    comm_used, comm_ranks = "none", 1
     if world > 1 and args.comm == "rccl":
-        import torch
-        from sqrtlm._lib import lib, SqlmError
-        uid = comm_unique_id() if rank == 0 else bytes(lib().sqlm_comm_id_size())
-        t = torch.tensor(list(uid), dtype=torch.uint8)
-        dist.broadcast(t, 0)
-        ok = torch.tensor([1], dtype=torch.int32)
-        try:
-            ctx.set_comm(bytes(t.tolist()), rank, world)
-        except SqlmError as err:  # every rank switches together: the exchange is collective
-            print(f"rank {rank}: RCCL communicator failed ({err}); using the host transport", file=sys.stderr)
-            ok[0] = 0
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok[0]) == 0:
-            ctx.close()
-            ctx = Context(0 if one_gpu else local_rank)
-            ctx.set_host_comm(rank, world, _gloo_allreduce, _gloo_p2p)
-            comm_used = "host (RCCL communicator init failed)"
+        from sqrtlm.optimizer import comm_unique_id
+        comm_used, comm_ranks = connect_rccl(ctx, rank, world, dist, comm_unique_id)
     elif world > 1:
         ctx.set_host_comm(rank, world, _gloo_allreduce, _gloo_p2p)
+        comm_used, comm_ranks = "host (gloo, %d ranks on GPU 0)" % world, world
     ctx.set_problem(local)
     # the timed run without the per-phase HIP events (they cost ≈2 %), then the
     # same run from the same initial state with them, for the phase breakdown
@@ -582,7 +611,7 @@ def run_ba(args, world, rank, local_rank, dist, config, cpu_iters=10, cpu_min_s=
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (repo generator, SplitMix64 seed; inputs rounded through float32 like the reference)",
-            "config": dict(desc, parallelism=f"landmark-shard x{world}", comm=comm_used),
+            "config": dict(desc, parallelism=f"landmark-shard x{world}", comm=comm_used, comm_ranks=comm_ranks),
             "trials_per_step": st["trials"] / max(1, st["iterations"]),
             "final_rmse_px": None,
             "chi2_first": st["trace_chi2"][0] if st["trace_chi2"] else None,

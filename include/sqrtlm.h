@@ -189,6 +189,15 @@ void sqlm_pose_to_Tcw_f32(const double q[4], const double t[3], float T[16]);
 int sqlm_comm_id_size(void);
 int sqlm_comm_get_unique_id(char *id_out);
 int sqlm_ctx_set_comm(sqlm_ctx *ctx, const char *unique_id, int rank, int nranks);
+/* What the context's exchange actually runs on: *transport = SQLM_COMM_NONE,
+ * _RCCL, _RCCL_SELFLOOP or _HOST; for RCCL *rank / *nranks are the ones the
+ * communicator itself reports (ncclCommUserRank / ncclCommCount), otherwise
+ * the ones the caller set. No reference counterpart (bench / test hook). */
+#define SQLM_COMM_NONE 0
+#define SQLM_COMM_RCCL 1
+#define SQLM_COMM_RCCL_SELFLOOP 2
+#define SQLM_COMM_HOST 3
+int sqlm_ctx_comm_info(const sqlm_ctx *ctx, int *transport, int *rank, int *nranks);
 /* RCCL transport checks on ONE GPU (no reference counterpart; test hooks).
  * sqlm_ctx_set_comm_selfloop: a one-rank RCCL communicator on which the
  * context takes the sharded code path (every all-reduce, the rank-0 gather and

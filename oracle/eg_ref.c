@@ -489,7 +489,7 @@ int orc_eg_optimize(orc_eg_graph *g, int iterations, double user_lambda, const v
       for (int i = 0; i < w.nP; ++i) sim3_oplus(g->Siw + 8 * w.pose_of[i], w.x + 7 * i, g->fix_scale);
       eg_errors(&w);
       tempChi = eg_chi2(&w);
-      if (!ok || isnan(tempChi)) tempChi = DBL_MAX;  // NaN: a failed trial (g2o_ref.c)
+      if (!ok || (isnan(tempChi) && isfinite(currentChi))) tempChi = DBL_MAX;  // NaN: a failed trial (g2o_ref.c)
       rho = (currentChi - tempChi);
       double scale = 0.;
       for (int j = 0; j < 7 * w.nP; ++j) scale += w.x[j] * (lambda * w.x[j] + w.b[j]);

@@ -879,7 +879,8 @@ int orc_optimize(orc_graph *g, int level, int iterations, double user_lambda, co
       // a NaN chi2 (our sin / cos past 2^20 pi / 2, where glibc's stay finite and
       // the reference's chi2 is astronomically large) is a failed trial, as in
       // the library's lm_decide
-      if (!ok2 || isnan(tempChi)) tempChi = DBL_MAX;
+      // (only when currentChi is finite: NaN input keeps g2o's rho = NaN)
+      if (!ok2 || (isnan(tempChi) && isfinite(currentChi))) tempChi = DBL_MAX;
       rho = (currentChi - tempChi);
       double scale = compute_scale(&w, lambda);
       scale += 1e-3;

@@ -6,7 +6,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/pmc
-ARGS="--no-cpu-baseline --steps 5 --warmup 1 $*"
+ARGS="--no-cpu-baseline --no-extras --steps 5 --warmup 1 $*"
 run() {  # pass counters...
   local pass=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --output-format csv -d gpurun_out/pmc/$pass -o run \

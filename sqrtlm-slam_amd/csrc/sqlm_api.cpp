@@ -296,6 +296,7 @@ struct SmallUploads {
     host.resize(off + ((std::max<size_t>(bytes, 1) + 255) & ~size_t(255)));
     if (bytes) std::memcpy(host.data() + off, v.data(), bytes);
     dst.push_back({off, reinterpret_cast<void **>(out)});
+    *out = nullptr;  // set when the arena is copied: a kernel launched before that reads null, not stale memory
   }
 };
 
@@ -2577,6 +2578,11 @@ int sqlm_ctx_set_comm(sqlm_ctx *c, const char *id, int rank, int nranks) {
   if (!c || !id || rank < 0 || nranks < 1 || rank >= nranks) return SQLM_ERR_INVALID_ARG;
   if (hipSetDevice(c->device) != hipSuccess) return SQLM_ERR_HIP;
   return comm_init(c->comm, id, rank, nranks);
+}
+
+int sqlm_ctx_comm_info(const sqlm_ctx *c, int *transport, int *rank, int *nranks) {
+  if (!c || !transport || !rank || !nranks) return SQLM_ERR_INVALID_ARG;
+  return comm_info(c->comm, transport, rank, nranks);
 }
 
 int sqlm_ctx_set_comm_selfloop(sqlm_ctx *c, const char *id) {

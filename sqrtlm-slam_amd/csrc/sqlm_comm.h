@@ -91,6 +91,22 @@ inline int comm_init_selfloop(Comm &c, const char *idbytes) {
   return 0;
 }
 
+// transport, rank and rank count as the communicator reports them
+inline int comm_info(const Comm &c, int *transport, int *rank, int *nranks) {
+  if (c.comm) {
+    int n = 0, r = 0;
+    if (ncclCommCount(c.comm, &n) != ncclSuccess || ncclCommUserRank(c.comm, &r) != ncclSuccess) return SQLM_ERR_COMM;
+    *transport = c.selfloop ? SQLM_COMM_RCCL_SELFLOOP : SQLM_COMM_RCCL;
+    *rank = r;
+    *nranks = n;
+    return SQLM_OK;
+  }
+  *transport = c.host_fn ? SQLM_COMM_HOST : SQLM_COMM_NONE;
+  *rank = c.rank;
+  *nranks = c.nranks;
+  return SQLM_OK;
+}
+
 inline int comm_init_host(Comm &c, int rank, int nranks, sqlm_allreduce_fn fn, void *user) {
   const sqlm_p2p_fn p2p = c.host_p2p;  // survives a re-init of the collective
   void *p2p_user = c.host_p2p_user;

@@ -709,7 +709,8 @@ int EGSolver::optimize(int iterations, double user_lambda, const volatile uint8_
         std::fprintf(stderr, "eg it %d trial %d lambda %.6g chi_cur %.17g chi_new %.17g scale %.6g ok %d\n", it,
                      qmax, lambda, currentChi, h_scal[1], h_scal[2], (int)ok);
       // a NaN chi2 is a failed trial (lm_decide, sqlm_internal.h)
-      double tempChi = ok && !std::isnan(h_scal[1]) ? h_scal[1] : std::numeric_limits<double>::max();
+      double tempChi = ok && !(std::isnan(h_scal[1]) && std::isfinite(currentChi)) ? h_scal[1]
+                                                                                   : std::numeric_limits<double>::max();
       rho = (currentChi - tempChi);
       double scale = ok ? h_scal[2] : 0.0;
       scale += 1e-3;

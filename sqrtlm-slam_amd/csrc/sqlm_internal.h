@@ -49,8 +49,11 @@ inline bool lm_decide(LMCtl &c, double chi_cur, double chi_new, double scale, bo
   // a NaN trial chi2 is a failed trial: our sin / cos (include/sqlm_libm.h)
   // return NaN past fdlibm's medium-range reduction (a rotation step of
   // > 2^20 pi / 2 rad), where glibc's stay finite and the reference's chi2 is
-  // astronomically large -- rejected with a larger lambda either way
-  const double tempChi = ok && !std::isnan(chi_new) ? chi_new : DBL_MAX;
+  // astronomically large -- rejected with a larger lambda either way. Only
+  // when the current chi2 is finite: NaN input (a NaN measurement or state)
+  // keeps g2o's arithmetic, rho = NaN, and the iteration ends after this one
+  // trial (levenberg.cpp:124-160; tests/test_gpu_parity.py::test_nan_measurement)
+  const double tempChi = ok && !(std::isnan(chi_new) && std::isfinite(c.currentChi)) ? chi_new : DBL_MAX;
   double rho = c.currentChi - tempChi;
   const double scl = (ok ? scale : 0.0) + 1e-3;
   rho /= scl;

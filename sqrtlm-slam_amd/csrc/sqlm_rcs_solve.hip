@@ -900,14 +900,24 @@ __global__ __launch_bounds__(512) void k_cr_back_u(CRView v, int h) {
 // reset); the consumer polls that word with sc1 loads and s_sleep and reads x
 // with sc1 loads only. Bounded: a wait that gives up fails the solve
 // (cr_fail -> SQLM_ERR_HIP), and every wave still reaches the end.
+// Assumption: a workgroup is dispatched no earlier than every lower-numbered
+// workgroup of the same launch (the command processor's in-order dispatch on
+// gfx950; HIP does not promise it). If it ever fails, a waiting workgroup
+// that holds the CU a producer needs times out and the solve fails loudly
+// instead of hanging. -DSQLM_SPIN_FORCE_TIMEOUT (tests) makes this wait, like
+// aug::spin / spin_to, report a timeout after it has completed, so
+// tests/test_gpu_fail_loud.py runs this hand-off's give-up path too.
 __device__ __forceinline__ bool wait_x(const CRView &v, int J) {
-  if (J == 0) return true;  // the top superblock: solved by an earlier launch
+  bool ok = J == 0;  // the top superblock: solved by an earlier launch
   const int *f = v.done + J;
-  for (int it = 0; it < aug::kSpinLimit; ++it) {
-    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v.epoch) return true;
-    __builtin_amdgcn_s_sleep(2);
+  for (int it = 0; !ok && it < aug::kSpinLimit; ++it) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == v.epoch) ok = true;
+    else __builtin_amdgcn_s_sleep(2);
   }
-  return false;
+#ifdef SQLM_SPIN_FORCE_TIMEOUT
+  ok = false;
+#endif
+  return ok;
 }
 __device__ __forceinline__ double ld_x(const double *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

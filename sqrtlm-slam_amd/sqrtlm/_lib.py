@@ -28,7 +28,7 @@ EXPORTS = [
     "sqlm_local_ba", "sqlm_global_ba", "sqlm_get_poses", "sqlm_get_points", "sqlm_get_edge_chi2",
     "sqlm_get_edge_depth_positive", "sqlm_get_edge_level", "sqlm_pose_from_Tcw_f32", "sqlm_pose_to_Tcw_f32",
     "sqlm_comm_id_size", "sqlm_comm_get_unique_id", "sqlm_ctx_set_comm", "sqlm_ctx_set_host_comm",
-    "sqlm_ctx_set_host_p2p", "sqlm_ctx_set_comm_selfloop", "sqlm_comm_selftest",
+    "sqlm_ctx_set_host_p2p", "sqlm_ctx_set_comm_selfloop", "sqlm_comm_selftest", "sqlm_ctx_comm_info",
     "sqlm_bench_iterations",
     "sqlm_kernel_timer_name", "sqlm_set_stereo",
     "sqlm_eg_set_problem", "sqlm_eg_optimize", "sqlm_eg_get_poses", "sqlm_eg_get_edge_chi2",

@@ -128,6 +128,14 @@ class Context:
         buf = C.create_string_buffer(unique_id, len(unique_id))
         check(lib().sqlm_ctx_set_comm(self._h, buf, int(rank), int(nranks)), "sqlm_ctx_set_comm")
 
+    def comm_info(self) -> dict:
+        """The transport the exchange runs on and the rank / rank count as
+        the communicator reports them (RCCL: ncclCommUserRank / ncclCommCount)."""
+        tr, r, n = C.c_int(), C.c_int(), C.c_int()
+        check(lib().sqlm_ctx_comm_info(self._h, C.byref(tr), C.byref(r), C.byref(n)), "sqlm_ctx_comm_info")
+        names = {0: "none", 1: "rccl", 2: "rccl-selfloop", 3: "host"}
+        return {"transport": names.get(tr.value, str(tr.value)), "rank": r.value, "nranks": n.value}
+
     def set_comm_selfloop(self, unique_id: bytes) -> None:
         """A one-rank RCCL communicator: the sharded code path with every
         exchange through real RCCL on one GPU (sqlm_ctx_set_comm_selfloop)."""

@@ -61,3 +61,65 @@ def test_spawn_ranks_failure_ends_the_job():
     assert bench.spawn_ranks(3, [sys.executable, "-c", code]) != 0
     assert __import__("time").time() - t0 < 30
 
+
+
+def _rccl_rank(rank, world, port, mode, q):
+    """One gloo rank of connect_rccl with a stand-in context whose
+    set_comm / comm_info behave as `mode` says."""
+    import torch.distributed as dist
+    from sqrtlm._lib import SqlmError
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class FakeCtx:
+        def set_comm(self, uid, r, n):
+            self.uid = uid
+            if mode == "fail" and r == 1:
+                raise SqlmError(-9, "sqlm_ctx_set_comm")
+
+        def comm_info(self):
+            n = world - 1 if mode == "short" else world
+            return {"transport": "rccl", "rank": rank, "nranks": n}
+
+    ctx = FakeCtx()
+    try:
+        res = bench.connect_rccl(ctx, rank, world, dist, lambda: bytes(range(7, 135)))
+        q.put((rank, "ok", res, ctx.uid == bytes(range(7, 135))))
+    except SystemExit as e:
+        q.put((rank, "exit", e.code, None))
+    dist.destroy_process_group()
+
+
+def _run_rccl(mode, world=2):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench.free_port()
+    ps = [ctx.Process(target=_rccl_rank, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    return out
+
+
+def test_rccl_init_failure_exits_nonzero_on_every_rank():
+    """A communicator that fails on one rank ends EVERY rank with a non-zero
+    status (no silent switch to the host transport, bench.py writes no line)."""
+    out = _run_rccl("fail")
+    assert [o[1] for o in out] == ["exit", "exit"], out
+    assert {o[2] for o in out} == {bench.CommInitFailed.STATUS} and bench.CommInitFailed.STATUS != 0
+
+
+def test_rccl_rank_count_mismatch_exits_nonzero():
+    """ncclCommCount disagreeing with WORLD_SIZE is a failure too."""
+    out = _run_rccl("short")
+    assert [o[1] for o in out] == ["exit", "exit"], out
+
+
+def test_rccl_success_reports_communicator_ranks():
+    out = _run_rccl("ok", world=3)
+    assert [o[1] for o in out] == ["ok"] * 3, out
+    for _r, _s, (desc, n), same_uid in out:
+        assert n == 3 and "3 ranks reported by ncclCommCount" in desc and same_uid

@@ -245,3 +245,21 @@ def test_double_inputs_path(gpu_ctx, oracle, what):
     gpu_ctx.set_problem(synth.make_problem(14, 400, pair_window=4, n_fixed=3, seed=5, robust=True))
     gpu_ctx.optimize(0, 2)
     assert gpu_ctx.exec_info()["obs_f32"] is True
+
+
+@pytest.mark.parametrize("robust", [False, True])
+def test_nan_measurement(gpu_ctx, oracle, robust):
+    """A NaN measurement: like g2o (and the oracle) every iteration ends after
+    one rejected trial and the state is left as it was (the
+    NaN-trial rule of lm_decide applies only to a finite current chi2)."""
+    prob = synth.make_problem(10, 200, pair_window=3, n_fixed=2, seed=3, robust=robust)
+    prob.obs_uv[5, 0] = np.nan
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(0, 5)
+    gpu_ctx.set_problem(prob)
+    n, st = gpu_ctx.optimize(0, 5)
+    assert n == nr == 5 and st["trials"] == sr["trials"] == 5
+    assert list(st["trace_trials"][:5]) == [1] * 5
+    q, t = gpu_ctx.poses()
+    np.testing.assert_array_equal(q, prob.pose_q)
+    np.testing.assert_array_equal(gpu_ctx.points(), prob.pt)

@@ -201,3 +201,23 @@ def test_openmp_variant_bit_identical(gen):
     assert na == nb and sa == sb
     for k in ("pose_q", "pose_t", "pt", "obs_err"):
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k))
+
+
+def test_nan_measurement_ends_each_iteration_after_one_trial(oracle):
+    """NaN input keeps g2o's arithmetic (levenberg.cpp:124-160): chi2 is NaN,
+    so rho is NaN, the `rho < 0` retry loop exits after one trial, the step
+    is rejected (lambda grows) and the state is left as it was. The NaN-trial
+    substitution of lm_decide (a failed trial) applies only when the current
+    chi2 is finite (sqlm_internal.h, g2o_ref.c)."""
+    for robust in (False, True):
+        prob = synth.make_problem(10, 200, pair_window=3, n_fixed=2, seed=3, robust=robust)
+        prob.obs_uv[5, 0] = np.nan
+        g = oracle.OracleGraph(prob)
+        n, st = g.optimize(0, 5)
+        assert n == 5 and st["trials"] == 5 and st["trace_trials"][:5] == [1] * 5
+        assert all(np.isnan(c) for c in st["trace_chi2"][:5])
+        lam = st["trace_lambda"][:5]
+        # every trial rejected: lambda *= ni, ni *= 2 (never reset to 2)
+        assert [b / a for a, b in zip(lam, lam[1:])] == [4.0, 8.0, 16.0, 32.0]
+        np.testing.assert_array_equal(g.pose_q, prob.pose_q)
+        np.testing.assert_array_equal(g.pt, prob.pt)
