@@ -1,6 +1,8 @@
 """A/B: the same GBA on two library builds must give bitwise-equal results
 (a kernel change that keeps every summation order). usage:
-python scripts/ab_bits.py libsqrtlm_old.so [scale]"""
+python scripts/ab_bits.py libsqrtlm_old.so[:VAR=V...] [scale]
+(the A side may carry environment settings, e.g. libsqrtlm.so:SQLM_TILE_PROD=0
+compares the in-tree library against itself with that switch)"""
 import os
 import subprocess
 import sys
@@ -10,10 +12,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run(lib, scale, out):
+def run(spec, scale, out):
+    lib, *var = spec.split(":") if spec else ("",)
     env = dict(os.environ, SQLM_LIB_PATH=os.path.join(ROOT, "sqrtlm-slam_amd", "sqrtlm", lib) if lib else "")
     if not lib:
         env.pop("SQLM_LIB_PATH")
+    for v in var:
+        k, _, x = v.partition("=")
+        env[k] = x
     code = f"""
 import sys; sys.path.insert(0, {os.path.join(ROOT, 'sqrtlm-slam_amd')!r})
 import numpy as np

@@ -1442,6 +1442,10 @@ int prepare(sqlm_ctx *c, int level) {
   std::copy(tp.cls_cnt, tp.cls_cnt + kTileNtMax + 1, d.tile_cls_cnt);
   d.tile_dups = tp.dups ? 1 : 0;
   {
+    const char *tw = std::getenv("SQLM_TILE_PROD");  // read per setup: tests switch it
+    d.tile_prod = tw && std::atoi(tw) == 0 ? 0 : 1;
+  }
+  {
     int mk = 0;
     for (int sl = 0; sl < nL; ++sl) mk = std::max(mk, lm_begin[sl + 1] - lm_begin[sl]);
     d.tile_maxk = mk;

@@ -202,6 +202,7 @@ struct DevProblem {
   int *long_s = nullptr, *long_g = nullptr;
   int tile_dups = 0;                        // some landmark observed twice by one camera
   int tile_maxk = 0;                        // longest track (staging fast path needs <= kTileFastK = 64)
+  int tile_prod = 1;                        // mono tiles: producer / consumer k_rcs_tile_p (SQLM_TILE_PROD=0: k_rcs_tile)
   // block-tridiagonal cyclic reduction workspace (sqlm_rcs_solve.hip)
   double *cr_D = nullptr, *cr_E = nullptr;  // [p][n][n]
   double *cr_L = nullptr;                   // [p][n][n] Linv_I of the factored superblocks

@@ -999,6 +999,50 @@ __device__ __forceinline__ void tile_mfma_wave(int wave, d4v *acc, const double 
   tile_mfma<NT, P>(acc, Y, tmin, tmax, nks, r16, k4);
 }
 
+// Y block of one mono observation into rows Y[0..2] (row stride ld) at
+// column col: Y = R'^-T P with P = jl^T jp (types_six_dof_expmap.cpp:103-139)
+// factored as P = [-B' [X_c]x | B'], B' = R^T A, A = s^2 J_pi^T J_pi (five
+// distinct entries) -- ~45 % fewer FP64 operations than forming jl, jp and
+// their 18 products. pr: the camera's R t fx fy, xl: the landmark, r: R'^-1
+// (upper: r0 r1 r2 / r3 r4 / r5), ps: sqrt(rho' info).
+__device__ __forceinline__ void stage_mono_y(const double *pr, const double *xl, const double *r, double ps,
+                                             double *Y, int ld, int col) {
+  MonoEval m;
+  m.x = pr[0] * xl[0] + pr[1] * xl[1] + pr[2] * xl[2] + pr[9];
+  m.y = pr[3] * xl[0] + pr[4] * xl[1] + pr[5] * xl[2] + pr[10];
+  m.z = pr[6] * xl[0] + pr[7] * xl[1] + pr[8] * xl[2] + pr[11];
+  const double iz = 1.0 / m.z, xz = m.x * iz, yz = m.y * iz, fx = pr[12], fy = pr[13];
+  const double t00 = -iz * fx, t02 = (xz * iz) * fx, t11 = -iz * fy, t12 = (yz * iz) * fy;
+  const double s2 = ps * ps;
+  const double A00 = s2 * (t00 * t00), A02 = s2 * (t00 * t02), A11 = s2 * (t11 * t11),
+               A12 = s2 * (t11 * t12), A22 = s2 * (t02 * t02 + t12 * t12);
+  double Q[3][3];  // R^T A
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    Q[i][0] = pr[i] * A00 + pr[6 + i] * A02;
+    Q[i][1] = pr[3 + i] * A11 + pr[6 + i] * A12;
+    Q[i][2] = pr[i] * A02 + pr[3 + i] * A12 + pr[6 + i] * A22;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {  // B = R'^-T Q
+    const double b0 = r[0] * Q[0][j], b1 = r[1] * Q[0][j] + r[3] * Q[1][j],
+                 b2 = r[2] * Q[0][j] + r[4] * Q[1][j] + r[5] * Q[2][j];
+    Q[0][j] = b0;
+    Q[1][j] = b1;
+    Q[2][j] = b2;
+  }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    double *yr = Y + (size_t)q * ld + col;
+    yr[0] = Q[q][2] * m.y - Q[q][1] * m.z;
+    yr[1] = Q[q][0] * m.z - Q[q][2] * m.x;
+    yr[2] = Q[q][1] * m.x - Q[q][0] * m.y;
+    yr[3] = Q[q][0];
+    yr[4] = Q[q][1];
+    yr[5] = Q[q][2];
+  }
+}
+
 // occupancy the mono kernel of width NT is compiled for (its accumulators and
 // LDS shrink with NT, so the narrower classes fit more workgroups per CU)
 #ifndef SQLM_TILE_OCC_NARROW
@@ -1249,6 +1293,237 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_t
   if (gcol >= 0 && gcol < ncol) go[gcol] = gacc;
 }
 
+// ---- producer / consumer RCS tiles (mono, no repeated cameras) ----
+// k_rcs_tile runs every batch in two barrier-separated phases that all four
+// waves take part in: wave 0 stages the batch while waves 1-3 clear, then
+// every wave runs its quarter of the MFMAs. The phase profile
+// (scripts/tile_prof.py) puts wave 0 at 31 % staging, 32 % MFMA and 20 %
+// parked at the two barriers. Here wave 0 only produces: while waves 1-3 run
+// batch b's MFMAs (tiles q with q % 3 == wave - 1) and gradient columns from
+// one LDS buffer, wave 0 clears the entries it staged two batches ago in the
+// other buffer and stages batch b + 1 there (two observations per lane, so a
+// batch of up to 128 observations is one pass, and the two chains give the
+// lone wave some ILP); ONE barrier per batch hands the buffers over. Every
+// accumulator tile sums the same products in the same order as k_rcs_tile
+// (only its owner wave changes) and the gradient code is the same: the
+// partials are bitwise identical to k_rcs_tile's.
+constexpr int kTileCons = kTileWaves - 1;  // consumer waves
+template <int NT, int P, int NC>
+__device__ __forceinline__ void tile_mfma_cons(d4v *acc, const double (*Y)[NC], int tmin, int tmax, int nks, int r16,
+                                               int k4) {
+  double op[NT][kTileKS];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int ks = 0; ks < kTileKS; ++ks) op[t][ks] = Y[4 * ks + k4][t * 16 + r16];
+  int q = 0;
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti) {
+#pragma unroll
+    for (int tj = ti; tj < NT; ++tj, ++q) {
+      if (q % kTileCons == P && ti >= tmin && tj <= tmax) {
+#pragma unroll
+        for (int ks = 0; ks < kTileKS; ++ks)
+          if (ks < nks)
+            acc[q / kTileCons] =
+                __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti][ks], op[tj][ks], acc[q / kTileCons], 0, 0, 0);
+      }
+    }
+  }
+}
+
+// observations a producer lane stages per batch (lane, lane + 64): batches of
+// up to kProdObs observations take the producer path
+constexpr int kProdPer = 2, kProdObs = 64 * kProdPer;
+
+// Consumer wave P (wave P + 1) of k_rcs_tile_p: one instantiation per wave,
+// so its accumulator tiles (q % 3 == P) are compile-time registers that live
+// in this branch only. After each batch's MFMAs and gradient column it joins
+// the batch barrier; at the end it writes its tiles of the partial.
+template <int NT, int P, int NC>
+__device__ __forceinline__ void tile_consumer(const DevProblem &d, int t, int cp, int ntl, int nbatch,
+                                              const double (*Ys)[kTileRows][NC], const double (*Lw)[3],
+                                              const int2 *Bs, int tid) {
+  constexpr int NQ = NT * (NT + 1) / 2, NQW = (NQ + kTileCons - 1) / kTileCons, BL = kTileBL;
+  const int lane = tid & 63, r16 = lane & 15, k4 = lane >> 4, gcol = tid - 64;
+  const int ncol = 6 * cp, nt = (ncol + 15) >> 4;
+  d4v acc[NQW];
+#pragma unroll
+  for (int q = 0; q < NQW; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
+  double gacc = 0.0;
+  lds_barrier();  // batch 0 staged
+  for (int bt = 0; bt < nbatch; ++bt) {
+    const int lb = BL * bt, nl = min(BL, ntl - lb);
+    const double(*Y)[NC] = Ys[bt & 1];
+    const int2 bsp = Bs[bt];
+    const int cmin = __builtin_amdgcn_readfirstlane(bsp.x), cmax = __builtin_amdgcn_readfirstlane(bsp.y);
+    if (cmax > 0) {
+      const int tmin = cmin >> 4, tmax = (cmax - 1) >> 4;
+      tile_mfma_cons<NT, P>(acc, Y, tmin, tmax, (3 * nl + 3) >> 2, r16, k4);
+      if (gcol >= cmin && gcol < cmax) {
+        double gs = 0.0;
+        for (int li = 0; li < nl; ++li)
+          gs += Y[3 * li][gcol] * Lw[lb + li][0] + Y[3 * li + 1][gcol] * Lw[lb + li][1] +
+                Y[3 * li + 2][gcol] * Lw[lb + li][2];
+        gacc -= gs;
+      }
+    }
+    lds_barrier();  // batch bt + 1 staged, batch bt's buffer free
+  }
+  // -G_t as the tile's partial, block-major (as k_rcs_tile)
+  double *out = d.part + d.tile_part_ptr[t];
+  const int n6 = 6 * cp;
+  int q = 0;
+#pragma unroll
+  for (int ti = 0; ti < NT; ++ti)
+#pragma unroll
+    for (int tj = ti; tj < NT; ++tj, ++q) {
+      if (q % kTileCons == P && tj < nt) {
+        const int C = tj * 16 + r16, w = C / 6, c = C - 6 * w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int R = ti * 16 + k4 + 4 * j, u = R / 6, r = R - 6 * u;
+          if (R < n6 && C < n6 && u <= w) {
+            double *blk = out + 36 * tile_blk(u, w, cp);
+            const double v = -acc[q / kTileCons][j];
+            blk[6 * r + c] = v;
+            if (u == w && ti < tj) blk[6 * c + r] = v;
+          }
+        }
+      }
+    }
+  double *go = d.gpart + d.tile_gpart_ptr[t];
+  if (gcol >= 0 && gcol < ncol) go[gcol] = gacc;
+}
+
+// waves per SIMD k_rcs_tile_p is compiled for: the consumer waves' registers
+// (NT = 8: 155 VGPRs, 6: 102) without spills
+template <int NT>
+constexpr int tile_p_occ() {
+  return NT <= 3 ? 5 : NT <= 6 ? 4 : 3;
+}
+template <int NT>
+__global__ __launch_bounds__(kTileThreads, tile_p_occ<NT>()) void k_rcs_tile_p(DevProblem d, double lambda, int cls_off) {
+  constexpr int TH = kTileThreads, NC = NT * 16, BL = kTileBL;
+  __shared__ double Ys[2][kTileRows][NC];
+  __shared__ int Lb[kTileMaxLm + 1];
+  __shared__ double Lw[kTileMaxLm][3];
+  __shared__ double Lr[kTileMaxLm][6];
+  __shared__ double Lx[kTileMaxLm][3];
+  __shared__ double Lc[kTileHardCams][16];
+  __shared__ int2 Bs[(kTileMaxLm + kTileBL - 1) / kTileBL];
+  const int t = d.tile_order[cls_off + blockIdx.x], tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform: the role branches are scalar
+  const int cp = d.tile_cam_ptr[t + 1] - d.tile_cam_ptr[t];
+  static_assert(NT * 16 <= kTileThreads - 64, "one gradient column per thread of waves 1..");
+  static_assert(kTileHardCams <= 32, "the producer's staged-position code holds a camera in 5 bits");
+  for (int k = tid; k < 2 * kTileRows * NC; k += TH) (&Ys[0][0][0])[k] = 0.0;
+  const int l0 = d.tile_lm_ptr[t], l1 = d.tile_lm_ptr[t + 1], ntl = l1 - l0;
+  const int nbatch = (ntl + BL - 1) / BL;
+  for (int k = tid; k <= ntl; k += TH) Lb[k] = d.lm_begin[l0 + k];
+  for (int li = tid; li < ntl; li += TH) damp_factor(d.lm_R + 8 * (l0 + li), d.lm_b + 4 * (l0 + li), lambda, Lr[li], Lw[li]);
+  for (int k = tid; k < 3 * ntl; k += TH) {
+    const int li = k / 3, c = k - 3 * li;
+    Lx[li][c] = d.X[0][4 * (l0 + li) + c];
+  }
+  {
+    const int cb = d.tile_cam_ptr[t];
+    for (int k = tid; k < 16 * cp; k += TH) {
+      const int u = k >> 4, c = k & 15;
+      Lc[u][c] = d.pose_rt[0][16 * d.hidx_pose[d.tile_cams[cb + u]] + c];
+    }
+  }
+  for (int bt = tid; bt < nbatch; bt += TH) {  // batch spans from the landmarks' camera ranges
+    int cmin = 1 << 30, cmax = -1;
+    for (int li = BL * bt; li < min(BL * bt + BL, ntl); ++li) {
+      const int2 ur = d.lm_urange[l0 + li];
+      if (ur.x >= 0) { cmin = min(cmin, 6 * ur.x); cmax = max(cmax, 6 * ur.y + 6); }
+    }
+    Bs[bt] = int2{cmin, cmax};
+  }
+  if (d.cr_direct) {  // this tile's share of clearing the CR superblocks that k_rcs_reduce fills next
+    const int64_t tot = (int64_t)d.cr_p * d.cr_n * d.cr_n;
+    const int64_t per = ((tot + d.n_tiles - 1) / d.n_tiles + 1) & ~(int64_t)1;
+    const int64_t a0 = (int64_t)t * per, a1 = min(tot, a0 + per);
+    for (int64_t k = a0 + 2 * tid; k < a1; k += 2 * TH) {
+      store2(d.cr_D + k, 0.0, 0.0);
+      store2(d.cr_E + k, 0.0, 0.0);
+    }
+  }
+  __syncthreads();
+  // Two role loops with the same number of barriers (nbatch + 1): between
+  // barriers b - 1 and b the producer stages batch b into buffer b & 1 while
+  // the consumers work on batch b - 1 in the other buffer. Each role keeps
+  // only its own state live (the accumulators exist in the consumer branch).
+  if (wave == 0) {
+    // the prefetched raw inputs of the next batch (two observations per lane),
+    // and where this lane staged in each buffer: 32 row + camera, -1: nothing
+    // (separate registers per buffer, selected by value: a runtime index into
+    // a register array would put it in scratch)
+    int pu0 = -1, pu1 = -1, pl0 = 0, pl1 = 0, w00 = -1, w01 = -1, w10 = -1, w11 = -1;
+    double ps0 = 0.0, ps1 = 0.0;
+    auto fetch_in = [&](int sb) {
+      const int lb = BL * sb, nl = min(BL, ntl - lb);
+      const int b0 = Lb[lb], bn = Lb[lb + nl];
+      const int e1 = nl > 1 ? Lb[lb + 1] : bn, e2 = nl > 2 ? Lb[lb + 2] : bn, e3 = nl > 3 ? Lb[lb + 3] : bn;
+      const int o0 = b0 + lane, o1 = o0 + 64;
+      pu0 = o0 < bn ? d.obs_local[o0] : -1;
+      pu1 = o1 < bn ? d.obs_local[o1] : -1;
+      ps0 = o0 < bn ? d.obs_s[o0] : 0.0;
+      ps1 = o1 < bn ? d.obs_s[o1] : 0.0;
+      pl0 = lb + (o0 >= e1) + (o0 >= e2) + (o0 >= e3);
+      pl1 = lb + (o1 >= e1) + (o1 >= e2) + (o1 >= e3);
+    };
+    if (nbatch > 0) fetch_in(0);
+    for (int sb = 0; sb <= nbatch; ++sb) {
+      if (sb < nbatch) {
+        const int buf = sb & 1, lb = BL * sb;
+        double(*Y)[NC] = Ys[buf];
+        // clear what this lane staged in this buffer two batches ago
+        const int c0 = buf ? w10 : w00, c1 = buf ? w11 : w01;
+        if (c0 >= 0) {
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; c += 2) store2(&Y[(c0 >> 5) + r][6 * (c0 & 31) + c], 0.0, 0.0);
+        }
+        if (c1 >= 0) {
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; c += 2) store2(&Y[(c1 >> 5) + r][6 * (c1 & 31) + c], 0.0, 0.0);
+        }
+        int n0 = -1, n1 = -1;
+        if (pu0 >= 0) {
+          const int row = 3 * (pl0 - lb);
+          stage_mono_y(Lc[pu0], Lx[pl0], Lr[pl0], ps0, &Y[row][0], NC, 6 * pu0);
+          n0 = 32 * row + pu0;  // (cp <= 24 cameras)
+        }
+        if (pu1 >= 0) {
+          const int row = 3 * (pl1 - lb);
+          stage_mono_y(Lc[pu1], Lx[pl1], Lr[pl1], ps1, &Y[row][0], NC, 6 * pu1);
+          n1 = 32 * row + pu1;
+        }
+        if (buf) {
+          w10 = n0;
+          w11 = n1;
+        } else {
+          w00 = n0;
+          w01 = n1;
+        }
+        if (sb + 1 < nbatch) fetch_in(sb + 1);  // in flight across the barrier (LDS-only)
+      }
+      lds_barrier();
+    }
+  } else if (wave == 1) {
+    tile_consumer<NT, 0>(d, t, cp, ntl, nbatch, Ys, Lw, Bs, tid);
+  } else if (wave == 2) {
+    tile_consumer<NT, 1>(d, t, cp, ntl, nbatch, Ys, Lw, Bs, tid);
+  } else {
+    tile_consumer<NT, 2>(d, t, cp, ntl, nbatch, Ys, Lw, Bs, tid);
+  }
+}
+
 // S block s = sum of its tile partials + H_pp + lambda I on the diagonal; g
 // row i likewise. Each contribution is one 36-double block of a tile's
 // block-major partial (tile_blk), or 6 doubles of its g partial, at a
@@ -1458,6 +1733,17 @@ __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double
   }
 }
 
+// the producer / consumer kernel for classes up to 8 tiles wide (the
+// 9-wide class keeps k_rcs_tile: 15 accumulator tiles per consumer wave would
+// not fit its 3 waves per SIMD)
+template <int NTT>
+void launch_tile_p(int cnt, hipStream_t S, const DevProblem &d, double lambda, int off) {
+  if constexpr (NTT <= 8)
+    hipLaunchKernelGGL((k_rcs_tile_p<NTT>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);
+  else
+    hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);
+}
+
 void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k, hipStream_t st,
                       const TileStreams *ts) {
   if (d.nP == 0) return;
@@ -1492,12 +1778,17 @@ void launch_rcs_tiles(const DevProblem &d, double lambda, int max_cp, int max_k,
       (void)hipEventRecord(ts->fork, st);
       TH_MARK;
     }
+    // mono tiles without repeated cameras whose batches fit the producer wave:
+    // the producer / consumer kernel
+    const bool prod_tiles = !d.has_stereo && !d.tile_dups && d.tile_maxk * kTileBL <= kProdObs && d.tile_prod;
 #define SQLM_TILE(NTT, S)                                                                                     \
   do {                                                                                                        \
     const int cnt = d.tile_cls_cnt[NTT], off = d.tile_cls_off[NTT];                                            \
     if (cnt > 0) {                                                                                            \
       if (d.has_stereo)                                                                                       \
         hipLaunchKernelGGL((k_rcs_tile<NTT, true>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);      \
+      else if (prod_tiles)                                                                                    \
+        launch_tile_p<NTT>(cnt, S, d, lambda, off);                                                           \
       else                                                                                                    \
         hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);     \
     }                                                                                                         \
