@@ -941,7 +941,16 @@ __device__ long long g_tile_prof[kTileProfTiles][kTileProfSlots];
     if (threadIdx.x == 0 && blockIdx.x < kTileProfTiles)                \
       for (int i_ = 0; i_ < kTileProfSlots; ++i_) g_tile_prof[blockIdx.x][i_] += tp_acc[i_]; \
   } while (0)
+// one role's stamps, stored by thread `who` (k_rcs_tile_p: producer lane 0, first consumer lane 0)
+#define TP_STORE_BY(who)                                                \
+  do {                                                                  \
+    if (threadIdx.x == (who) && blockIdx.x < kTileProfTiles)            \
+      for (int i_ = 0; i_ < kTileProfSlots; ++i_) g_tile_prof[blockIdx.x][i_] += tp_acc[i_]; \
+  } while (0)
 #else
+#define TP_STORE_BY(who) \
+  do {                   \
+  } while (0)
 #define TP_DECL
 #define TP(slot) \
   do {           \
@@ -1351,7 +1360,9 @@ __device__ __forceinline__ void tile_consumer(const DevProblem &d, int t, int cp
 #pragma unroll
   for (int q = 0; q < NQW; ++q) acc[q] = d4v{0.0, 0.0, 0.0, 0.0};
   double gacc = 0.0;
+  TP_DECL
   lds_barrier();  // batch 0 staged
+  TP(3);
   for (int bt = 0; bt < nbatch; ++bt) {
     const int lb = BL * bt, nl = min(BL, ntl - lb);
     const double(*Y)[NC] = Ys[bt & 1];
@@ -1368,8 +1379,11 @@ __device__ __forceinline__ void tile_consumer(const DevProblem &d, int t, int cp
         gacc -= gs;
       }
     }
+    TP(2);  // consumer: MFMAs + gradient
     lds_barrier();  // batch bt + 1 staged, batch bt's buffer free
+    TP(3);  // consumer: waiting for the producer
   }
+  if (P == 0) TP_STORE_BY(64);
   // -G_t as the tile's partial, block-major (as k_rcs_tile)
   double *out = d.part + d.tile_part_ptr[t];
   const int n6 = 6 * cp;
@@ -1400,7 +1414,7 @@ __device__ __forceinline__ void tile_consumer(const DevProblem &d, int t, int cp
 // (NT = 8: 155 VGPRs, 6: 102) without spills
 template <int NT>
 constexpr int tile_p_occ() {
-  return NT <= 3 ? 5 : NT <= 6 ? 4 : 3;
+  return NT <= 3 ? 5 : NT <= 6 ? 4 : NT <= 8 ? 3 : 2;
 }
 template <int NT>
 __global__ __launch_bounds__(kTileThreads, tile_p_occ<NT>()) void k_rcs_tile_p(DevProblem d, double lambda, int cls_off) {
@@ -1475,6 +1489,7 @@ __global__ __launch_bounds__(kTileThreads, tile_p_occ<NT>()) void k_rcs_tile_p(D
       pl1 = lb + (o1 >= e1) + (o1 >= e2) + (o1 >= e3);
     };
     if (nbatch > 0) fetch_in(0);
+    TP_DECL
     for (int sb = 0; sb <= nbatch; ++sb) {
       if (sb < nbatch) {
         const int buf = sb & 1, lb = BL * sb;
@@ -1513,8 +1528,11 @@ __global__ __launch_bounds__(kTileThreads, tile_p_occ<NT>()) void k_rcs_tile_p(D
         }
         if (sb + 1 < nbatch) fetch_in(sb + 1);  // in flight across the barrier (LDS-only)
       }
+      TP(0);  // producer: clear + stage + prefetch issue
       lds_barrier();
+      TP(1);  // producer: waiting for the consumers
     }
+    TP_STORE_BY(0);
   } else if (wave == 1) {
     tile_consumer<NT, 0>(d, t, cp, ntl, nbatch, Ys, Lw, Bs, tid);
   } else if (wave == 2) {
@@ -1736,9 +1754,12 @@ __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double
 // the producer / consumer kernel for classes up to 8 tiles wide (the
 // 9-wide class keeps k_rcs_tile: 15 accumulator tiles per consumer wave would
 // not fit its 3 waves per SIMD)
+#ifndef SQLM_TILE_PROD_MAXNT
+#define SQLM_TILE_PROD_MAXNT 8
+#endif
 template <int NTT>
 void launch_tile_p(int cnt, hipStream_t S, const DevProblem &d, double lambda, int off) {
-  if constexpr (NTT <= 8)
+  if constexpr (NTT <= SQLM_TILE_PROD_MAXNT)
     hipLaunchKernelGGL((k_rcs_tile_p<NTT>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);
   else
     hipLaunchKernelGGL((k_rcs_tile<NTT, false>), dim3(cnt), dim3(kTileThreads), 0, S, d, lambda, off);
@@ -1985,10 +2006,25 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool
 #ifndef SQLM_UPD_OCC_MONO
 #define SQLM_UPD_OCC_MONO 4
 #endif
+// The observations a lane streams after its kObsPreload preloaded ones are
+// read twice, by the back substitution and then by the trial evaluation /
+// speculative linearization; a tile's inputs do not stay in L2 in between
+// (the re-reads were ~100 MB of the pass's 342 MB, profiles/r05/pmc_gba.json).
+// The first pass parks the first kUpdCache of them in LDS (camera + the f32
+// measurement, as loaded: the same doubles come back) for the second.
+constexpr int kUpdCache = 3;
+#ifndef SQLM_UPD_CACHE  // A/B: -DSQLM_UPD_CACHE=0 reads them twice
+#define SQLM_UPD_CACHE 1
+#endif
+struct UpdCache {
+  int cam[kUpdCache][kBlock];
+  float4 q[kUpdCache][kBlock];
+};
 template <int W, bool ST, bool SPEC, bool FUSE>
 __device__ __forceinline__ void landmark_update_body(const DevProblem &d, int slot_begin, int slot_end, double lambda,
                                                     int part_off, const int2 *rng, int nlm_blocks, int bid,
-                                                    double *red, double *Wp0, double *Wp1, double *Wdx) {
+                                                    double *red, double *Wp0, double *Wp1, double *Wdx,
+                                                    UpdCache *oc) {
   constexpr bool fuse_pose = FUSE;
   if (fuse_pose && bid >= nlm_blocks) {  // k_pose_update<true>
     const int pb = bid - nlm_blocks;
@@ -2069,7 +2105,44 @@ __device__ __forceinline__ void landmark_update_body(const DevProblem &d, int sl
     };
 #pragma unroll
     for (int i = 0; i < kObsPreload; ++i) hlp_dx(o[i]);  // camh = -1 for lanes past the track
-    for (int e = beg + lane + kObsPreload * W; e < end; e += W) hlp_dx(load_obs<ST, true>(d, e, true));
+    // (mono, f32 measurements: the streamed ones are parked for the second pass)
+    const bool park = SQLM_UPD_CACHE && !ST && oc != nullptr && d.obs_f32;
+    {
+      int j = 0;
+      for (int e = beg + lane + kObsPreload * W; e < end; e += W, ++j) {
+        if (park && j < kUpdCache) {  // the raw inputs straight into the cache, then only what hlp_dx reads
+          const int cam = d.obs_cam[e];
+          oc->cam[j][threadIdx.x] = cam;
+          oc->q[j][threadIdx.x] = *reinterpret_cast<const float4 *>(d.obs_q + 4 * (int64_t)e);
+          ObsIn oi{cam, d.obs_camh[e], 0.0, 0.0, 0.0, 0.0, -1.0, d.obs_s[e]};
+          hlp_dx(oi);
+        } else {
+          hlp_dx(load_obs<ST, true>(d, e, true));
+        }
+      }
+    }
+    // a parked observation for the second pass (j < kUpdCache)
+    auto parked = [&](int j) {
+      ObsIn oi{0, -1, 0.0, 0.0, 0.0, 0.0, -1.0, 0.0};
+      oi.cam = oc->cam[j][threadIdx.x];
+      const float4 q = oc->q[j][threadIdx.x];
+      oi.u = q.x;
+      oi.v = q.y;
+      oi.info = q.z;
+      oi.delta = q.w;
+      return oi;
+    };
+    // the second pass over the streamed observations: the parked ones from LDS
+    // (a loop of their own: one loop choosing per observation spilled), then
+    // any further ones loaded again
+    auto stream2 = [&](auto &&use) {
+      int e = beg + lane + kObsPreload * W;
+      if (park) {
+#pragma unroll 1
+        for (int j = 0; j < kUpdCache && e < end; ++j, e += W) use(parked(j), e);
+      }
+      for (; e < end; e += W) use(load_obs<ST, true>(d, e, true), e);
+    };
     a0 = seg_sum<W>(a0); a1 = seg_sum<W>(a1); a2 = seg_sum<W>(a2);
     double chi = 0.0;
     double R[6] = {0, 0, 0, 0, 0, 0};  // SPEC: QR of the landmark's rows at the trial state
@@ -2096,9 +2169,9 @@ __device__ __forceinline__ void landmark_update_body(const DevProblem &d, int sl
           const int e = beg + lane + i * W;
           if (e < end) lin_edge<ST>(d, o[i], e, P1, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
         }
-        for (int e = beg + lane + kObsPreload * W; e < end; e += W)
-          lin_edge<ST>(d, load_obs<ST, true>(d, e, true), e, P1, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2,
-                       g0, g1, g2, chi);
+        stream2([&](const ObsIn &oi, int e) {
+          lin_edge<ST>(d, oi, e, P1, X0, X1, X2, d.obs_s_nx, false, R, b0, b1, b2, g0, g1, g2, chi);
+        });
       } else {
         auto trial_err = [&](const ObsIn &o, int e) {
           MonoEval m;
@@ -2112,7 +2185,7 @@ __device__ __forceinline__ void landmark_update_body(const DevProblem &d, int sl
 #pragma unroll
         for (int i = 0; i < kObsPreload; ++i)
           if (beg + lane + i * W < end) trial_err(o[i], beg + lane + i * W);
-        for (int e = beg + lane + kObsPreload * W; e < end; e += W) trial_err(load_obs<ST, true>(d, e, true), e);
+        stream2([&](const ObsIn &oi, int e) { trial_err(oi, e); });
       }
     }
     if (SPEC) {
@@ -2186,8 +2259,9 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
                                                          double lambda, int part_off, const int2 *rng, int nlm_blocks) {
   __shared__ double red[4];
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
+  __shared__ UpdCache oc;
   landmark_update_body<W, ST, SPEC, FUSE>(d, slot_begin, slot_end, lambda, part_off, rng, nlm_blocks, blockIdx.x, red,
-                                          Wp0, Wp1, Wdx);
+                                          Wp0, Wp1, Wdx, ST ? nullptr : &oc);
 }
 
 // Every bucket of a trial in one launch: the block range [blk0[b], blk0[b] +
@@ -2204,6 +2278,7 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
                                                                                                  UpdLaunch u) {
   __shared__ double red[4];
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
+  __shared__ UpdCache oc;
   const int bx = blockIdx.x;
   int b = 0;
 #pragma unroll
@@ -2214,7 +2289,7 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
 #define SQLM_UCASE(WW)                                                                                       \
   case WW:                                                                                                   \
     landmark_update_body<WW, ST, SPEC, false>(d, u.slot_begin[b], u.slot_end[b], lambda, u.part_off[b], rng, \
-                                              u.nblk[b], bid, red, Wp0, Wp1, Wdx);                           \
+                                              u.nblk[b], bid, red, Wp0, Wp1, Wdx, ST ? nullptr : &oc);       \
     break;
   switch (u.W[b]) {
     SQLM_UCASE(2) SQLM_UCASE(4) SQLM_UCASE(8) SQLM_UCASE(16) SQLM_UCASE(32) SQLM_UCASE(64)
