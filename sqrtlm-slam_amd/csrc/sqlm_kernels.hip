@@ -1317,25 +1317,54 @@ __global__ __launch_bounds__(kTileThreads, ST ? 2 : tile_occ<NT>()) void k_rcs_t
 // (only its owner wave changes) and the gradient code is the same: the
 // partials are bitwise identical to k_rcs_tile's.
 constexpr int kTileCons = kTileWaves - 1;  // consumer waves
+// Wide classes (NT >= 8) one K step at a time (its NT operand tiles in
+// registers, then every owned pair of the span): each accumulator still adds
+// its K steps in order, so the sums are the same bits as k_rcs_tile's, with a
+// third of the operand registers (NT = 8: 155 -> 124 VGPRs, 4 waves per SIMD;
+// NT = 9 fits 3). The narrow classes keep all operands loaded at once (the
+// stepped form of NT = 4 spilled).
+#ifndef SQLM_TILE_KS_STEP_MIN
+#define SQLM_TILE_KS_STEP_MIN 8
+#endif
 template <int NT, int P, int NC>
 __device__ __forceinline__ void tile_mfma_cons(d4v *acc, const double (*Y)[NC], int tmin, int tmax, int nks, int r16,
                                                int k4) {
-  double op[NT][kTileKS];
+  if constexpr (NT >= SQLM_TILE_KS_STEP_MIN) {
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
+  for (int ks = 0; ks < kTileKS; ++ks) {
+    if (ks < nks) {
+      double op[NT];
 #pragma unroll
-    for (int ks = 0; ks < kTileKS; ++ks) op[t][ks] = Y[4 * ks + k4][t * 16 + r16];
-  int q = 0;
+      for (int t = 0; t < NT; ++t) op[t] = Y[4 * ks + k4][t * 16 + r16];
+      int q = 0;
 #pragma unroll
-  for (int ti = 0; ti < NT; ++ti) {
+      for (int ti = 0; ti < NT; ++ti) {
 #pragma unroll
-    for (int tj = ti; tj < NT; ++tj, ++q) {
-      if (q % kTileCons == P && ti >= tmin && tj <= tmax) {
+        for (int tj = ti; tj < NT; ++tj, ++q) {
+          if (q % kTileCons == P && ti >= tmin && tj <= tmax)
+            acc[q / kTileCons] = __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti], op[tj], acc[q / kTileCons], 0, 0, 0);
+        }
+      }
+    }
+  }
+  } else {
+    double op[NT][kTileKS];
 #pragma unroll
-        for (int ks = 0; ks < kTileKS; ++ks)
-          if (ks < nks)
-            acc[q / kTileCons] =
-                __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti][ks], op[tj][ks], acc[q / kTileCons], 0, 0, 0);
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int ks = 0; ks < kTileKS; ++ks) op[t][ks] = Y[4 * ks + k4][t * 16 + r16];
+    int q = 0;
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
+#pragma unroll
+      for (int tj = ti; tj < NT; ++tj, ++q) {
+        if (q % kTileCons == P && ti >= tmin && tj <= tmax) {
+#pragma unroll
+          for (int ks = 0; ks < kTileKS; ++ks)
+            if (ks < nks)
+              acc[q / kTileCons] =
+                  __builtin_amdgcn_mfma_f64_16x16x4f64(op[ti][ks], op[tj][ks], acc[q / kTileCons], 0, 0, 0);
+        }
       }
     }
   }
@@ -1411,10 +1440,13 @@ __device__ __forceinline__ void tile_consumer(const DevProblem &d, int t, int cp
 }
 
 // waves per SIMD k_rcs_tile_p is compiled for: the consumer waves' registers
-// (NT = 8: 155 VGPRs, 6: 102) without spills
+// without spills (NT = 8: 124 VGPRs, 6: 84, 9: 150)
+#ifndef SQLM_TILE_P_OCC_MID
+#define SQLM_TILE_P_OCC_MID 4
+#endif
 template <int NT>
 constexpr int tile_p_occ() {
-  return NT <= 3 ? 5 : NT <= 6 ? 4 : NT <= 8 ? 3 : 2;
+  return NT <= 3 ? 5 : NT <= 8 ? SQLM_TILE_P_OCC_MID : 3;
 }
 template <int NT>
 __global__ __launch_bounds__(kTileThreads, tile_p_occ<NT>()) void k_rcs_tile_p(DevProblem d, double lambda, int cls_off) {
@@ -1755,7 +1787,7 @@ __global__ __launch_bounds__(kRedThreads) void k_rcs_reduce(DevProblem d, double
 // 9-wide class keeps k_rcs_tile: 15 accumulator tiles per consumer wave would
 // not fit its 3 waves per SIMD)
 #ifndef SQLM_TILE_PROD_MAXNT
-#define SQLM_TILE_PROD_MAXNT 8
+#define SQLM_TILE_PROD_MAXNT 9
 #endif
 template <int NTT>
 void launch_tile_p(int cnt, hipStream_t S, const DevProblem &d, double lambda, int off) {
