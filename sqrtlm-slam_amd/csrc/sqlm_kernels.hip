@@ -2291,9 +2291,10 @@ __global__ __launch_bounds__(256, ST ? SQLM_UPD_OCC : SQLM_UPD_OCC_MONO) void k_
                                                          double lambda, int part_off, const int2 *rng, int nlm_blocks) {
   __shared__ double red[4];
   __shared__ double Wp0[kUpdWin * 16], Wp1[kUpdWin * 16], Wdx[kUpdWin * 8];
-  __shared__ UpdCache oc;
+  // (no observation cache here: the per-bucket launches serve small problems,
+  // where it measured slower -- local BA 0.0143 -> 0.0152 ms, profiles/r06/)
   landmark_update_body<W, ST, SPEC, FUSE>(d, slot_begin, slot_end, lambda, part_off, rng, nlm_blocks, blockIdx.x, red,
-                                          Wp0, Wp1, Wdx, ST ? nullptr : &oc);
+                                          Wp0, Wp1, Wdx, nullptr);
 }
 
 // Every bucket of a trial in one launch: the block range [blk0[b], blk0[b] +
