@@ -37,7 +37,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # = 78.6 TFLOP/s, AMD's MI355X FP64-matrix figure. The guide has no f64 row.
 MFMA_F64_PEAK_TFLOPS = 78.6
 # committed PMC summaries, newest round first (pmc_traffic takes the first on the same workload)
-PROFILE_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r05", "r04", "r03", "r02", "r01")]
+PROFILE_DIRS = [os.path.join(ROOT, "profiles", r) for r in ("r06", "r05", "r04", "r03", "r02", "r01")]
 
 
 def make_workload(name: str, scale: float):
