@@ -2044,7 +2044,12 @@ void launch_pose_update(const DevProblem &d, double lambda, hipStream_t st, bool
 // (the re-reads were ~100 MB of the pass's 342 MB, profiles/r05/pmc_gba.json).
 // The first pass parks the first kUpdCache of them in LDS (camera + the f32
 // measurement, as loaded: the same doubles come back) for the second.
-constexpr int kUpdCache = 3;
+// Depth 3 measured best: 1 / 2 / 4 entries (6 / 5 / 3 workgroups per CU by
+// LDS) gave 0.155 / 0.153 / 0.156 ms against 0.150 (profiles/r06/ab_upd_cache_depth.log).
+#ifndef SQLM_UPD_NCACHE
+#define SQLM_UPD_NCACHE 3
+#endif
+constexpr int kUpdCache = SQLM_UPD_NCACHE;
 #ifndef SQLM_UPD_CACHE  // A/B: -DSQLM_UPD_CACHE=0 reads them twice
 #define SQLM_UPD_CACHE 1
 #endif
