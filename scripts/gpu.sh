@@ -59,6 +59,19 @@ ab)
   done
   cat $out
   ;;
+e2e)
+  # drop-in GBA call timing per library (setup phases on stderr), interleaved
+  out=gpurun_out/e2e_${E2E_TAG:-ab}.log
+  : > $out
+  for r in $(seq 1 ${REPS:-2}); do
+    for lib in "$@"; do
+      echo "== $lib" >> $out
+      SQLM_LIB_PATH=$PWD/sqrtlm-slam_amd/sqrtlm/$lib SQLM_PREP_TIMING=1 REPS=4 \
+        timeout -k 10 300 python -u scripts/e2e_timing.py >> $out 2>&1 || { tail -20 $out; exit 1; }
+    done
+  done
+  grep -E "^==|^rep|median|obs\+camcsr|active\+sort" $out
+  ;;
 bits)
   timeout -k 10 400 python -u scripts/ab_bits.py "$@" > gpurun_out/ab_bits.log 2>&1 || { tail -20 gpurun_out/ab_bits.log; exit 1; }
   tail -20 gpurun_out/ab_bits.log

@@ -18,6 +18,7 @@
 #include <new>
 #include <queue>
 #include <thread>
+#include <sys/mman.h>
 #include <unistd.h>
 #include <vector>
 
@@ -34,7 +35,53 @@ namespace {
 struct DevBuf {
   void *p = nullptr;
   size_t cap = 0;
+  size_t map = 0;  // page-locked buffers: mapped length of a registered huge-page mapping (0: hipHostMalloc)
 };
+
+// Large host arrays on transparent huge pages. The setup's scatter and
+// planning passes read 5M-edge arrays at random landmark runs and write the
+// page-locked upload buffers; with 4 KiB pages nearly every run costs TLB
+// misses. MADV_HUGEPAGE is set before the first touch (the box's THP mode is
+// "madvise"); arrays under one huge page use malloc. (SQLM_HOST_HUGE=0: A/B.)
+#ifndef SQLM_HOST_HUGE
+#define SQLM_HOST_HUGE 1
+#endif
+constexpr size_t kHugePage = size_t(2) << 20;
+inline size_t huge_len(size_t bytes) { return (bytes + kHugePage - 1) & ~(kHugePage - 1); }
+// an anonymous mapping of huge_len(bytes), aligned to a huge page, advised; nullptr on failure
+inline void *huge_map(size_t bytes) {
+  const size_t len = huge_len(bytes);
+  void *raw = mmap(nullptr, len + kHugePage, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (raw == MAP_FAILED) return nullptr;
+  const uintptr_t r = (uintptr_t)raw, a = (r + kHugePage - 1) & ~(uintptr_t)(kHugePage - 1);
+  if (a > r) munmap(raw, a - r);
+  if (r + kHugePage > a) munmap((void *)(a + len), r + kHugePage - a);
+  (void)madvise((void *)a, len, MADV_HUGEPAGE);
+  return (void *)a;
+}
+template <class T>
+struct HugeAlloc {
+  using value_type = T;
+  HugeAlloc() = default;
+  template <class U>
+  HugeAlloc(const HugeAlloc<U> &) {}
+  static bool huge(size_t n) { return SQLM_HOST_HUGE && n * sizeof(T) >= kHugePage; }
+  T *allocate(size_t n) {
+    void *p = huge(n) ? huge_map(n * sizeof(T)) : std::malloc(std::max<size_t>(n, 1) * sizeof(T));
+    if (!p) throw std::bad_alloc();
+    return static_cast<T *>(p);
+  }
+  void deallocate(T *p, size_t n) {
+    if (huge(n)) munmap(p, huge_len(n * sizeof(T)));
+    else std::free(p);
+  }
+  template <class U>
+  bool operator==(const HugeAlloc<U> &) const { return true; }
+  template <class U>
+  bool operator!=(const HugeAlloc<U> &) const { return false; }
+};
+template <class T>
+using HVec = std::vector<T, HugeAlloc<T>>;
 
 struct Timer {
   std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
@@ -104,9 +151,9 @@ struct sqlm_ctx {
   int64_t n_obs = 0, n_lid = 0;
   std::vector<double> pose_q, pose_t, intr, pt;
   std::vector<uint8_t> pose_fixed;
-  std::vector<int32_t> obs_pose, obs_pt;
-  std::vector<double> obs_uv, obs_info, obs_delta, obs_err;
-  std::vector<uint8_t> obs_level;
+  HVec<int32_t> obs_pose, obs_pt;
+  HVec<double> obs_uv, obs_info, obs_delta, obs_err;
+  HVec<uint8_t> obs_level;
   bool has_stereo = false;           // some edge is an EdgeStereoSE3ProjectXYZ
   std::vector<double> obs_ur, pose_bf, obs_err3;
   std::vector<int32_t> lid_pose;
@@ -119,7 +166,7 @@ struct sqlm_ctx {
   UpdLaunch upd;  // every bucket's landmark update in one launch (nb = 0: per bucket)
   int n_lm_parts = 0;
   std::vector<int> slot_pt;          // device slot -> point id
-  std::vector<int64_t> dev_edge;     // device obs -> edge id
+  HVec<int64_t> dev_edge;            // device obs -> edge id
   std::vector<int64_t> dev_lid_edge; // device lidar -> lidar edge id
   int max_row_blocks = 0;
   int n_active_edges = 0;
@@ -238,17 +285,41 @@ struct PinVec {
   T *end() const { return p + n; }
 };
 
+inline void free_pinned(DevBuf &b) {
+  if (b.p && b.map) {
+    (void)hipHostUnregister(b.p);
+    munmap(b.p, b.map);
+  } else if (b.p) {
+    (void)hipHostFree(b.p);
+  }
+  b.p = nullptr;
+  b.cap = b.map = 0;
+}
+
 template <class T>
 int pinned(sqlm_ctx *c, int idx, size_t n, PinVec<T> &out) {
   if ((int)c->pins.size() <= idx) c->pins.resize(idx + 1);
   DevBuf &b = c->pins[idx];
   const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
   if (b.cap < bytes) {
-    if (b.p) (void)hipHostFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) return SQLM_ERR_OOM;
-    b.cap = bytes;
+    free_pinned(b);
+    // large arrays: a huge-page mapping, touched, then page-locked for the DMA
+    if (SQLM_HOST_HUGE && bytes >= kHugePage) {
+      if (void *p = huge_map(bytes)) {
+        std::memset(p, 0, huge_len(bytes));
+        if (hipHostRegister(p, huge_len(bytes), hipHostRegisterDefault) == hipSuccess) {
+          b.p = p;
+          b.cap = bytes;
+          b.map = huge_len(bytes);
+        } else {
+          munmap(p, huge_len(bytes));
+        }
+      }
+    }
+    if (!b.p) {
+      if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) return SQLM_ERR_OOM;
+      b.cap = bytes;
+    }
   }
   out.p = static_cast<T *>(b.p);
   out.n = n;
@@ -387,8 +458,8 @@ inline int host_threads(int64_t work) {
 }
 
 // v <- src[0 .. n) on host threads (the caller's arrays are copied in: ABI)
-template <class T>
-void par_assign(std::vector<T> &v, const T *src, size_t n) {
+template <class T, class A>
+void par_assign(std::vector<T, A> &v, const T *src, size_t n) {
   v.resize(n);  // same size as the last call: no fill
   const int nth = host_threads((int64_t)n);
   run_threads(nth, [&](int t) {
@@ -836,6 +907,17 @@ inline bool stopped(const volatile uint8_t *s) { return s && *s; }
 // camera CSR and the upper block pattern of the reduced camera system.
 int fetch_errors(sqlm_ctx *c);
 
+// setup passes (A/B builds: =0 keeps the previous form)
+#ifndef SQLM_ACTIVE_FAST
+#define SQLM_ACTIVE_FAST 1
+#endif
+#ifndef SQLM_SCATTER_BY_SLOT
+#define SQLM_SCATTER_BY_SLOT 1
+#endif
+#ifndef SQLM_SCATTER_PF
+#define SQLM_SCATTER_PF 8
+#endif
+
 int prepare(sqlm_ctx *c, int level) {
   DevProblem &d = c->d;
   // edges outside this call's level keep their last error (g2o semantics):
@@ -864,18 +946,51 @@ int prepare(sqlm_ctx *c, int level) {
   fill_par(span_hi, (size_t)c->n_pt, -1);
   fill_par(efirst, (size_t)c->n_pt, std::numeric_limits<int>::max());
   fill_par(elast, (size_t)c->n_pt, -1);
+  phase("  fills");
   int64_t n_ae = 0;
-  {  // active set, track lengths and camera spans in one pass on host threads (relaxed atomics)
+  // active set, track lengths and camera spans in one pass on host threads.
+  // Fast pass: the chunks start at landmark changes, and a landmark's edges
+  // are one run (g2o adds a point's edges together, g2oOptimizer.cc:213-281),
+  // so a run's results are stored plainly; one atomic exchange per run on
+  // pt_act finds a landmark met twice, and then the pass is redone with
+  // relaxed atomics for every field.
+  for (int pass = SQLM_ACTIVE_FAST ? 0 : 1; pass < 2; ++pass) {
+    if (pass == 1 && SQLM_ACTIVE_FAST) {
+      fill_par(pt_act, (size_t)c->n_pt, (uint8_t)0);
+      fill_par(kcount, (size_t)c->n_pt, 0);
+      fill_par(span_lo, (size_t)c->n_pt, std::numeric_limits<int>::max());
+      fill_par(span_hi, (size_t)c->n_pt, -1);
+      fill_par(efirst, (size_t)c->n_pt, std::numeric_limits<int>::max());
+      fill_par(elast, (size_t)c->n_pt, -1);
+    }
+    const bool fast = pass == 0;
     const int nth = host_threads(c->n_obs);
-    std::vector<int64_t> cnt(nth, 0);
+    std::vector<int64_t> cnt(nth, 0), cut(nth + 1, c->n_obs);
+    std::vector<uint8_t> dup(nth, 0);
+    for (int t = 0; t < nth; ++t) {  // chunk starts moved forward to a change of landmark
+      int64_t e = c->n_obs * t / nth;
+      if (fast && t > 0)
+        while (e < c->n_obs && e > 0 && c->obs_pt[e] == c->obs_pt[e - 1]) ++e;
+      cut[t] = std::max(e, t > 0 ? cut[t - 1] : (int64_t)0);
+    }
     run_threads(nth, [&](int t) {
-      const int64_t e0 = c->n_obs * t / nth, e1 = c->n_obs * (t + 1) / nth;
+      const int64_t e0 = cut[t], e1 = cut[t + 1];
       int64_t n = 0;
+      bool seen_twice = false;
       // runs of one landmark (the reference adds a point's edges together,
       // g2oOptimizer.cc:213-281) are folded locally: one set of atomics per run
       int rl = -1, rk = 0, rlo = 0, rhi = 0, rf = 0, rla = 0;
       auto flush = [&] {
         if (rl < 0) return;
+        if (fast && nth > 1) {  // the landmark's only run (checked): plain stores
+          seen_twice |= __atomic_exchange_n(&pt_act[rl], (uint8_t)1, __ATOMIC_RELAXED) != 0;
+          kcount[rl] = rk;
+          span_lo[rl] = rlo;
+          span_hi[rl] = rhi;
+          efirst[rl] = rf;
+          elast[rl] = rla;
+          return;
+        }
         if (nth == 1) {  // one thread (a local-BA window): plain updates (the min / max atomics are CAS loops)
           pt_act[rl] = 1;
           kcount[rl] += rk;
@@ -911,9 +1026,13 @@ int prepare(sqlm_ctx *c, int level) {
       }
       flush();
       cnt[t] = n;
+      dup[t] = seen_twice;
     });
+    if (std::find(dup.begin(), dup.end(), 1) != dup.end()) continue;  // a landmark in two runs: the atomic pass
     for (int64_t v : cnt) n_ae += v;
+    break;
   }
+  phase("  active pass");
   std::vector<int64_t> lid_act;
   const bool sharded = c->comm.enabled();
   for (int64_t e = 0; e < c->n_lid; ++e) {
@@ -932,6 +1051,7 @@ int prepare(sqlm_ctx *c, int level) {
     if (pose_act[p] && !c->pose_fixed[p]) { phidx[p] = (int)hidxp.size(); hidxp.push_back(p); }
   const int nP = (int)hidxp.size();
   if (nP > kMaxFreePoses) return SQLM_ERR_UNSUPPORTED;
+  phase("  lidar+poses");
   // landmark slots: bucket by segment width; inside a bucket by camera span
   // (first, last observing pose, then id), so a batch of consecutive slots in
   // the RCS tiles shares nearly one span (dense MFMA panels)
@@ -996,6 +1116,7 @@ int prepare(sqlm_ctx *c, int level) {
     for (int s = (int)((int64_t)nL * t / nks); s < (int)((int64_t)nL * (t + 1) / nks); ++s) pt_slot[pts[s]] = s;
   });
   c->slot_pt = pts;
+  phase("  pt_slot");
   c->buckets.clear();
   c->upd = UpdLaunch{};
   c->bucket_part_off.clear();
@@ -1023,6 +1144,7 @@ int prepare(sqlm_ctx *c, int level) {
     s = e;
   }
   if (c->n_lm_parts > 16384) return SQLM_ERR_UNSUPPORTED;
+  phase("  buckets");
   // observations in slot order (edge-id order inside a landmark): offsets by a
   // two-pass prefix over slot chunks
   std::vector<int> lm_begin(nL + 1, 0);
@@ -1045,6 +1167,7 @@ int prepare(sqlm_ctx *c, int level) {
   }
   const int64_t nE = lm_begin[nL];
   if (nE > (int64_t)std::numeric_limits<int>::max()) return SQLM_ERR_UNSUPPORTED;
+  phase("  lm_begin");
   c->dev_edge.resize(nE);  // every entry is written by the scatter below
   PinVec<int> obs_lm, obs_cam, obs_camh;
   PinVec<double> obs_uv, obs_info, obs_delta, obs_ur;
@@ -1056,6 +1179,7 @@ int prepare(sqlm_ctx *c, int level) {
         (e = pinned(c, P_OBSUR, c->has_stereo ? nE : 0, obs_ur)))
       return e;
   }
+  phase("  pinned");
   // Stable scatter of the observations into slot order on a few host threads
   // (edge-id order inside a landmark). When every landmark's active edges are
   // one contiguous run of edge ids -- g2o's graphs add a point's edges together
@@ -1091,7 +1215,31 @@ int prepare(sqlm_ctx *c, int level) {
     });
     contig = std::find(split.begin(), split.end(), 1) == split.end();
   }
-  if (contig) {  // edge order (streaming reads): edge e of landmark l goes to its slot's base + (e - first edge)
+  phase("  contig check");
+  if (contig && SQLM_SCATTER_BY_SLOT) {
+    // slot order: the outputs are written front to back (whole cache lines)
+    // and each landmark's inputs are one run of edge ids
+    par([&](int t) {
+      bool bad = false;
+      const int s1 = (int)((int64_t)nL * (t + 1) / nth);
+      for (int sl = (int)((int64_t)nL * t / nth); sl < s1; ++sl) {
+        // the inputs of the landmarks kPf slots ahead (their edge runs sit at
+        // random places of the edge arrays), and the run starts 2 kPf ahead
+        if (SQLM_SCATTER_PF > 0 && sl + 2 * SQLM_SCATTER_PF < s1) __builtin_prefetch(&efirst[pts[sl + 2 * SQLM_SCATTER_PF]]);
+        if (SQLM_SCATTER_PF > 0 && sl + SQLM_SCATTER_PF < s1) {
+          const int64_t ep = efirst[pts[sl + SQLM_SCATTER_PF]];
+          __builtin_prefetch(&c->obs_uv[2 * ep]);
+          __builtin_prefetch(&c->obs_info[ep]);
+          __builtin_prefetch(&c->obs_delta[ep]);
+          __builtin_prefetch(&c->obs_pose[ep]);
+        }
+        const int b = lm_begin[sl], k = lm_begin[sl + 1] - b;
+        const int64_t e0 = efirst[pts[sl]];
+        for (int i = 0; i < k; ++i) put(e0 + i, b + i, sl, bad);
+      }
+      inexact[t] = bad;
+    });
+  } else if (contig) {  // edge order (streaming reads): edge e of landmark l goes to its slot's base + (e - first edge)
     par([&](int t) {
       bool bad = false;
       for (int64_t e = c->n_obs * t / nth; e < c->n_obs * (t + 1) / nth; ++e) {
@@ -1129,6 +1277,7 @@ int prepare(sqlm_ctx *c, int level) {
       inexact[t] = bad;
     });
   }
+  phase("  scatter");
   // inputs that are not all float32 values: the double arrays, from the same slot order
   const bool obs_f32 = std::find(inexact.begin(), inexact.end(), 1) == inexact.end();
   if (!obs_f32) {
@@ -1182,6 +1331,7 @@ int prepare(sqlm_ctx *c, int level) {
     });
     for (int64_t k : cnt) n_cam_obs += k;
   }
+  phase("  camh count");
   {  // the observation arrays go to the device now, overlapped with the rest of the setup
     int e = 0;
     if ((e = upload(c, B_OBSLM, obs_lm, &d.obs_lm)) || (e = upload(c, B_OBSCAM, obs_cam, &d.obs_cam)) ||
@@ -2272,8 +2422,7 @@ int sqlm_ctx_destroy(sqlm_ctx *c) {
   if (c->orb) orb_destroy(c->orb);
   for (auto &b : c->bufs)
     if (b.p) (void)hipFree(b.p);
-  for (auto &b : c->pins)
-    if (b.p) (void)hipHostFree(b.p);
+  for (auto &b : c->pins) free_pinned(b);
   for (auto &e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
