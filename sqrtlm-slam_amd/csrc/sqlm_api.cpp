@@ -168,6 +168,7 @@ struct sqlm_ctx {
   std::vector<int> slot_pt;          // device slot -> point id
   HVec<int64_t> dev_edge;            // device obs -> edge id
   std::vector<int64_t> dev_lid_edge; // device lidar -> lidar edge id
+  std::vector<int> h_btot;           // setup: landmark-slot bucket totals
   int max_row_blocks = 0;
   int n_active_edges = 0;
   CRPlan cr;
@@ -1076,10 +1077,31 @@ int prepare(sqlm_ctx *c, int level) {
         if (key[l] >= 0) ++h[key[l]];
       }
     });
-    for (int64_t b = 0, run = 0; b < nb; ++b) {
-      bcnt[b] = (int)run;
-      for (int t = 0; t < nk; ++t) { const int k = hist[t][b]; hist[t][b] = (int)run; run += k; }
-      bcnt[b + 1] = (int)run;
+    // bucket totals over the chunks, the bucket bases, then every chunk's base
+    // inside each bucket (bucket ranges on host threads; one serial pass over
+    // nb instead of nb x chunks)
+    {
+      std::vector<int> &btot = c->h_btot;
+      btot.resize(nb);
+      run_threads(nk, [&](int t) {
+        for (int64_t b = nb * t / nk; b < nb * (t + 1) / nk; ++b) {
+          int k = 0;
+          for (int u = 0; u < nk; ++u) k += hist[u][b];
+          btot[b] = k;
+        }
+      });
+      int64_t run = 0;
+      for (int64_t b = 0; b < nb; ++b) {
+        bcnt[b] = (int)run;
+        run += btot[b];
+      }
+      bcnt[nb] = (int)run;
+      run_threads(nk, [&](int t) {
+        for (int64_t b = nb * t / nk; b < nb * (t + 1) / nk; ++b) {
+          int r = bcnt[b];
+          for (int u = 0; u < nk; ++u) { const int k = hist[u][b]; hist[u][b] = r; r += k; }
+        }
+      });
     }
     pts.resize(bcnt[nb]);
     run_threads(nk, [&](int t) {
