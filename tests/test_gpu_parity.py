@@ -263,3 +263,31 @@ def test_nan_measurement(gpu_ctx, oracle, robust):
     q, t = gpu_ctx.poses()
     np.testing.assert_array_equal(q, prob.pose_q)
     np.testing.assert_array_equal(gpu_ctx.points(), prob.pt)
+
+
+@pytest.mark.parametrize("order", ["shuffled", "two_runs"])
+def test_edge_order(gpu_ctx, oracle, order):
+    """Edges of a landmark that are not one run of edge ids (a caller adding
+    them in another order than g2oOptimizer.cc:213-281): the setup's active-set
+    pass meets a landmark twice and reruns with atomics, and the observation
+    scatter takes the chunked counting path instead of the slot-order copy.
+    300k edges, so the host passes run on more than one thread. Parity with
+    the oracle on the same edge order; per-edge chi2 in caller order."""
+    prob = synth.config4(scale=0.06, seed=7)
+    E = prob.n_obs
+    if order == "shuffled":
+        perm = np.random.default_rng(7).permutation(E)
+    else:  # every other edge moved behind all the rest: each track in two runs
+        perm = np.concatenate([np.arange(0, E, 2), np.arange(1, E, 2)])
+    p2 = prob.copy()
+    for f in ("obs_pose", "obs_pt", "obs_uv", "obs_info", "obs_delta", "obs_level"):
+        setattr(p2, f, np.ascontiguousarray(getattr(prob, f)[perm]))
+    assert np.count_nonzero(np.diff(p2.obs_pt)) + 1 > prob.n_pt  # landmarks in several runs
+    ref = oracle.OracleGraph(p2)
+    nr, sr = ref.global_ba(5)
+    gpu_ctx.set_problem(p2)
+    ng, sg = gpu_ctx.global_ba(5)
+    assert ng == nr
+    _compare_stats(sg, sr)
+    _compare_state(gpu_ctx, ref)
+    np.testing.assert_allclose(gpu_ctx.edge_chi2(), ref.edge_chi2(), rtol=1e-6, atol=1e-9)
