@@ -1,0 +1,61 @@
+"""A seeded sweep of problem shapes, HIP path vs the CPU oracle (g2o
+semantics), beside the hand-picked cases of test_gpu_parity.py: keyframe
+counts from a handful to a few hundred, short and long tracks, local-BA pair
+layouts, many or few fixed keyframes, robust or plain, an occasional loop
+closure. Each shape lands on a different mix of RCS tile classes, cyclic-
+reduction level counts / superblock widths, band + border or dense layouts.
+The bar is the north-star one: poses / points within 1e-6 of the oracle,
+identical iteration counts, trial counts and chi2 / lambda traces.
+
+The shapes are drawn once from a fixed seed (listed by pytest), so a failure
+names a reproducible case.
+"""
+import numpy as np
+import pytest
+
+from sqrtlm import synth
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-6
+
+
+def _shapes(n=48, seed=2026):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        kind = ["track", "track", "pairs", "loop"][i % 4]
+        n_kf = int(rng.integers(6, 300 if kind != "loop" else 120))
+        kw = dict(seed=1000 + i, robust=bool(rng.integers(0, 2)), n_fixed=int(rng.integers(1, max(2, n_kf // 4))))
+        if kind == "pairs":
+            kw["pair_window"] = int(rng.integers(2, 8))
+            n_lm = int(rng.integers(20, 60)) * n_kf
+        else:
+            k_min = int(rng.integers(2, 5))
+            kw["k_min"], kw["k_max"] = k_min, int(rng.integers(k_min, min(18, n_kf) + 1))
+            n_lm = int(rng.integers(10, 80)) * n_kf
+            if kind == "loop":
+                kw["loop"] = int(rng.integers(3, max(4, n_kf // 4)))
+        out.append((i, kind, n_kf, n_lm, kw))
+    return out
+
+
+@pytest.mark.parametrize("case", _shapes(), ids=lambda c: f"{c[0]}-{c[1]}-kf{c[2]}-lm{c[3]}")
+def test_shape_sweep(gpu_ctx, oracle, case):
+    _, _, n_kf, n_lm, kw = case
+    prob = synth.make_problem(n_kf, n_lm, **kw)
+    ref = oracle.OracleGraph(prob)
+    nr, sr = ref.optimize(0, 8)
+    gpu_ctx.set_problem(prob)
+    ng, sg = gpu_ctx.optimize(0, 8)
+    assert ng == nr
+    assert sg["iterations"] == sr["iterations"]
+    assert sg["trace_trials"] == sr["trace_trials"]
+    np.testing.assert_allclose(sg["trace_chi2"], sr["trace_chi2"], rtol=TOL)
+    np.testing.assert_allclose(sg["trace_lambda"], sr["trace_lambda"], rtol=TOL)
+    q, t = gpu_ctx.poses()
+    X = gpu_ctx.points()
+    assert np.abs(q - ref.pose_q).max() < TOL
+    assert np.abs(t - ref.pose_t).max() / max(1.0, np.abs(ref.pose_t).max()) < TOL
+    assert np.abs(X - ref.pt).max() / max(1.0, np.abs(ref.pt).max()) < TOL
+    np.testing.assert_allclose(gpu_ctx.edge_chi2(), ref.edge_chi2(), rtol=1e-6, atol=1e-9)
