@@ -12,9 +12,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "sqrtlm-slam_amd"), os.path.join(ROOT, "tests")]
 from oracle import oracle as O  # noqa: E402  (the checker)
-from sqrtlm import synth  # noqa: E402
 from sqrtlm.optimizer import Context  # noqa: E402
-from test_gpu_sweep import _shapes  # noqa: E402
+from test_gpu_sweep import _shapes, make  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 seed = int(sys.argv[2]) if len(sys.argv) > 2 else 7
@@ -23,7 +22,7 @@ bad = 0
 t0 = time.time()
 with Context(0) as ctx:
     for i, kind, n_kf, n_lm, kw in _shapes(n, seed):
-        prob = synth.make_problem(n_kf, n_lm, **kw)
+        prob = make(n_kf, n_lm, kw)
         ref = O.OracleGraph(prob)
         nr, sr = ref.optimize(0, 8)
         ctx.set_problem(prob)

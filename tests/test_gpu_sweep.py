@@ -2,7 +2,8 @@
 semantics), beside the hand-picked cases of test_gpu_parity.py: keyframe
 counts from a handful to a few hundred, short and long tracks, local-BA pair
 layouts, many or few fixed keyframes, robust or plain, an occasional loop
-closure. Each shape lands on a different mix of RCS tile classes, cyclic-
+closure, stereo edges (every fifth shape) and LiDAR flat-point edges (every
+seventh). Each shape lands on a different mix of RCS tile classes, cyclic-
 reduction level counts / superblock widths, band + border or dense layouts.
 The bar is the north-star one: poses / points within 1e-6 of the oracle,
 identical iteration counts, trial counts and chi2 / lambda traces.
@@ -36,14 +37,33 @@ def _shapes(n=48, seed=2026):
             n_lm = int(rng.integers(10, 80)) * n_kf
             if kind == "loop":
                 kw["loop"] = int(rng.integers(3, max(4, n_kf // 4)))
-        out.append((i, kind, n_kf, n_lm, kw))
+        # every fifth shape with stereo edges (the 3-D error row, float invz),
+        # every seventh with LiDAR flat-point edges on one free keyframe
+        extra = {}
+        if i % 5 == 4:
+            extra["stereo"] = float(rng.uniform(0.2, 0.9))
+        if i % 7 == 6:
+            extra["lidar"] = int(rng.integers(20, 200))
+        out.append((i, kind, n_kf, n_lm, dict(kw, **({"_extra": extra} if extra else {}))))
     return out
 
 
-@pytest.mark.parametrize("case", _shapes(), ids=lambda c: f"{c[0]}-{c[1]}-kf{c[2]}-lm{c[3]}")
+def make(n_kf, n_lm, kw):
+    """The problem of one shape (synth.make_problem + the optional edges)."""
+    kw = dict(kw)
+    extra = kw.pop("_extra", {})
+    prob = synth.make_problem(n_kf, n_lm, **kw)
+    if "stereo" in extra:
+        synth.add_stereo(prob, extra["stereo"], seed=kw["seed"])
+    if "lidar" in extra:
+        synth.add_lidar_flat(prob, n_kf - 1, extra["lidar"], seed=kw["seed"])
+    return prob
+
+
+@pytest.mark.parametrize("case", _shapes(), ids=lambda c: f"{c[0]}-{c[1]}-kf{c[2]}-lm{c[3]}" + "".join("-" + k for k in c[4].get("_extra", {})))
 def test_shape_sweep(gpu_ctx, oracle, case):
     _, _, n_kf, n_lm, kw = case
-    prob = synth.make_problem(n_kf, n_lm, **kw)
+    prob = make(n_kf, n_lm, kw)
     ref = oracle.OracleGraph(prob)
     nr, sr = ref.optimize(0, 8)
     gpu_ctx.set_problem(prob)
@@ -58,4 +78,10 @@ def test_shape_sweep(gpu_ctx, oracle, case):
     assert np.abs(q - ref.pose_q).max() < TOL
     assert np.abs(t - ref.pose_t).max() / max(1.0, np.abs(ref.pose_t).max()) < TOL
     assert np.abs(X - ref.pt).max() / max(1.0, np.abs(ref.pt).max()) < TOL
-    np.testing.assert_allclose(gpu_ctx.edge_chi2(), ref.edge_chi2(), rtol=1e-6, atol=1e-9)
+    # per-edge chi2 of well-fit edges moves with the state's last digits
+    # (a 0.1 px residual of a 500 px projection: 5e3 x the state's relative
+    # difference); with LiDAR flat-point edges (central-difference Jacobians,
+    # delta 1e-9: the documented 1-ulp sensitivity, test_gpu_parity.py
+    # TRACE_TOL) the states agree to ~1e-9, so their edge chi2 to ~1e-5
+    lidar = "lidar" in kw.get("_extra", {})
+    np.testing.assert_allclose(gpu_ctx.edge_chi2(), ref.edge_chi2(), rtol=1e-3 if lidar else 1e-6, atol=1e-9)
