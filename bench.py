@@ -635,8 +635,9 @@ def run_ba(args, world, rank, local_rank, dist, config, cpu_iters=10, cpu_min_s=
                          "peak": MFMA_F64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ach_tf / MFMA_F64_PEAK_TFLOPS,
                          "traffic": traffic, "traffic_source": tsrc, "algorithmic_flops": flops,
                          "launch_ms": t_rcs,
-                         "note": "one RCS tile phase per trial = the width-class launches k_rcs_tile<8>, <6>, <9>, "
-                                 "<4> on three streams; launch_ms is the phase's wall time (HIP events on the "
+                         "note": "one RCS tile phase per trial = the width-class launches k_rcs_tile_p<8>, <6>, "
+                                 "<9>, <4> (producer / consumer kernel; k_rcs_tile for stereo or repeated cameras) "
+                                 "on three streams; launch_ms is the phase's wall time (HIP events on the "
                                  "context stream around the fork and join), rocprof lists the class kernels "
                                  "separately with overlapping durations"},
             "roofline_secondary": {"bound": "hbm", "kernel": f"{lin_kernel} (all buckets)", "achieved": achieved,
